@@ -1,0 +1,200 @@
+/*
+ * orx.h -- C-ABI of the MI355X batched Optimax Rogue tick engine (liborx.so).
+ *
+ * This is the drop-in boundary for the reference's per-tick updater.  Every
+ * entry point below replaces one reference interface; the citation after each
+ * declaration is the reference file:line (paths relative to the reference
+ * repository root, optimax_rogue @ v0).
+ *
+ * Conventions
+ *  - Plain pointers and sizes only; no C++ or torch types cross the boundary.
+ *  - Every device pointer is owned by the caller (PyTorch tensors in the Python
+ *    host layer); the library never allocates device memory.
+ *  - Calls are asynchronous on the caller's HIP stream (`stream`, a
+ *    hipStream_t passed as void*; NULL = the legacy default stream).  The
+ *    library is stateless and re-entrant; the caller selects the device.
+ *  - Return value: ORX_OK (0) or a negative error code; orx_last_error() gives
+ *    a thread-local message for the most recent failure on the calling thread.
+ *  - Randomness is Philox4x32-10 keyed by (seed) with the counter
+ *    (global game id, episode, tick-or-depth, purpose|block); global game id =
+ *    game_offset + local index, so results do not depend on how games are
+ *    sharded across GPUs.  The 32-bit words are consumed through the exact
+ *    CPython random._randbelow / numpy RandomState.randint transforms used at
+ *    the reference's draw sites ("Random streams").
+ */
+#ifndef ORX_H
+#define ORX_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ORX_ABI_VERSION 1
+
+/* ---- error codes -------------------------------------------------------- */
+#define ORX_OK 0
+#define ORX_EINVAL (-22) /* bad config, pointer, size or argument            */
+#define ORX_EIO (-5)     /* HIP runtime error (launch failure, bad stream)    */
+
+/* ---- enums: same integer values as the reference ------------------------ */
+/* Move            optimax_rogue/logic/moves.py:6-12                         */
+#define ORX_MOVE_UP 1
+#define ORX_MOVE_RIGHT 2
+#define ORX_MOVE_DOWN 3
+#define ORX_MOVE_LEFT 4
+#define ORX_MOVE_STAY 5
+/* UpdateResult    optimax_rogue/logic/updater.py:16-21                      */
+#define ORX_IN_PROGRESS 1
+#define ORX_PLAYER1_WIN 2
+#define ORX_PLAYER2_WIN 3
+#define ORX_TIE 4
+/* build-only per-game status codes (>= 16): the game is stopped            */
+#define ORX_STATUS_BAD_ACTION 16   /* an action outside 1..5 (reference would
+                                      attack itself, updater.py:229-234)     */
+#define ORX_STATUS_RNG_EXHAUSTED 17 /* a rejection loop ran past its word cap
+                                      (probability < 1e-180; never observed) */
+/* DungeonDespawningStrategy  optimax_rogue/logic/updater.py:47-50           */
+#define ORX_DESPAWN_UNREACHABLE 1
+#define ORX_DESPAWN_UNUSED 2
+/* GameStartGenerator plugins optimax_rogue/logic/worldgen.py:61-135         */
+#define ORX_START_TOGETHER 1
+#define ORX_START_SEPARATED 2
+/* Tile            optimax_rogue/game/world.py:10-17                         */
+#define ORX_TILE_GROUND 1
+#define ORX_TILE_WALL 2
+#define ORX_TILE_STAIRCASE_DOWN 3
+/* CombatFlag      optimax_rogue/game/modifiers.py:7-12                      */
+#define ORX_FLAG_BLOCK 1
+#define ORX_FLAG_AMBUSH 2
+#define ORX_FLAG_FLEE 3
+#define ORX_FLAG_PARRY 4
+/* action producers (bots) optimax_rogue_bots/{randombot,staircasebot}.py   */
+#define ORX_POLICY_NONE 0      /* leave the action untouched                  */
+#define ORX_POLICY_RANDOM 1    /* RandomBot.move   randombot.py:20-21          */
+#define ORX_POLICY_STAIRCASE 2 /* StaircaseBot.move staircasebot.py:9-21       */
+#define ORX_POLICY_STAY 3      /* always Move.Stay                            */
+
+/* per-game event counters (rows of orx_state_t.counters)                    */
+#define ORX_CNT_COMBAT 0        /* handle_combat calls       updater.py:298  */
+#define ORX_CNT_DESCEND 1       /* player descents           updater.py:259  */
+#define ORX_CNT_DUNGEON 2       /* spawn_dungeon calls in ticks updater.py:274 */
+#define ORX_CNT_NPC_DEATH 3     /* EntityDeathUpdate sweeps  updater.py:136  */
+#define ORX_NCOUNTERS 4
+
+#define ORX_MAX_NPCS 16 /* NPCs per game (alive mask is 32-bit; registers)  */
+#define ORX_MAX_GRID_NPC 256 /* NPC (x,y) pack into 8+8 bits when K > 0    */
+
+/* trajectory fields, rows of one orx_rollout tick record                    */
+#define ORX_OBS_P1_X 0
+#define ORX_OBS_P1_Y 1
+#define ORX_OBS_P1_DEPTH 2
+#define ORX_OBS_P1_HEALTH 3
+#define ORX_OBS_P2_X 4
+#define ORX_OBS_P2_Y 5
+#define ORX_OBS_P2_DEPTH 6
+#define ORX_OBS_P2_HEALTH 7
+#define ORX_OBS_TICK 8
+#define ORX_OBS_STATUS 9
+#define ORX_OBS_FIELDS 10
+
+/* ---- configuration (POD) ------------------------------------------------ */
+/* Mirrors the reference's construction arguments:
+ *   Updater(dgen, despawn_strat, max_ticks)        updater.py:65-69
+ *   EmptyDungeonGenerator(width, height)           worldgen.py:29-43
+ *   Together/SeparatedGameStartGenerator(...)      worldgen.py:61-135
+ *   Entity(iden, depth, x, y, 10, 10, 2, 1, ...)   worldgen.py:85-86        */
+typedef struct orx_cfg {
+  int32_t width;          /* W >= 4  (np.random.randint(1, W-2) needs W > 3) */
+  int32_t height;         /* H >= 4                                          */
+  int32_t despawn;        /* ORX_DESPAWN_*                                   */
+  int32_t max_ticks;      /* 0 = no limit ("if self.max_ticks and ...")      */
+  int32_t start_mode;     /* ORX_START_*                                     */
+  int32_t p1_depth;       /* Separated start depths (Together: both 0)       */
+  int32_t p2_depth;
+  int32_t n_npcs;         /* K NPCs at reset on player 1's start depth       */
+  int32_t npc_health;     /* 1..127                                          */
+  int32_t npc_damage;
+  int32_t npc_armor;
+  int32_t player_health;  /* 10 */
+  int32_t player_damage;  /* 2  */
+  int32_t player_armor;   /* 1  */
+  int32_t autoreset;      /* 1: a finished game is reset by the next step    */
+  int32_t flags;          /* extension flags; 0 = reference parity           */
+} orx_cfg_t;
+
+/* ---- batch state (SoA, batch axis contiguous; all device pointers) ------- */
+/* Shapes use B = games in this call.  "[2][B]" = player 1 row then player 2. */
+typedef struct orx_state {
+  int32_t* p_x;        /* [2][B] Entity.x        entities.py:36-59           */
+  int32_t* p_y;        /* [2][B] Entity.y                                    */
+  int32_t* p_depth;    /* [2][B] Entity.depth                                */
+  int32_t* p_health;   /* [2][B] Entity.health                               */
+  int32_t* st_x;       /* [2][B] Dungeon.staircase() of each player's depth  */
+  int32_t* st_y;       /* [2][B]                     world.py:52-55          */
+  int32_t* tick;       /* [B]    GameState.tick      state.py:25-29          */
+  int32_t* status;     /* [B]    last UpdateResult (or ORX_STATUS_*)         */
+  int32_t* episode;    /* [B]    episode index (Philox counter word 1)       */
+  int32_t* ret_sum;    /* [B]    sum of finished-episode outcomes, p1 view:
+                                 +1 Player1Win, -1 Player2Win, 0 Tie         */
+  int32_t* ep_count;   /* [B]    finished episodes                           */
+  int32_t* counters;   /* [ORX_NCOUNTERS][B] event counters (may be NULL)    */
+  uint16_t* npc_pos;   /* [K][B] x | y << 8  (NULL when K == 0)              */
+  int8_t* npc_health;  /* [K][B]                                             */
+  uint32_t* npc_alive; /* [B]    bit k = NPC k still in GameState.entities   */
+} orx_state_t;
+
+/* ---- entry points --------------------------------------------------------- */
+
+/* ORX_ABI_VERSION of the loaded library. */
+int orx_abi_version(void);
+
+/* Message for the last non-zero return on this thread ("" if none). */
+const char* orx_last_error(void);
+
+/* Validates a configuration without touching the device.
+ * Replaces the constructor checks of Updater / generators
+ * (updater.py:65-69, worldgen.py:61-135; ValueError -> ORX_EINVAL). */
+int orx_validate_cfg(const orx_cfg_t* cfg);
+
+/* Starts episode st->episode[b] for every game b with mask[b] != 0
+ * (mask == NULL: all games).  Replaces GameStartGenerator.setup_game:
+ * TogetherGameStartGenerator.setup_game  worldgen.py:77-87
+ * SeparatedGameStartGenerator.setup_game worldgen.py:124-135
+ * plus the NPC spawner (build-defined). */
+int orx_reset(const orx_cfg_t* cfg, const orx_state_t* st, const uint8_t* mask,
+              int64_t n_games, uint64_t seed, int64_t game_offset, void* stream);
+
+/* Advances every game one tick with actions[b][0] (player 1) and
+ * actions[b][1] (player 2), values Move 1..5.  Replaces
+ * Updater.update(game_state, player1_move, player2_move)  updater.py:76-162
+ * (with GameState.on_tick, state.py:46-51, folded in).  A game whose status
+ * is not ORX_IN_PROGRESS is reset to its next episode when cfg->autoreset,
+ * else left unchanged. */
+int orx_step(const orx_cfg_t* cfg, const orx_state_t* st, const int8_t* actions,
+             int64_t n_games, uint64_t seed, int64_t game_offset, void* stream);
+
+/* Writes actions[b][p] from the stock bots.  Replaces
+ * RandomBot.move    optimax_rogue_bots/randombot.py:20-21
+ * StaircaseBot.move optimax_rogue_bots/staircasebot.py:9-21 */
+int orx_policy(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p1,
+               int32_t policy_p2, int8_t* actions, int64_t n_games,
+               uint64_t seed, int64_t game_offset, void* stream);
+
+/* Fused rollout: n_ticks x (orx_policy then orx_step) in one launch, state
+ * kept in registers between ticks.  If obs != NULL, tick t's post-step
+ * observation is written to obs[(t * ORX_OBS_FIELDS + f) * n_games + b]
+ * (int32) and its actions to act[(t * n_games + b) * 2 + p] (int8, may be
+ * NULL).  Bit-identical to the unfused sequence (tested).  Replaces the
+ * server hot loop server/main.py:110-113 around Updater.update. */
+int orx_rollout(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p1,
+                int32_t policy_p2, int32_t n_ticks, int32_t* obs, int8_t* act,
+                int64_t n_games, uint64_t seed, int64_t game_offset,
+                void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ORX_H */

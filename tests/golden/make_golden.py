@@ -1,0 +1,459 @@
+"""Generates the golden fixtures in tests/golden/ from the REFERENCE updater.
+
+Run in the build container only (it needs /root/reference; nothing at test
+time imports the reference):
+
+    python tests/golden/make_golden.py
+
+What it does
+------------
+It imports the unmodified reference packages (optimax_rogue, optimax_rogue_bots)
+and drives the in-process loop of SURVEY.md s3.3:
+``gs.on_tick(); result, updates = Updater.update(gs, m1, m2)``
+with the engine's Philox4x32-10 word stream injected at the reference's own draw
+sites, so that the reference's code -- not a restatement -- computes every
+output:
+
+* ``optimax_rogue.logic.updater.random`` and ``optimax_rogue_bots.randombot.random``
+  are replaced by a ``random.Random`` subclass whose ``getrandbits(k)`` returns
+  ``word >> (32 - k)``.  CPython's own ``shuffle``/``choice``/``_randbelow``
+  (Lib/random.py, 3.10) run unchanged on top of it (updater.py:114,127,
+  randombot.py:21).
+* ``np`` in ``optimax_rogue.logic.worldgen`` and ``optimax_rogue.game.world`` is
+  a proxy whose ``random.randint`` is numpy's legacy bounded-integer transform
+  (masked rejection over 32-bit words, numpy/random/_bounded_integers.pyx,
+  ``_rand_int64`` -> ``random_bounded_uint64_fill`` with ``use_masked``);
+  every other attribute is numpy itself (worldgen.py:39-40, world.py:62).
+* Dungeons come from ``KeyedDungeonGenerator``, a subclass of the reference's
+  ``EmptyDungeonGenerator`` (its plugin API, worldgen.py:9-43) that only selects
+  the word stream (episode, depth, generation) before calling the reference's
+  ``spawn_dungeon``.
+* NPCs ("enemies") come from ``NpcGameStart``, a ``GameStartGenerator``
+  (worldgen.py:47-58) that calls the reference's Together/Separated
+  ``setup_game`` and then places K NPCs with the reference's
+  ``Dungeon.get_random_unblocked`` and ``GameState.add_entity``.
+
+The third-party module ``inflection`` (imported by serializer.py:27, unpinned:
+setup.py:11 has install_requires=[]) is not installed.  It is only used for
+serializer registry names (serializer.py:95), never on the tick path; a stub
+restating ``inflection.underscore`` (inflection 0.5.1: two regex passes, '-'
+to '_', lower-case) is put in sys.modules.
+
+Stream keys (must match include/orx.h / DESIGN.md): Philox key = seed;
+counter = (global game id, episode, c2, purpose << 28 | gen << 24 | block)
+with purposes INIT=1 (c2 = 0), DUNGEON=2 (c2 = depth), SHUFFLE=3, SPAWN=4,
+POLICY=5 (c2 = tick before the update).
+"""
+from __future__ import annotations
+
+import contextlib
+import io
+import json
+import os
+import random
+import re
+import sys
+import types
+
+import numpy as np
+
+REF = "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+# --------------------------------------------------------------------------
+# Philox4x32-10 (independent pure-Python implementation)
+# --------------------------------------------------------------------------
+M = 0xFFFFFFFF
+
+
+def philox4x32_10(ctr, key):
+    c0, c1, c2, c3 = ctr
+    k0, k1 = key
+    for _ in range(10):
+        p0 = 0xD2511F53 * c0
+        p1 = 0xCD9E8D57 * c2
+        c0, c1, c2, c3 = ((p1 >> 32) ^ c1 ^ k0) & M, p1 & M, ((p0 >> 32) ^ c3 ^ k1) & M, p0 & M
+        k0 = (k0 + 0x9E3779B9) & M
+        k1 = (k1 + 0xBB67AE85) & M
+    return c0, c1, c2, c3
+
+
+PUR_INIT, PUR_DUNGEON, PUR_SHUFFLE, PUR_SPAWN, PUR_POLICY = 1, 2, 3, 4, 5
+
+
+class Stream:
+    def __init__(self, seed, game, episode, c2, purpose, gen=0):
+        self.key = (seed & M, (seed >> 32) & M)
+        self.c = (game & M, episode & M, c2 & M, (purpose << 28) | (gen << 24))
+        self.idx = 0
+        self.buf = None
+
+    def next(self):
+        if self.idx % 4 == 0:
+            self.buf = philox4x32_10(
+                (self.c[0], self.c[1], self.c[2], self.c[3] | (self.idx // 4)), self.key)
+        w = self.buf[self.idx % 4]
+        self.idx += 1
+        return w
+
+
+class PhiloxRandom(random.Random):
+    """random.Random whose bits come from the current Philox stream."""
+
+    def __init__(self):
+        super().__init__(0)
+        self.stream = None
+
+    def getrandbits(self, k):
+        assert 0 < k <= 32
+        return self.stream.next() >> (32 - k)
+
+
+class NpRandom:
+    """numpy.random stand-in exposing the legacy scalar randint transform."""
+
+    def __init__(self):
+        self.stream = None
+
+    def randint(self, low, high=None, size=None, dtype=int):
+        assert size is None
+        if high is None:
+            low, high = 0, low
+        if low >= high:
+            raise ValueError("low >= high")
+        rng = high - 1 - low
+        if rng == 0:
+            return low
+        mask = (1 << rng.bit_length()) - 1
+        while True:
+            v = self.stream.next() & mask
+            if v <= rng:
+                return low + v
+
+
+class NpProxy:
+    def __init__(self, rnd):
+        self.random = rnd
+
+    def __getattr__(self, name):
+        return getattr(np, name)
+
+
+def _underscore(word):
+    word = re.sub(r"([A-Z]+)([A-Z][a-z])", r"\1_\2", word)
+    word = re.sub(r"([a-z\d])([A-Z])", r"\1_\2", word)
+    word = word.replace("-", "_")
+    return word.lower()
+
+
+def import_reference():
+    stub = types.ModuleType("inflection")
+    stub.underscore = _underscore
+    sys.modules.setdefault("inflection", stub)
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+    import optimax_rogue.logic.updater as updater_mod
+    import optimax_rogue.logic.worldgen as worldgen_mod
+    import optimax_rogue.game.world as world_mod
+    import optimax_rogue_bots.randombot as randombot_mod
+    import optimax_rogue_bots.staircasebot as staircasebot_mod
+    import optimax_rogue.game.state as state_mod
+    import optimax_rogue.game.entities as entities_mod
+    import optimax_rogue.logic.updates as updates_mod
+    import optimax_rogue.logic.moves as moves_mod
+    pyrand = PhiloxRandom()
+    nprand = NpRandom()
+    updater_mod.random = pyrand
+    randombot_mod.random = pyrand
+    worldgen_mod.np = NpProxy(nprand)
+    world_mod.np = NpProxy(nprand)
+    return types.SimpleNamespace(
+        updater=updater_mod, worldgen=worldgen_mod, world=world_mod,
+        randombot=randombot_mod, staircasebot=staircasebot_mod, state=state_mod,
+        entities=entities_mod, updates=updates_mod, moves=moves_mod,
+        pyrand=pyrand, nprand=nprand)
+
+
+# --------------------------------------------------------------------------
+# Harness around the reference
+# --------------------------------------------------------------------------
+class Harness:
+    """One reference game (GameState + Updater) with keyed streams."""
+
+    def __init__(self, R, cfg, seed, game_id):
+        self.R, self.cfg, self.seed, self.gid = R, cfg, seed, game_id
+        self.episode = 0
+        self.gens = {}
+        R_ = R
+
+        harness = self
+
+        class KeyedDungeonGenerator(R_.worldgen.EmptyDungeonGenerator):
+            def spawn_dungeon(self, depth):
+                gen = harness.gens.get(depth, 0)
+                harness.gens[depth] = gen + 1
+                saved = R_.nprand.stream
+                R_.nprand.stream = Stream(harness.seed, harness.gid, harness.episode, depth,
+                                          PUR_DUNGEON, gen)
+                try:
+                    return super().spawn_dungeon(depth)
+                finally:
+                    R_.nprand.stream = saved
+
+        class NpcGameStart(R_.worldgen.GameStartGenerator):
+            def __init__(self, inner, k, hp, dmg, arm):
+                self.inner, self.k, self.hp, self.dmg, self.arm = inner, k, hp, dmg, arm
+
+            def setup_game(self):
+                gs = self.inner.setup_game()
+                d = gs.player_1.depth
+                dung = gs.world.get_at_depth(d)
+                for k in range(self.k):
+                    x, y = dung.get_random_unblocked()
+                    while (d, x, y) in gs.pos_lookup:
+                        x, y = dung.get_random_unblocked()
+                    gs.add_entity(R_.entities.Entity(3 + k, d, x, y, self.hp, self.hp,
+                                                     self.dmg, self.arm, [], dict()))
+                return gs
+
+        self.dgen = KeyedDungeonGenerator(cfg["width"], cfg["height"])
+        if cfg["start_mode"] == 2:
+            inner = R.worldgen.SeparatedGameStartGenerator(self.dgen, cfg["p1_depth"],
+                                                           cfg["p2_depth"])
+        else:
+            inner = R.worldgen.TogetherGameStartGenerator(self.dgen)
+        self.start = NpcGameStart(inner, cfg["n_npcs"], cfg["npc_health"], cfg["npc_damage"],
+                                  cfg["npc_armor"])
+        strat = R.updater.DungeonDespawningStrategy(cfg["despawn"])
+        self.updater = R.updater.Updater(self.dgen, strat, cfg["max_ticks"] or None)
+        self.bots = [self._bot(cfg["policy"][0], 1), self._bot(cfg["policy"][1], 2)]
+        self.ret_sum = 0
+        self.ep_count = 0
+        self.counters = [0, 0, 0, 0]
+        self.status = 1
+        self.setup()
+
+    def _bot(self, pol, iden):
+        if pol == 1:
+            return self.R.randombot.RandomBot(iden)
+        if pol == 2:
+            return self.R.staircasebot.StaircaseBot(iden)
+        return None
+
+    def setup(self):
+        self.gens = {}
+        self.R.nprand.stream = Stream(self.seed, self.gid, self.episode, 0, PUR_INIT)
+        self.gs = self.start.setup_game()
+        self.status = 1
+
+    def policy(self, given=None):
+        self.R.pyrand.stream = Stream(self.seed, self.gid, self.episode, self.gs.tick, PUR_POLICY)
+        acts = []
+        for p in range(2):
+            bot = self.bots[p]
+            if bot is None:
+                acts.append(int(given[p]))
+            else:
+                acts.append(int(bot.move(self.gs)))
+        return acts
+
+    def step(self, acts):
+        """One engine step: autoreset a finished game, else one reference tick."""
+        R = self.R
+        events = []
+        if self.status != 1:
+            if self.cfg["autoreset"]:
+                self.episode += 1
+                self.setup()
+            return events
+        self.gs.on_tick()
+        R.pyrand.stream = Stream(self.seed, self.gid, self.episode, self.gs.tick, PUR_SHUFFLE)
+        R.nprand.stream = Stream(self.seed, self.gid, self.episode, self.gs.tick, PUR_SPAWN)
+        with contextlib.redirect_stdout(io.StringIO()):
+            res, upds = self.updater.update(self.gs, R.moves.Move(acts[0]), R.moves.Move(acts[1]))
+        self.status = int(res)
+        if self.status == 2:
+            self.ret_sum += 1
+        elif self.status == 3:
+            self.ret_sum -= 1
+        if self.status != 1:
+            self.ep_count += 1
+        U = R.updates
+        for u in upds:
+            if isinstance(u, U.EntityCombatUpdate):
+                (flag,) = tuple(u.tags)
+                events.append((1, u.attacker_iden, u.defender_iden, int(flag)))
+                self.counters[0] += 1
+            elif isinstance(u, U.EntityDeathUpdate):
+                events.append((2, u.entity_iden, 0, 0))
+                if u.entity_iden not in (1, 2):
+                    self.counters[3] += 1
+            elif isinstance(u, U.EntityPositionUpdate):
+                events.append((3, u.entity_iden, u.depth, (u.posx & 0xFFFF) | (u.posy << 16)))
+                if u.depth != u.old_depth:
+                    self.counters[1] += 1
+            elif isinstance(u, U.DungeonCreatedUpdate):
+                events.append((4, 0, u.depth, 0))
+                self.counters[2] += 1
+            else:
+                raise AssertionError(type(u))
+        return events
+
+    def snapshot(self):
+        gs = self.gs
+        K = self.cfg["n_npcs"]
+        p = [gs.player_1, gs.player_2]
+        rec = {}
+        rec["p_x"] = [e.x for e in p]
+        rec["p_y"] = [e.y for e in p]
+        rec["p_depth"] = [e.depth for e in p]
+        rec["p_health"] = [e.health for e in p]
+        st = [gs.world.get_at_depth(e.depth).staircase() for e in p]
+        rec["st_x"] = [s[0] for s in st]
+        rec["st_y"] = [s[1] for s in st]
+        rec["tick"] = gs.tick
+        rec["status"] = self.status
+        rec["episode"] = self.episode
+        rec["ret_sum"] = self.ret_sum
+        rec["ep_count"] = self.ep_count
+        rec["counters"] = list(self.counters)
+        pos = [0] * K
+        hp = [0] * K
+        alive = 0
+        for e in gs.entities:
+            if e.iden >= 3:
+                k = e.iden - 3
+                alive |= 1 << k
+                pos[k] = (e.x & 0xFF) | ((e.y & 0xFF) << 8)
+                hp[k] = e.health
+        rec["npc_pos"] = pos
+        rec["npc_health"] = hp
+        rec["npc_alive"] = alive
+        rec["world"] = [(d, *gs.world.dungeons[d].staircase()) for d in gs.world.dungeons]
+        rec["entities"] = [(e.iden, e.depth, e.x, e.y, e.health) for e in gs.entities]
+        return rec
+
+
+DEFAULT_CFG = dict(width=32, height=32, despawn=1, max_ticks=1000, start_mode=1, p1_depth=0,
+                   p2_depth=0, n_npcs=0, npc_health=3, npc_damage=1, npc_armor=0,
+                   player_health=10, player_damage=2, player_armor=1, autoreset=1, flags=0,
+                   policy=(1, 1))
+
+CASES = {
+    # C1 of BASELINE.json: 32x32, 2x RandomBot, max_ticks 1000 (long enough to autoreset)
+    "c1_random_32": dict(cfg=dict(), seed=1, games=4, ticks=1100),
+    # combat-heavy: tiny board, NPCs, short episodes
+    "small_npc_random": dict(cfg=dict(width=6, height=6, n_npcs=4, max_ticks=60), seed=2,
+                             games=24, ticks=260),
+    # player deaths (no tick limit) on a 5x5 board
+    "duel_5": dict(cfg=dict(width=5, height=5, max_ticks=0), seed=3, games=24, ticks=700),
+    # deep multi-depth play, despawn Unreachable
+    "stairs_unreachable": dict(cfg=dict(width=8, height=7, max_ticks=150, policy=(2, 2)), seed=4,
+                               games=16, ticks=320),
+    # despawn Unused: regenerated depths (generation 1)
+    "stairs_unused": dict(cfg=dict(width=7, height=8, max_ticks=150, despawn=2, policy=(2, 1)),
+                          seed=5, games=16, ticks=320),
+    "stairs_unused_both": dict(cfg=dict(width=6, height=6, max_ticks=120, despawn=2,
+                                        policy=(2, 2), n_npcs=2), seed=6, games=16, ticks=260),
+    # Separated start, both strategies
+    "separated_unreachable": dict(cfg=dict(width=6, height=7, max_ticks=120, start_mode=2,
+                                           p1_depth=0, p2_depth=3, policy=(2, 1), n_npcs=3),
+                                  seed=7, games=12, ticks=260),
+    "separated_unused": dict(cfg=dict(width=7, height=6, max_ticks=120, start_mode=2, despawn=2,
+                                      p1_depth=2, p2_depth=0, policy=(1, 2)), seed=8, games=12,
+                             ticks=260),
+    # C3 shape: 64x64, K=8 NPCs, random
+    "c3_npc_64": dict(cfg=dict(width=64, height=64, n_npcs=8), seed=3, games=6, ticks=300),
+    # minimum board (W=H=4: staircase fixed at (1,1), no dungeon draws)
+    "tiny_4": dict(cfg=dict(width=4, height=4, max_ticks=40, n_npcs=1, policy=(1, 2)), seed=9,
+                   games=16, ticks=200),
+    # non-square, game_offset != 0, seed > 2^32
+    "offset_seed": dict(cfg=dict(width=9, height=5, max_ticks=80, n_npcs=2), seed=(7 << 32) | 11,
+                        games=8, ticks=200, offset=1000),
+}
+
+SNAP_KEYS_I32 = ["p_x", "p_y", "p_depth", "p_health", "st_x", "st_y", "tick", "status",
+                 "episode", "ret_sum", "ep_count", "counters", "npc_pos", "npc_health",
+                 "npc_alive"]
+
+
+def run_case(R, name, spec):
+    cfg = dict(DEFAULT_CFG)
+    cfg.update(spec["cfg"])
+    seed, G, T = spec["seed"], spec["games"], spec["ticks"]
+    off = spec.get("offset", 0)
+    hs = [Harness(R, cfg, seed, off + g) for g in range(G)]
+    snaps = {k: [] for k in SNAP_KEYS_I32}
+    actions = np.zeros((T, G, 2), np.int8)
+    world_len = np.zeros((T + 1, G), np.int32)
+    world = []
+    ev_len = np.zeros((T, G), np.int32)
+    events = []
+    ent_len = np.zeros((T + 1, G), np.int32)
+    ents = []
+
+    def record(t):
+        recs = [h.snapshot() for h in hs]
+        for k in SNAP_KEYS_I32:
+            snaps[k].append([r[k] for r in recs])
+        for g, r in enumerate(recs):
+            world_len[t, g] = len(r["world"])
+            world.extend(r["world"])
+            ent_len[t, g] = len(r["entities"])
+            ents.extend(r["entities"])
+
+    record(0)
+    for t in range(T):
+        for g, h in enumerate(hs):
+            a = h.policy()
+            actions[t, g] = a
+            evs = h.step(a)
+            ev_len[t, g] = len(evs)
+            events.extend(evs)
+        record(t + 1)
+
+    out = {"cfg_json": np.frombuffer(json.dumps(cfg).encode(), np.uint8),
+           "seed": np.array([seed], np.uint64), "game_offset": np.array([off], np.int64),
+           "actions": actions, "world_len": world_len,
+           "world": np.array(world, np.int32).reshape(-1, 3),
+           "event_len": ev_len, "events": np.array(events, np.int32).reshape(-1, 4),
+           "entity_len": ent_len, "entities": np.array(ents, np.int32).reshape(-1, 5)}
+    for k in SNAP_KEYS_I32:
+        a = np.array(snaps[k])
+        if a.ndim == 3:  # [T+1, G, F] -> [T+1, F, G] (engine SoA layout)
+            a = a.transpose(0, 2, 1)
+        dt = {"npc_pos": np.uint16, "npc_health": np.int8, "npc_alive": np.uint32}.get(k, np.int32)
+        out[k] = np.ascontiguousarray(a.astype(dt))
+    path = os.path.join(HERE, f"{name}.npz")
+    np.savez_compressed(path, **out)
+    st = out["status"][1:]
+    print(f"{name}: {G} games x {T} ticks, finished episodes={int(out['ep_count'][-1].sum())}, "
+          f"combats={int(out['counters'][-1][0].sum())}, descents={int(out['counters'][-1][1].sum())}, "
+          f"dungeons={int(out['counters'][-1][2].sum())}, npc deaths={int(out['counters'][-1][3].sum())}, "
+          f"max depth={int(out['p_depth'].max())}, statuses={sorted(set(st.ravel().tolist()))}, "
+          f"bytes={os.path.getsize(path)}")
+
+
+def philox_kat():
+    """Random123 known-answer vectors for Philox4x32-10 (kat_vectors)."""
+    return [
+        ((0, 0, 0, 0), (0, 0), (0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8)),
+        ((M, M, M, M), (M, M), (0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD)),
+        ((0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344), (0xA4093822, 0x299F31D0),
+         (0xD16CFE09, 0x94FDCCEB, 0x5001E420, 0x24126EA1)),
+    ]
+
+
+def main():
+    for ctr, key, want in philox_kat():
+        assert philox4x32_10(ctr, key) == want
+    R = import_reference()
+    only = sys.argv[1:]
+    for name, spec in CASES.items():
+        if only and name not in only:
+            continue
+        run_case(R, name, spec)
+
+
+if __name__ == "__main__":
+    main()

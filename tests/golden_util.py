@@ -1,0 +1,81 @@
+"""Loading helpers for the committed golden fixtures (tests/golden/*.npz).
+
+The fixtures were produced by tests/golden/make_golden.py from the reference
+updater itself; they are data only (inputs and expected outputs).
+"""
+from __future__ import annotations
+
+import glob
+import json
+import os
+
+import numpy as np
+
+GOLDEN_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+STATE_KEYS = ["p_x", "p_y", "p_depth", "p_health", "st_x", "st_y", "tick", "status", "episode",
+              "ret_sum", "ep_count", "counters", "npc_pos", "npc_health", "npc_alive"]
+
+
+def case_names():
+    return sorted(os.path.splitext(os.path.basename(p))[0]
+                  for p in glob.glob(os.path.join(GOLDEN_DIR, "*.npz")))
+
+
+class Fixture:
+    def __init__(self, name: str):
+        self.name = name
+        z = np.load(os.path.join(GOLDEN_DIR, name + ".npz"), allow_pickle=False)
+        self.z = {k: z[k] for k in z.files}
+        self.cfg = json.loads(bytes(self.z["cfg_json"]).decode())
+        self.seed = int(self.z["seed"][0])
+        self.game_offset = int(self.z["game_offset"][0])
+        self.actions = self.z["actions"]            # [T, G, 2] int8
+        self.T, self.G = self.actions.shape[:2]
+        self.K = int(self.cfg["n_npcs"])
+        self.policy = tuple(self.cfg["policy"])
+        wl = self.z["world_len"]
+        self._world_off = np.concatenate([[0], np.cumsum(wl.ravel())])
+        el = self.z["event_len"]
+        self._ev_off = np.concatenate([[0], np.cumsum(el.ravel())])
+        nl = self.z["entity_len"]
+        self._ent_off = np.concatenate([[0], np.cumsum(nl.ravel())])
+
+    def state(self, t: int) -> dict:
+        """Engine-layout state after t steps (t = 0: after the initial reset)."""
+        return {k: self.z[k][t] for k in STATE_KEYS}
+
+    def world(self, t: int, g: int):
+        i = t * self.G + g
+        rows = self.z["world"][self._world_off[i]:self._world_off[i + 1]]
+        return [tuple(int(v) for v in r) for r in rows]
+
+    def events(self, t: int, g: int):
+        """Update events of step t (0-based) of game g."""
+        i = t * self.G + g
+        rows = self.z["events"][self._ev_off[i]:self._ev_off[i + 1]]
+        return [tuple(int(v) for v in r) for r in rows]
+
+    def entities(self, t: int, g: int):
+        i = t * self.G + g
+        rows = self.z["entities"][self._ent_off[i]:self._ent_off[i + 1]]
+        return [tuple(int(v) for v in r) for r in rows]
+
+
+def compare_state(got: dict, want: dict, K: int, where: str = ""):
+    """Asserts bit-exact equality of every state field (NPC slots only if K)."""
+    for k in STATE_KEYS:
+        if k.startswith("npc") and K == 0:
+            continue
+        g = np.asarray(got[k])
+        w = np.asarray(want[k])
+        if k in ("npc_pos", "npc_health"):
+            # dead NPC slots are unspecified: compare alive slots only
+            alive = np.asarray(want["npc_alive"])
+            mask = ((alive[None, :] >> np.arange(K)[:, None]) & 1).astype(bool)
+            g = np.where(mask, g, 0)
+            w = np.where(mask, w, 0)
+        if g.shape != w.shape or not np.array_equal(g.astype(np.int64), w.astype(np.int64)):
+            bad = np.argwhere(g.astype(np.int64) != w.astype(np.int64)) if g.shape == w.shape else None
+            raise AssertionError(f"{where}: field {k} differs; first mismatches {bad[:5] if bad is not None else 'shape'}"
+                                 f"\n got={g.ravel()[:16]}\nwant={w.ravel()[:16]}")
