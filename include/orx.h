@@ -97,7 +97,11 @@ extern "C" {
 #define ORX_OBS_P2_HEALTH 7
 #define ORX_OBS_TICK 8
 #define ORX_OBS_STATUS 9
-#define ORX_OBS_FIELDS 10
+#define ORX_OBS_P1_STAIR_X 10
+#define ORX_OBS_P1_STAIR_Y 11
+#define ORX_OBS_P2_STAIR_X 12
+#define ORX_OBS_P2_STAIR_Y 13
+#define ORX_OBS_FIELDS 14
 
 /* ---- configuration (POD) ------------------------------------------------ */
 /* Mirrors the reference's construction arguments:

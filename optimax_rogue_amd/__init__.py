@@ -1,0 +1,23 @@
+"""optimax_rogue_amd -- MI355X-native batched step engine for the Optimax Rogue
+per-tick updater (reference: optimax_rogue/logic + optimax_rogue/game).
+
+Host side is Python; the tick, reset and bot policies are HIP kernels for
+gfx950 in liborx.so, reached through the C-ABI declared in include/orx.h.
+"""
+from .config import EnvConfig
+from .enums import (CombatFlag, DungeonDespawningStrategy, Move, OBS_FIELDS, Policy, StartMode,
+                    Tile, UpdateResult)
+
+__all__ = ["EnvConfig", "Move", "UpdateResult", "DungeonDespawningStrategy", "Tile", "CombatFlag",
+           "StartMode", "Policy", "OBS_FIELDS", "BatchedEngine", "BatchedUpdater"]
+
+
+def __getattr__(name):
+    # lazy: importing the package must not require torch / the built library
+    if name == "BatchedEngine":
+        from .engine import BatchedEngine
+        return BatchedEngine
+    if name == "BatchedUpdater":
+        from .updater import BatchedUpdater
+        return BatchedUpdater
+    raise AttributeError(name)

@@ -1,0 +1,75 @@
+"""ctypes loader for liborx.so (the HIP engine, C-ABI in include/orx.h).
+
+There is no fallback: if the library is missing or cannot be loaded, every
+engine call raises.  Build it with ``python -m optimax_rogue_amd.build`` (or
+``__graft_entry__.build()``).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+from .config import OrxCfg
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "liborx.so")
+ABI_VERSION = 1
+
+
+class OrxState(ctypes.Structure):
+    """ctypes mirror of orx_state_t (device pointers)."""
+    _fields_ = [(n, ctypes.c_void_p) for n in (
+        "p_x", "p_y", "p_depth", "p_health", "st_x", "st_y", "tick", "status", "episode",
+        "ret_sum", "ep_count", "counters", "npc_pos", "npc_health", "npc_alive")]
+
+
+class OrxError(RuntimeError):
+    def __init__(self, fn: str, code: int, msg: str):
+        super().__init__(f"{fn} returned {code}: {msg}")
+        self.code = code
+
+
+_lib = None
+
+EXPORTS = ("orx_abi_version", "orx_last_error", "orx_validate_cfg", "orx_reset", "orx_step",
+           "orx_policy", "orx_rollout")
+
+
+def load() -> ctypes.CDLL:
+    """Loads liborx.so once.  torch is imported first so the library binds to the
+    HIP runtime (libamdhip64.so.7) already mapped by PyTorch-ROCm."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    import torch  # noqa: F401  (HIP runtime first)
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"HIP engine library missing: {LIB_PATH} -- run "
+                           "`python -m optimax_rogue_amd.build` first")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i64, i32, u64 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_uint64
+    P = ctypes.POINTER
+    L.orx_abi_version.restype = ctypes.c_int
+    L.orx_abi_version.argtypes = []
+    L.orx_last_error.restype = ctypes.c_char_p
+    L.orx_last_error.argtypes = []
+    L.orx_validate_cfg.restype = ctypes.c_int
+    L.orx_validate_cfg.argtypes = [P(OrxCfg)]
+    L.orx_reset.restype = ctypes.c_int
+    L.orx_reset.argtypes = [P(OrxCfg), P(OrxState), vp, i64, u64, i64, vp]
+    L.orx_step.restype = ctypes.c_int
+    L.orx_step.argtypes = [P(OrxCfg), P(OrxState), vp, i64, u64, i64, vp]
+    L.orx_policy.restype = ctypes.c_int
+    L.orx_policy.argtypes = [P(OrxCfg), P(OrxState), i32, i32, vp, i64, u64, i64, vp]
+    L.orx_rollout.restype = ctypes.c_int
+    L.orx_rollout.argtypes = [P(OrxCfg), P(OrxState), i32, i32, i32, vp, vp, i64, u64, i64, vp]
+    v = L.orx_abi_version()
+    if v != ABI_VERSION:
+        raise RuntimeError(f"liborx.so ABI {v} != expected {ABI_VERSION}")
+    _lib = L
+    return L
+
+
+def check(fn: str, code: int) -> None:
+    if code != 0:
+        msg = load().orx_last_error().decode(errors="replace")
+        raise OrxError(fn, code, msg)

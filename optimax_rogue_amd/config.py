@@ -1,0 +1,82 @@
+"""EnvConfig: the construction arguments of the reference's updater and
+generators, mirrored by the POD struct orx_cfg_t (include/orx.h).
+
+Reference counterparts:
+  Updater(dgen, despawn_strat, max_ticks)           optimax_rogue/logic/updater.py:65-69
+  EmptyDungeonGenerator(width, height)              optimax_rogue/logic/worldgen.py:29-43
+  TogetherGameStartGenerator(dgen)                  optimax_rogue/logic/worldgen.py:61-87
+  SeparatedGameStartGenerator(dgen, p1_depth, p2_depth)  worldgen.py:90-135
+  Entity(iden, depth, x, y, 10, 10, 2, 1, [], {})   worldgen.py:85-86
+"""
+from __future__ import annotations
+
+import ctypes
+import dataclasses
+
+from .enums import DungeonDespawningStrategy, StartMode
+
+CFG_FIELDS = ("width", "height", "despawn", "max_ticks", "start_mode", "p1_depth", "p2_depth",
+              "n_npcs", "npc_health", "npc_damage", "npc_armor", "player_health",
+              "player_damage", "player_armor", "autoreset", "flags")
+
+
+class OrxCfg(ctypes.Structure):
+    """ctypes mirror of orx_cfg_t (field order checked against include/orx.h)."""
+    _fields_ = [(f, ctypes.c_int32) for f in CFG_FIELDS]
+
+
+@dataclasses.dataclass
+class EnvConfig:
+    width: int = 32
+    height: int = 32
+    despawn: int = DungeonDespawningStrategy.Unreachable
+    max_ticks: int = 1000           # 0 / None = never time out
+    start_mode: int = StartMode.Together
+    p1_depth: int = 0               # Separated start only
+    p2_depth: int = 1000            # reference default, worldgen.py:101
+    n_npcs: int = 0                 # "enemies": NPCs placed at reset (build-defined spawner)
+    npc_health: int = 3
+    npc_damage: int = 1
+    npc_armor: int = 0
+    player_health: int = 10
+    player_damage: int = 2
+    player_armor: int = 1
+    autoreset: int = 1
+    flags: int = 0
+
+    def to_c(self) -> OrxCfg:
+        vals = {f: int(getattr(self, f) or 0) for f in CFG_FIELDS}
+        return OrxCfg(**vals)
+
+    def to_dict(self) -> dict:
+        return {f: int(getattr(self, f) or 0) for f in CFG_FIELDS}
+
+    @classmethod
+    def from_dict(cls, d: dict) -> "EnvConfig":
+        return cls(**{k: v for k, v in d.items() if k in CFG_FIELDS})
+
+    # --- the BASELINE.json configurations -------------------------------
+    @classmethod
+    def c1(cls) -> "EnvConfig":
+        """Single game, 2x RandomBot, 32x32 (CPU plumbing config)."""
+        return cls(width=32, height=32)
+
+    @classmethod
+    def c2(cls) -> "EnvConfig":
+        """batch=4096, 32x32, random actions."""
+        return cls(width=32, height=32)
+
+    @classmethod
+    def c3(cls) -> "EnvConfig":
+        """batch=65536, 64x64 with enemies (K=8 NPCs; items have no reference semantics)."""
+        return cls(width=64, height=64, n_npcs=8)
+
+    @classmethod
+    def c4(cls) -> "EnvConfig":
+        """batch=524288 over 8 GPUs, C3 settings."""
+        return cls.c3()
+
+    @classmethod
+    def c5(cls) -> "EnvConfig":
+        """128x128 multi-depth with the staircase ("ladder") policy."""
+        return cls(width=128, height=128)

@@ -1,0 +1,175 @@
+"""BatchedEngine: B independent Optimax Rogue games resident on one GPU.
+
+PyTorch-ROCm owns every buffer (struct-of-arrays int tensors, batch axis
+contiguous); the HIP kernels in liborx.so are reached through the C-ABI of
+include/orx.h and run asynchronously on the current torch stream.
+
+Reference counterpart: one ``GameState`` (optimax_rogue/game/state.py:14-34)
+plus one ``Updater`` (optimax_rogue/logic/updater.py:52-69) per game.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional
+
+import numpy as np
+import torch
+
+from . import _lib
+from .config import EnvConfig
+from .enums import N_COUNTERS, OBS_FIELDS, Policy
+
+STATE_FIELDS = ("p_x", "p_y", "p_depth", "p_health", "st_x", "st_y", "tick", "status", "episode",
+                "ret_sum", "ep_count", "counters", "npc_pos", "npc_health", "npc_alive")
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+class BatchedEngine:
+    """SoA state of ``n_games`` games and the launches that advance it.
+
+    Global game id of local game ``i`` is ``game_offset + i``; together with
+    ``seed`` and the game's episode it keys every random draw, so a game's
+    trajectory does not depend on the batch it runs in (or on the GPU count).
+    """
+
+    def __init__(self, cfg: EnvConfig, n_games: int, seed: int = 0, game_offset: int = 0,
+                 device: Optional[torch.device] = None, reset: bool = True):
+        self.lib = _lib.load()
+        self.cfg = cfg
+        self._ccfg = cfg.to_c()
+        code = self.lib.orx_validate_cfg(ctypes.byref(self._ccfg))
+        if code != 0:
+            raise ValueError(self.lib.orx_last_error().decode())
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        device = torch.device(device)
+        if device.type != "cuda":
+            raise RuntimeError("BatchedEngine runs on a ROCm GPU only (no CPU path)")
+        self.device = device
+        self.B = int(n_games)
+        self.K = int(cfg.n_npcs)
+        self.seed = int(seed)
+        self.game_offset = int(game_offset)
+        B, K = self.B, self.K
+        z = lambda *shape, dt=torch.int32: torch.zeros(shape, dtype=dt, device=device)
+        self.p_x, self.p_y, self.p_depth, self.p_health = z(2, B), z(2, B), z(2, B), z(2, B)
+        self.st_x, self.st_y = z(2, B), z(2, B)
+        self.tick, self.status, self.episode = z(B), z(B), z(B)
+        self.ret_sum, self.ep_count = z(B), z(B)
+        self.counters = z(N_COUNTERS, B)
+        # uint16 / uint32 payloads are stored in same-width signed tensors
+        self.npc_pos = z(max(K, 1), B, dt=torch.int16)
+        self.npc_health = z(max(K, 1), B, dt=torch.int8)
+        self.npc_alive = z(B)
+        self.actions = torch.full((B, 2), 5, dtype=torch.int8, device=device)
+        self._st = _lib.OrxState(**{f: getattr(self, f).data_ptr() for f in STATE_FIELDS})
+        if reset:
+            self.reset()
+
+    # -- plumbing -----------------------------------------------------------
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _call(self, name, *args):
+        with torch.cuda.device(self.device):
+            code = getattr(self.lib, name)(ctypes.byref(self._ccfg), ctypes.byref(self._st), *args)
+        _lib.check(name, code)
+
+    # -- the C-ABI entry points -------------------------------------------
+    def reset(self, mask: Optional[torch.Tensor] = None, episode=None) -> None:
+        """GameStartGenerator.setup_game for the masked games (all if None).
+
+        ``episode`` (int or tensor) sets the episode index first; by default
+        a full reset starts every game at episode 0."""
+        if mask is None and episode is None:
+            episode = 0
+        if episode is not None:
+            ep = torch.as_tensor(episode, dtype=torch.int32, device=self.device)
+            if mask is None:
+                self.episode.copy_(ep.expand(self.B))
+            else:
+                m = mask.to(self.device).bool()
+                self.episode.copy_(torch.where(m, ep.expand(self.B), self.episode))
+        m8 = None
+        if mask is not None:
+            m8 = mask.to(device=self.device, dtype=torch.uint8).contiguous()
+            if m8.numel() != self.B:
+                raise ValueError("mask must have n_games elements")
+        self._call("orx_reset", _ptr(m8), self.B, self.seed, self.game_offset, self._stream())
+
+    def step(self, actions: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Updater.update for every game: actions[b] = (player 1, player 2) Move
+        values.  Returns the status tensor (UpdateResult codes, asynchronous)."""
+        a = self.actions if actions is None else actions
+        if a.dtype != torch.int8 or a.shape != (self.B, 2) or not a.is_contiguous() \
+                or a.device != self.device:
+            raise ValueError("actions must be a contiguous int8 [n_games, 2] tensor on "
+                             f"{self.device}")
+        self._call("orx_step", _ptr(a), self.B, self.seed, self.game_offset, self._stream())
+        return self.status
+
+    def policy(self, p1: int = Policy.Random, p2: int = Policy.Random,
+               out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """RandomBot / StaircaseBot moves for both players into ``out``."""
+        a = self.actions if out is None else out
+        self._call("orx_policy", int(p1), int(p2), _ptr(a), self.B, self.seed, self.game_offset,
+                   self._stream())
+        return a
+
+    def rollout(self, n_ticks: int, p1: int = Policy.Random, p2: int = Policy.Random,
+                obs: Optional[torch.Tensor] = None, act: Optional[torch.Tensor] = None) -> None:
+        """n_ticks x (policy, step) fused in one launch.  ``obs`` (int32
+        [n_ticks, len(OBS_FIELDS), n_games]) and ``act`` (int8 [n_ticks,
+        n_games, 2]) receive every tick's observation and actions."""
+        if obs is not None and (obs.dtype != torch.int32 or obs.numel() <
+                                n_ticks * len(OBS_FIELDS) * self.B):
+            raise ValueError("obs must be int32 [n_ticks, 14, n_games]")
+        if act is not None and (act.dtype != torch.int8 or act.numel() < n_ticks * self.B * 2):
+            raise ValueError("act must be int8 [n_ticks, n_games, 2]")
+        self._call("orx_rollout", int(p1), int(p2), int(n_ticks), _ptr(obs), _ptr(act), self.B,
+                   self.seed, self.game_offset, self._stream())
+
+    # -- host views -----------------------------------------------------------
+    def snapshot(self) -> dict:
+        """Copies the whole SoA state to numpy (synchronizes)."""
+        out = {}
+        for f in STATE_FIELDS:
+            a = getattr(self, f).cpu().numpy()
+            if f == "npc_pos":
+                a = a.view(np.uint16)[: self.K]
+            elif f == "npc_health":
+                a = a[: self.K]
+            elif f == "npc_alive":
+                a = a.view(np.uint32)
+            out[f] = a
+        return out
+
+    def load_snapshot(self, snap: dict) -> None:
+        """Writes host arrays (engine layout) into the device state."""
+        for f in STATE_FIELDS:
+            if f not in snap:
+                continue
+            dst = getattr(self, f)
+            a = np.ascontiguousarray(snap[f])
+            if f == "npc_pos":
+                a = a.astype(np.uint16).view(np.int16)
+                if self.K == 0:
+                    continue
+                dst = dst[: self.K]
+            elif f == "npc_health":
+                if self.K == 0:
+                    continue
+                a = a.astype(np.int8)
+                dst = dst[: self.K]
+            elif f == "npc_alive":
+                a = a.astype(np.uint32).view(np.int32)
+            else:
+                a = a.astype(np.int32)
+            dst.copy_(torch.from_numpy(a.reshape(dst.shape)))
+
+    def episode_returns(self) -> torch.Tensor:
+        """(ret_sum, ep_count) stacked as int32 [2, n_games] (device)."""
+        return torch.stack([self.ret_sum, self.ep_count])

@@ -1,0 +1,70 @@
+"""Integer enums of the reference, same names and values.
+
+Move                       optimax_rogue/logic/moves.py:6-12
+UpdateResult               optimax_rogue/logic/updater.py:16-21
+DungeonDespawningStrategy  optimax_rogue/logic/updater.py:47-50
+Tile                       optimax_rogue/game/world.py:10-17
+CombatFlag                 optimax_rogue/game/modifiers.py:7-12
+"""
+import enum
+
+
+class Move(enum.IntEnum):
+    Up = 1
+    Right = 2
+    Down = 3
+    Left = 4
+    Stay = 5
+
+
+class UpdateResult(enum.IntEnum):
+    InProgress = 1
+    Player1Win = 2
+    Player2Win = 3
+    Tie = 4
+
+
+class DungeonDespawningStrategy(enum.IntEnum):
+    Unreachable = 1
+    Unused = 2
+
+
+class Tile(enum.IntEnum):
+    Ground = 1
+    Wall = 2
+    StaircaseDown = 3
+
+
+class CombatFlag(enum.IntEnum):
+    Block = 1
+    Ambush = 2
+    Flee = 3
+    Parry = 4
+
+
+class StartMode(enum.IntEnum):
+    """Which GameStartGenerator plugin (optimax_rogue/logic/worldgen.py:61-135)."""
+    Together = 1
+    Separated = 2
+
+
+class Policy(enum.IntEnum):
+    """On-device action producers (optimax_rogue_bots/randombot.py, staircasebot.py)."""
+    NONE = 0
+    Random = 1
+    Staircase = 2
+    Stay = 3
+
+
+# build-only per-game status codes (include/orx.h)
+STATUS_BAD_ACTION = 16
+STATUS_RNG_EXHAUSTED = 17
+
+# per-game event counter rows (include/orx.h ORX_CNT_*)
+CNT_COMBAT, CNT_DESCEND, CNT_DUNGEON, CNT_NPC_DEATH = range(4)
+N_COUNTERS = 4
+MAX_NPCS = 16
+
+OBS_FIELDS = ("p1_x", "p1_y", "p1_depth", "p1_health", "p2_x", "p2_y", "p2_depth",
+              "p2_health", "tick", "status", "p1_stair_x", "p1_stair_y", "p2_stair_x",
+              "p2_stair_y")

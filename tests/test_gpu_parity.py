@@ -1,0 +1,211 @@
+"""GPU parity: the HIP engine against the reference's golden fixtures and the
+C oracle (bit-exact; all state is integer)."""
+import numpy as np
+import pytest
+
+from golden_util import STATE_KEYS, Fixture, case_names, compare_state
+
+pytestmark = pytest.mark.gpu
+
+
+def _engine(cfg, n_games, seed, offset=0, reset=True):
+    import torch
+    from optimax_rogue_amd import EnvConfig
+    from optimax_rogue_amd.engine import BatchedEngine
+    return BatchedEngine(EnvConfig.from_dict(cfg), n_games, seed=seed, game_offset=offset,
+                         device=torch.device("cuda", 0), reset=reset)
+
+
+@pytest.mark.parametrize("name", case_names())
+def test_golden_step_by_step(name):
+    """policy kernel + step kernel, tick by tick, vs the reference fixtures."""
+    import torch
+    fx = Fixture(name)
+    eng = _engine(fx.cfg, fx.G, fx.seed, fx.game_offset)
+    compare_state(eng.snapshot(), fx.state(0), fx.K, f"{name} reset")
+    for t in range(fx.T):
+        a = eng.policy(*fx.policy)
+        got = a.cpu().numpy()
+        assert np.array_equal(got, fx.actions[t]), f"{name} policy t={t}"
+        eng.step(a)
+        compare_state(eng.snapshot(), fx.state(t + 1), fx.K, f"{name} t={t + 1}")
+    torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("name", case_names())
+def test_golden_step_given_actions(name):
+    """step kernel driven by the fixture's recorded actions (uploaded once)."""
+    import torch
+    fx = Fixture(name)
+    eng = _engine(fx.cfg, fx.G, fx.seed, fx.game_offset)
+    acts = torch.from_numpy(fx.actions).to(eng.device)
+    for t in range(fx.T):
+        eng.step(acts[t].contiguous())
+    compare_state(eng.snapshot(), fx.state(fx.T), fx.K, f"{name} final")
+
+
+@pytest.mark.parametrize("name", case_names())
+def test_golden_rollout(name):
+    """fused rollout kernel: every tick's observation vs the fixtures."""
+    import torch
+    from optimax_rogue_amd.enums import OBS_FIELDS
+    fx = Fixture(name)
+    eng = _engine(fx.cfg, fx.G, fx.seed, fx.game_offset)
+    # split in two launches to exercise state hand-over between launches
+    t1 = fx.T // 3
+    obs = torch.zeros((fx.T, len(OBS_FIELDS), fx.G), dtype=torch.int32, device=eng.device)
+    act = torch.zeros((fx.T, fx.G, 2), dtype=torch.int8, device=eng.device)
+    eng.rollout(t1, *fx.policy, obs=obs[:t1], act=act[:t1])
+    eng.rollout(fx.T - t1, *fx.policy, obs=obs[t1:], act=act[t1:])
+    o = obs.cpu().numpy()
+    assert np.array_equal(act.cpu().numpy(), fx.actions)
+    for t in range(fx.T):
+        s = fx.state(t + 1)
+        want = np.stack([s["p_x"][0], s["p_y"][0], s["p_depth"][0], s["p_health"][0],
+                         s["p_x"][1], s["p_y"][1], s["p_depth"][1], s["p_health"][1],
+                         s["tick"], s["status"], s["st_x"][0], s["st_y"][0], s["st_x"][1],
+                         s["st_y"][1]])
+        assert np.array_equal(o[t], want), f"{name} obs t={t + 1}"
+    compare_state(eng.snapshot(), fx.state(fx.T), fx.K, f"{name} final")
+
+
+ORACLE_CASES = {
+    "c2_random_32": (dict(width=32, height=32), (1, 1), 4096, 400, 2),
+    "npc_small_unused": (dict(width=7, height=6, n_npcs=5, despawn=2, max_ticks=90), (1, 2),
+                         4096, 300, 11),
+    "separated_stairs": (dict(width=9, height=9, start_mode=2, p1_depth=4, p2_depth=1,
+                              n_npcs=3, max_ticks=200), (2, 2), 2048, 400, 12),
+    "duel_4": (dict(width=4, height=5, max_ticks=0), (1, 1), 4096, 300, 13),
+    "c5_stairs_128": (dict(width=128, height=128), (2, 2), 1024, 600, 5),
+    "npc16_8x8": (dict(width=8, height=8, n_npcs=16, npc_health=2, max_ticks=50), (1, 1), 2048,
+                  200, 14),
+}
+
+
+@pytest.mark.parametrize("name", sorted(ORACLE_CASES))
+def test_vs_oracle_large(name, oracle_lib):
+    """thousands of games: engine (policy+step and rollout) vs the C oracle."""
+    import torch
+    cfg, pol, B, T, seed = ORACLE_CASES[name]
+    ora = oracle_lib.Oracle(cfg, B, seed, 0)
+    ora.reset(episode=np.zeros(B, np.int32))
+    eng = _engine(cfg, B, seed)
+    eng2 = _engine(cfg, B, seed)
+    compare_state(eng.snapshot(), ora.export(), ora.K, f"{name} reset")
+    chunk = T // 4
+    for c in range(4):
+        for _ in range(chunk):
+            a = ora.policy(*pol)
+            ora.step(a)
+            eng.step(eng.policy(*pol))
+        eng2.rollout(chunk, *pol)
+        want = ora.export()
+        compare_state(eng.snapshot(), want, ora.K, f"{name} step chunk {c}")
+        compare_state(eng2.snapshot(), want, ora.K, f"{name} rollout chunk {c}")
+    torch.cuda.synchronize()
+
+
+def test_sharding_invariance():
+    """a game's trajectory depends on its global id only (game_offset)."""
+    cfg = dict(width=10, height=10, n_npcs=3, max_ticks=80)
+    full = _engine(cfg, 3000, 21)
+    a = _engine(cfg, 1000, 21, 0)
+    b = _engine(cfg, 2000, 21, 1000)
+    for e in (full, a, b):
+        e.rollout(250, 1, 2)
+    sf, sa, sb = full.snapshot(), a.snapshot(), b.snapshot()
+    for k in STATE_KEYS:
+        axis = sf[k].ndim - 1
+        assert np.array_equal(sf[k], np.concatenate([sa[k], sb[k]], axis=axis)), k
+
+
+def test_rollout_equals_step_c3():
+    """C3 shape (B=65536, 64x64, K=8): fused rollout == per-tick policy+step."""
+    from optimax_rogue_amd import EnvConfig
+    cfg = EnvConfig.c3().to_dict()
+    e1 = _engine(cfg, 65536, 3)
+    e2 = _engine(cfg, 65536, 3)
+    for _ in range(64):
+        e1.step(e1.policy(1, 1))
+    e2.rollout(64, 1, 1)
+    s1, s2 = e1.snapshot(), e2.snapshot()
+    for k in STATE_KEYS:
+        assert np.array_equal(s1[k], s2[k]), k
+
+
+def _invariants(s, cfg):
+    W, H = cfg["width"], cfg["height"]
+    for p in range(2):
+        assert (s["p_x"][p] >= 1).all() and (s["p_x"][p] <= W - 2).all()
+        assert (s["p_y"][p] >= 1).all() and (s["p_y"][p] <= H - 2).all()
+        assert (s["st_x"][p] >= 1).all() and (s["st_x"][p] <= W - 3).all()
+        assert (s["st_y"][p] >= 1).all() and (s["st_y"][p] <= H - 3).all()
+        # a player never stands on its staircase (it would have descended)
+        assert not ((s["p_x"][p] == s["st_x"][p]) & (s["p_y"][p] == s["st_y"][p])).any()
+    same = ((s["p_depth"][0] == s["p_depth"][1]) & (s["p_x"][0] == s["p_x"][1])
+            & (s["p_y"][0] == s["p_y"][1]))
+    assert not same.any(), "two players on one cell"
+    both_same_depth = s["p_depth"][0] == s["p_depth"][1]
+    assert np.array_equal(s["st_x"][0][both_same_depth], s["st_x"][1][both_same_depth])
+    assert (s["p_health"] <= cfg.get("player_health", 10)).all()
+    assert set(np.unique(s["status"]).tolist()) <= {1, 2, 3, 4}
+
+
+def test_c3_full_size_properties(oracle_lib):
+    """B=65536 at 64x64 with K=8: invariants after 1000 ticks and a sample of
+    games replayed on the oracle by global id."""
+    from optimax_rogue_amd import EnvConfig
+    cfg = EnvConfig.c3().to_dict()
+    B, T = 65536, 1000
+    eng = _engine(cfg, B, 3)
+    eng.rollout(T, 1, 1)
+    s = eng.snapshot()
+    _invariants(s, cfg)
+    assert s["ep_count"].sum() >= B  # max_ticks 1000 -> every game finished once
+    rng = np.random.default_rng(0)
+    for gid in rng.choice(B, 48, replace=False):
+        ora = oracle_lib.Oracle(cfg, 1, 3, int(gid))
+        ora.reset(episode=np.zeros(1, np.int32))
+        ora.rollout(1, 1, T)
+        want = ora.export()
+        got = {k: (v[..., gid:gid + 1]) for k, v in s.items()}
+        compare_state(got, want, 8, f"gid {gid}")
+
+
+def test_bad_action_and_no_autoreset():
+    import torch
+    cfg = dict(width=8, height=8, max_ticks=5, autoreset=0)
+    eng = _engine(cfg, 256, 1)
+    a = torch.full((256, 2), 5, dtype=torch.int8, device=eng.device)
+    a[7, 0] = 0
+    a[9, 1] = 6
+    eng.step(a)
+    st = eng.status.cpu().numpy()
+    assert st[7] == 16 and st[9] == 16 and (np.delete(st, [7, 9]) == 1).all()
+    for _ in range(10):
+        eng.step(eng.policy(1, 1))
+    s = eng.snapshot()
+    ok = np.ones(256, bool)
+    ok[[7, 9]] = False
+    assert (s["tick"][ok] == 5).all() and (s["status"][ok] == 4).all()
+    assert (s["tick"][~ok] == 1).all()   # stopped games stay frozen
+
+
+def test_errors_raise():
+    from optimax_rogue_amd import EnvConfig
+    from optimax_rogue_amd.engine import BatchedEngine
+    import torch
+    with pytest.raises(ValueError):
+        BatchedEngine(EnvConfig(width=3), 16, device=torch.device("cuda", 0))
+    eng = _engine(dict(width=8, height=8), 16, 1)
+    with pytest.raises(ValueError):
+        eng.step(torch.zeros((16, 2), dtype=torch.int32, device=eng.device))
+    from optimax_rogue_amd._lib import OrxError
+    with pytest.raises(OrxError):
+        eng.rollout(4, 0, 1)
+
+
+def test_empty_batch():
+    eng = _engine(dict(width=8, height=8), 0, 1)
+    eng.step(eng.policy(1, 1))
+    eng.rollout(3, 1, 1)
