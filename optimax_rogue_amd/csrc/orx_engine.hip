@@ -3,9 +3,7 @@
 // One lane = one game.  All per-game state is struct-of-arrays with the batch
 // axis contiguous, so every field load/store of a wavefront is one coalesced
 // 256-byte access.  The tick is integer/branch work; there is nothing for the
-// matrix cores.  The kernels are HBM-bound (step, policy) or issue-bound
-// (rollout with state held in registers); see DESIGN.md for the byte
-// accounting.
+// matrix cores.  See DESIGN.md for the byte accounting and the roofline.
 //
 // Reference semantics restated here (paths relative to the reference repo):
 //   Updater.update            optimax_rogue/logic/updater.py:76-162
@@ -32,6 +30,17 @@
 //     index c (+1 past the staircase) -> x = 1 + ci / (H-2), y = 1 + ci % (H-2);
 //   * World.dungeons membership is derived from the players' start and
 //     current depths (DESIGN.md "Dungeon presence").
+//
+// Performance structure (gfx950, one wave per SIMD at the 65,536-game config):
+//   * the common tick is straight-line: the per-tick random words (policy and
+//     initiative streams, two Philox blocks each) are generated unconditionally
+//     and interleaved, accepted words are picked with selects; only lanes that
+//     exhaust 8 words take the generic stream loop (rare);
+//   * Philox rounds use v_mad_u64_u32 (64-bit product) and SGPR key schedule;
+//   * NPC occupancy is a packed 16-bit compare against registers (NCAP slots,
+//     a template parameter: 0, 8 or 16), dead slots hold 0xFFFF (no target);
+//   * rare events (descend, NPC hits, game start) sit behind branches, each
+//     with a single Philox call site.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -47,75 +56,65 @@ namespace {
 // ---------------------------------------------------------------------------
 enum : uint32_t { PUR_INIT = 1, PUR_DUNGEON = 2, PUR_SHUFFLE = 3, PUR_SPAWN = 4, PUR_POLICY = 5 };
 constexpr uint32_t kWordCap = 4096;  // per stream; exceeding it stops the game
+constexpr uint32_t kDeadSlot = 0xFFFFu;
 
 struct Key {
   uint32_t k0, k1;
 };
 
-__device__ __forceinline__ void philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
-                                       Key key, uint32_t& o0, uint32_t& o1, uint32_t& o2,
-                                       uint32_t& o3) {
+struct W4 {
+  uint32_t a, b, c, d;
+};
+
+__device__ __forceinline__ W4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, Key key) {
   uint32_t k0 = key.k0, k1 = key.k1;
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
-    const uint32_t hi0 = __umulhi(0xD2511F53u, c0);
-    const uint32_t lo0 = 0xD2511F53u * c0;
-    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2);
-    const uint32_t lo1 = 0xCD9E8D57u * c2;
-    c0 = hi1 ^ c1 ^ k0;
-    c1 = lo1;
-    c2 = hi0 ^ c3 ^ k1;
-    c3 = lo0;
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+    c1 = (uint32_t)p1;
+    c3 = (uint32_t)p0;
+    c0 = n0;
+    c2 = n2;
     k0 += 0x9E3779B9u;
     k1 += 0xBB67AE85u;
   }
-  o0 = c0; o1 = c1; o2 = c2; o3 = c3;
+  return W4{c0, c1, c2, c3};
 }
 
-// A word stream: counter (game, episode, c2, purpose<<28 | gen<<24 | block).
+__device__ __forceinline__ uint32_t tag(uint32_t purpose, uint32_t gen) {
+  return (purpose << 28) | (gen << 24);
+}
+
+// A lazily evaluated word stream: counter (game, ep, c2, tag | block).
 struct Stream {
   uint32_t c0, c1, c2, c3;
   uint32_t idx;
-  uint32_t w0, w1, w2, w3;
+  W4 w;
 
-  __device__ __forceinline__ void init(uint32_t game, uint32_t ep, uint32_t cc2, uint32_t purpose,
-                                       uint32_t gen) {
-    c0 = game; c1 = ep; c2 = cc2; c3 = (purpose << 28) | (gen << 24); idx = 0;
+  __device__ __forceinline__ void init(uint32_t game, uint32_t ep, uint32_t cc2, uint32_t t,
+                                       uint32_t start = 0) {
+    c0 = game; c1 = ep; c2 = cc2; c3 = t; idx = start;
   }
   __device__ __forceinline__ uint32_t next(Key key) {
     const uint32_t j = idx & 3u;
-    if (j == 0) philox(c0, c1, c2, c3 | (idx >> 2), key, w0, w1, w2, w3);
+    if (j == 0) w = philox(c0, c1, c2, c3 | (idx >> 2), key);
     ++idx;
-    return j == 0 ? w0 : j == 1 ? w1 : j == 2 ? w2 : w3;
+    return j == 0 ? w.a : j == 1 ? w.b : j == 2 ? w.c : w.d;
   }
 };
 
-__device__ __forceinline__ int bit_length(uint32_t n) { return n ? 32 - __clz(n) : 0; }
-
-// CPython Random._randbelow_with_getrandbits(n): getrandbits(k) = w >> (32-k).
-__device__ __forceinline__ uint32_t py_randbelow(Stream& s, Key key, uint32_t n, bool& err) {
-  const int k = bit_length(n);
-  for (uint32_t t = 0; t < kWordCap; ++t) {
-    const uint32_t r = s.next(key) >> (32 - k);
-    if (r < n) return r;
+// numpy legacy RandomState.randint(low, high): rng = high-1-low; rng == 0
+// draws nothing; otherwise masked rejection on 32-bit words.
+struct NpBound {
+  uint32_t rng, mask;
+  __device__ __forceinline__ void set(int32_t n) {  // n = high - low
+    rng = (uint32_t)(n - 1);
+    mask = rng ? 0xFFFFFFFFu >> __clz(rng) : 0u;
   }
-  err = true;
-  return 0;
-}
-
-// numpy legacy RandomState.randint(low, high), masked rejection on 32-bit words.
-__device__ __forceinline__ int32_t np_randint(Stream& s, Key key, int32_t low, int32_t high,
-                                              bool& err) {
-  const uint32_t rng = (uint32_t)(high - 1 - low);
-  if (rng == 0) return low;
-  const uint32_t mask = 0xFFFFFFFFu >> __clz(rng);
-  for (uint32_t t = 0; t < kWordCap; ++t) {
-    const uint32_t v = s.next(key) & mask;
-    if (v <= rng) return low + (int32_t)v;
-  }
-  err = true;
-  return low;
-}
+};
 
 // ---------------------------------------------------------------------------
 // Per-game registers
@@ -123,92 +122,89 @@ __device__ __forceinline__ int32_t np_randint(Stream& s, Key key, int32_t low, i
 struct Player {
   int32_t x, y, d, hp, sx, sy;
   int32_t move;   // validated move for this tick
-  int32_t start;  // start depth of the episode (dungeon presence rule)
 };
 
-struct Cfg {  // device copy of orx_cfg_t plus derived constants
+// Field-wise select: a conditional copy of the whole struct would be lowered
+// through scratch memory (two allocas + pointer select).
+__device__ __forceinline__ Player pick(bool c, const Player& a, const Player& b) {
+  Player r;
+  r.x = c ? a.x : b.x;
+  r.y = c ? a.y : b.y;
+  r.d = c ? a.d : b.d;
+  r.hp = c ? a.hp : b.hp;
+  r.sx = c ? a.sx : b.sx;
+  r.sy = c ? a.sy : b.sy;
+  r.move = c ? a.move : b.move;
+  return r;
+}
+
+struct Cfg {  // device copy of orx_cfg_t plus derived constants (all wave-uniform)
   int32_t W, H, despawn, max_ticks, start_mode, d1, d2, K;
   int32_t npc_hp, player_hp, player_dmg_net, autoreset;
-  int32_t n_ground;  // (W-2)(H-2) - 1 Ground tiles per dungeon
+  int32_t ih;        // H - 2 (interior column height)
+  NpBound ground;    // randint(n_ground), n_ground = (W-2)(H-2) - 1
+  NpBound stair_x;   // randint(1, W-2)
+  NpBound stair_y;   // randint(1, H-2)
 };
 
 struct Deltas {  // counter / return increments, flushed once per launch
-  int32_t c0, c1, c2, c3, ret, eps;
+  int32_t combat, descend, dungeon, npc_death, ret, eps;
 };
 
-// NPC slots: positions either cached in registers (rollout) or read from HBM
-// on demand (step).  Dead slots are never consulted (alive mask).
-template <bool kReg>
+// NPC slots in registers: packed (x | y << 8) u16 pairs; dead slot = 0xFFFF,
+// which no legal target can equal (targets are interior cells, x, y <= 254).
+template <int NCAP>
 struct Npcs {
+  static constexpr int kRegs = NCAP > 0 ? NCAP / 2 : 1;
+  // named registers (an array would be demoted to scratch by SROA)
+  uint32_t q0, q1, q2, q3, q4, q5, q6, q7;
   uint32_t alive;
-  uint32_t pos[kReg ? ORX_MAX_NPCS / 2 : 1];  // two packed u16 per register
-  const uint16_t* gpos;
-  int8_t* ghp;
-  int64_t B, i;
-  int32_t K;
 
-  __device__ __forceinline__ void load(const orx_state_t& st, int32_t KK, int64_t BB, int64_t ii) {
-    K = KK; B = BB; i = ii;
-    gpos = st.npc_pos; ghp = st.npc_health;
-    alive = K ? st.npc_alive[i] : 0u;
-    if constexpr (kReg) {
-#pragma unroll
-      for (int k = 0; k < ORX_MAX_NPCS / 2; ++k) pos[k] = 0xFFFFFFFFu;
-#pragma unroll
-      for (int k = 0; k < ORX_MAX_NPCS; ++k)
-        if (k < K) set_pos_reg(k, gpos[(int64_t)k * B + i]);
+  __device__ __forceinline__ uint32_t rd(int r) const {
+    switch (r) {
+      case 0: return q0; case 1: return q1; case 2: return q2; case 3: return q3;
+      case 4: return q4; case 5: return q5; case 6: return q6; default: return q7;
     }
   }
-  __device__ __forceinline__ void set_pos_reg(int k, uint32_t v) {
-    if constexpr (kReg) {
-      const int r = k >> 1, sh = (k & 1) * 16;
-      pos[r] = (pos[r] & ~(0xFFFFu << sh)) | ((v & 0xFFFFu) << sh);
+  __device__ __forceinline__ void wr(int r, uint32_t v) {
+    switch (r) {
+      case 0: q0 = v; break; case 1: q1 = v; break; case 2: q2 = v; break;
+      case 3: q3 = v; break; case 4: q4 = v; break; case 5: q5 = v; break;
+      case 6: q6 = v; break; default: q7 = v; break;
     }
   }
-  // Slot of the NPC at (x, y) on the NPC depth, or -1.
-  __device__ __forceinline__ int find(int32_t x, int32_t y) const {
-    if (!alive) return -1;
-    const uint32_t key = (uint32_t)(x & 0xFF) | ((uint32_t)(y & 0xFF) << 8);
-    if (x < 0 || y < 0 || x > 255 || y > 255) return -1;
-    int hit = -1;
-    if constexpr (kReg) {
-#pragma unroll
-      for (int k = 0; k < ORX_MAX_NPCS; ++k) {
-        const uint32_t v = (pos[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu;
-        if (k < K && ((alive >> k) & 1u) && v == key) hit = k;
-      }
+  __device__ __forceinline__ void clear() {
+    q0 = q1 = q2 = q3 = q4 = q5 = q6 = q7 = 0xFFFFFFFFu;
+    alive = 0;
+  }
+  __device__ __forceinline__ uint32_t get(int k) const {
+    return (rd(k >> 1) >> ((k & 1) * 16)) & 0xFFFFu;
+  }
+  __device__ __forceinline__ void set(int k, uint32_t v) {
+    const int sh = (k & 1) * 16;
+    wr(k >> 1, (rd(k >> 1) & ~(0xFFFFu << sh)) | ((v & 0xFFFFu) << sh));
+  }
+  // Slot holding `key` (a live NPC), or -1.
+  __device__ __forceinline__ int find(uint32_t key) const {
+    if constexpr (NCAP == 0) {
+      return -1;
     } else {
-      for (int k = 0; k < K; ++k)
-        if (((alive >> k) & 1u) && (uint32_t)gpos[(int64_t)k * B + i] == key) hit = k;
+      const uint32_t k2 = key | (key << 16);
+      uint32_t hitmask = 0;
+#pragma unroll
+      for (int r = 0; r < kRegs; ++r) {
+        const uint32_t x = rd(r) ^ k2;
+        const uint32_t lo = (x & 0xFFFFu) == 0 ? 1u : 0u;
+        const uint32_t hi = (x >> 16) == 0 ? 2u : 0u;
+        hitmask |= (lo | hi) << (2 * r);
+      }
+      return hitmask ? (int)__ffs(hitmask) - 1 : -1;
     }
-    return hit;
-  }
-  __device__ __forceinline__ void store_pos(int k, uint32_t v) {
-    const_cast<uint16_t*>(gpos)[(int64_t)k * B + i] = (uint16_t)v;
-    set_pos_reg(k, v);
   }
 };
 
-// Dungeon staircase from the keyed stream (episode, depth, generation):
-// EmptyDungeonGenerator.spawn_dungeon draws randint(1, W-2) then randint(1, H-2).
-__device__ __forceinline__ void dungeon_stair(const Cfg& c, Key key, uint32_t game, uint32_t ep,
-                                              int32_t depth, uint32_t gen, int32_t& sx,
-                                              int32_t& sy, bool& err) {
-  Stream s;
-  s.init(game, ep, (uint32_t)depth, PUR_DUNGEON, gen);
-  sx = np_randint(s, key, 1, c.W - 2, err);
-  sy = np_randint(s, key, 1, c.H - 2, err);
-}
-
-// get_random_unblocked on the dungeon with staircase (sx, sy).
-__device__ __forceinline__ void random_ground(const Cfg& c, Stream& s, Key key, int32_t sx,
-                                              int32_t sy, int32_t& x, int32_t& y, bool& err) {
-  const int32_t ih = c.H - 2;
-  const int32_t ch = np_randint(s, key, 0, c.n_ground, err);
-  const int32_t s_idx = (sx - 1) * ih + (sy - 1);
-  const int32_t ci = ch + (ch >= s_idx ? 1 : 0);
-  x = 1 + ci / ih;
-  y = 1 + ci - (ci / ih) * ih;
+__device__ __forceinline__ uint32_t pack_xy(int32_t x, int32_t y) {
+  return (uint32_t)(x & 0xFF) | ((uint32_t)(y & 0xFF) << 8);
 }
 
 __device__ __forceinline__ void calc_pos(int32_t x, int32_t y, int32_t m, int32_t& nx, int32_t& ny) {
@@ -220,60 +216,99 @@ __device__ __forceinline__ bool blocked(const Cfg& c, int32_t x, int32_t y) {
   return x <= 0 || x >= c.W - 1 || y <= 0 || y >= c.H - 1;
 }
 
-// ---------------------------------------------------------------------------
-// Game start (setup_game + NPC spawner)
-// ---------------------------------------------------------------------------
-template <bool kReg>
-__device__ __forceinline__ void setup_game(const Cfg& c, Key key, uint32_t game, uint32_t ep,
-                                           Player& p1, Player& p2, Npcs<kReg>& npc,
-                                           int32_t& tick, int32_t& status) {
-  bool err = false;
+// c-th Ground tile of the dungeon with staircase (sx, sy), x-major order.
+__device__ __forceinline__ void ground_cell(const Cfg& c, uint32_t ch, int32_t sx, int32_t sy,
+                                            int32_t& x, int32_t& y) {
+  const uint32_t s_idx = (uint32_t)((sx - 1) * c.ih + (sy - 1));
+  const uint32_t ci = ch + (ch >= s_idx ? 1u : 0u);
+  const uint32_t q = ci / (uint32_t)c.ih;
+  x = 1 + (int32_t)q;
+  y = 1 + (int32_t)(ci - q * (uint32_t)c.ih);
+}
+
+// EmptyDungeonGenerator.spawn_dungeon with words from (episode, depth, gen):
+// randint(1, W-2) then randint(1, H-2).  One loop, one Philox call site.
+__device__ __forceinline__ void dungeon_stair(const Cfg& c, Key key, uint32_t game, uint32_t ep,
+                                           int32_t depth, uint32_t gen, int32_t& sx, int32_t& sy,
+                                           bool& err) {
   Stream s;
-  s.init(game, ep, 0, PUR_INIT, 0);
-  if (c.start_mode == ORX_START_SEPARATED) {
-    p1.d = c.d1; p2.d = c.d2;
-    dungeon_stair(c, key, game, ep, c.d1, 0, p1.sx, p1.sy, err);
-    dungeon_stair(c, key, game, ep, c.d2, 0, p2.sx, p2.sy, err);
-    random_ground(c, s, key, p1.sx, p1.sy, p1.x, p1.y, err);
-    random_ground(c, s, key, p2.sx, p2.sy, p2.x, p2.y, err);
+  s.init(game, ep, (uint32_t)depth, tag(PUR_DUNGEON, gen));
+  int n = 0;
+  int32_t v0 = 0, v1 = 0;
+  for (uint32_t t = 0; t < 2 * kWordCap && n < 2; ++t) {
+    const NpBound b = n == 0 ? c.stair_x : c.stair_y;
+    uint32_t v = 0;
+    if (b.rng != 0) {  // rng 0 consumes no word
+      v = s.next(key) & b.mask;
+      if (v > b.rng) continue;
+    }
+    if (n == 0) v0 = (int32_t)v; else v1 = (int32_t)v;
+    ++n;
+  }
+  if (n < 2) err = true;
+  sx = 1 + v0;
+  sy = 1 + v1;
+}
+
+// ---------------------------------------------------------------------------
+// Game start (setup_game + NPC spawner), all placements in one rejection loop
+// over the INIT stream (one Philox call site, one division site).
+// ---------------------------------------------------------------------------
+template <int NCAP>
+__device__ __forceinline__ void setup_game(const Cfg& c, Key key, uint32_t game, uint32_t ep,
+                                        Player& p1, Player& p2, Npcs<NCAP>& npc, int32_t& tick,
+                                        int32_t& status) {
+  bool err = false;
+  const bool sep = c.start_mode == ORX_START_SEPARATED;
+  p1.d = sep ? c.d1 : 0;
+  p2.d = sep ? c.d2 : 0;
+  dungeon_stair(c, key, game, ep, p1.d, 0, p1.sx, p1.sy, err);
+  if (sep) {
+    dungeon_stair(c, key, game, ep, p2.d, 0, p2.sx, p2.sy, err);
   } else {
-    p1.d = 0; p2.d = 0;
-    dungeon_stair(c, key, game, ep, 0, 0, p1.sx, p1.sy, err);
     p2.sx = p1.sx; p2.sy = p1.sy;
-    random_ground(c, s, key, p1.sx, p1.sy, p1.x, p1.y, err);
-    for (uint32_t t = 0; t < kWordCap; ++t) {
-      random_ground(c, s, key, p2.sx, p2.sy, p2.x, p2.y, err);
-      if (p2.x != p1.x || p2.y != p1.y) break;
-      if (t + 1 == kWordCap) err = true;
-    }
   }
-  p1.start = p1.d; p2.start = p2.d;
-  p1.hp = c.player_hp; p2.hp = c.player_hp;
-  // NPC spawner: K NPCs on player 1's start depth, redrawn while occupied.
-  uint32_t alive = 0;
-  for (int k = 0; k < c.K; ++k) {
-    int32_t x = 0, y = 0;
-    for (uint32_t t = 0; t < kWordCap; ++t) {
-      random_ground(c, s, key, p1.sx, p1.sy, x, y, err);
-      bool occ = (x == p1.x && y == p1.y) || (p2.d == p1.d && x == p2.x && y == p2.y);
-      for (int j = 0; j < k; ++j) {
-        const uint32_t v = npc.gpos[(int64_t)j * npc.B + npc.i];
-        occ = occ || (v == ((uint32_t)x | ((uint32_t)y << 8)));
-      }
-      if (!occ) break;
-      if (t + 1 == kWordCap) err = true;
+  npc.clear();
+  Stream s;
+  s.init(game, ep, 0, tag(PUR_INIT, 0));
+  const int total = 2 + (NCAP ? c.K : 0);
+  int placed = 0;
+  p1.x = p1.y = p2.x = p2.y = 0;
+  for (uint32_t t = 0; t < kWordCap && placed < total; ++t) {
+    uint32_t v = 0;
+    if (c.ground.rng != 0) {
+      v = s.next(key) & c.ground.mask;
+      if (v > c.ground.rng) continue;
     }
-    npc.store_pos(k, (uint32_t)x | ((uint32_t)y << 8));
-    npc.ghp[(int64_t)k * npc.B + npc.i] = (int8_t)c.npc_hp;
-    alive |= 1u << k;
+    // placement 0: player 1, 1: player 2, 2+k: NPC k (all NPCs on p1's depth)
+    const bool is_p2 = placed == 1;
+    const int32_t sx = is_p2 ? p2.sx : p1.sx, sy = is_p2 ? p2.sy : p1.sy;
+    int32_t x, y;
+    ground_cell(c, v, sx, sy, x, y);
+    bool occ = false;
+    if (placed >= 1) occ = x == p1.x && y == p1.y && (placed >= 2 || !sep);
+    if (placed >= 2) {
+      occ = occ || (p2.d == p1.d && x == p2.x && y == p2.y);
+      occ = occ || npc.find(pack_xy(x, y)) >= 0;
+    }
+    if (occ) continue;
+    if (placed == 0) { p1.x = x; p1.y = y; }
+    else if (placed == 1) { p2.x = x; p2.y = y; }
+    else if constexpr (NCAP > 0) {
+      npc.set(placed - 2, pack_xy(x, y));
+      npc.alive |= 1u << (placed - 2);
+    }
+    ++placed;
   }
-  npc.alive = alive;
+  if (placed < total) err = true;
+  p1.hp = c.player_hp;
+  p2.hp = c.player_hp;
   tick = 1;
   status = err ? ORX_STATUS_RNG_EXHAUSTED : ORX_IN_PROGRESS;
 }
 
 // ---------------------------------------------------------------------------
-// The tick
+// Descend (rare): dungeon presence, staircase, spawn cell
 // ---------------------------------------------------------------------------
 // Dungeon presence when `self` enters depth nd (derivation in DESIGN.md):
 //   Unreachable: World has nd iff the other player has been on nd
@@ -281,18 +316,18 @@ __device__ __forceinline__ void setup_game(const Cfg& c, Key key, uint32_t game,
 //   Unused:      World == {p1.d, p2.d}, so nd is present iff other.d == nd;
 //                a fresh copy is generation 1 iff the other player already
 //                passed through nd (other.start <= nd < other.d).
-template <bool kReg>
+template <int NCAP>
 __device__ __forceinline__ void descend(const Cfg& c, Key key, uint32_t game, uint32_t ep,
-                                        Player& self, const Player& other, Npcs<kReg>& npc,
-                                        Stream& spawn, Deltas& dl, bool& err) {
+                                     Player& self, const Player& other, int32_t other_start,
+                                     const Npcs<NCAP>& npc, Stream& spawn, Deltas& dl, bool& err) {
   const int32_t nd = self.d + 1;
   bool present;
   uint32_t gen = 0;
   if (c.despawn == ORX_DESPAWN_UNREACHABLE) {
-    present = other.start <= nd && nd <= other.d;
+    present = other_start <= nd && nd <= other.d;
   } else {
     present = other.d == nd;
-    gen = (!present && other.start <= nd && nd < other.d) ? 1u : 0u;
+    gen = (!present && other_start <= nd && nd < other.d) ? 1u : 0u;
   }
   int32_t sx, sy;
   if (present && other.d == nd) {
@@ -300,97 +335,195 @@ __device__ __forceinline__ void descend(const Cfg& c, Key key, uint32_t game, ui
   } else {
     dungeon_stair(c, key, game, ep, nd, gen, sx, sy, err);
   }
-  if (!present) dl.c2 += 1;
-  const bool npc_depth = nd == c.d1 && npc.alive;
+  if (!present) dl.dungeon += 1;
+  const bool npc_depth = NCAP > 0 && nd == c.d1 && npc.alive;
   int32_t x = 0, y = 0;
-  for (uint32_t t = 0; t < kWordCap; ++t) {
-    random_ground(c, spawn, key, sx, sy, x, y, err);
+  bool done = false;
+  for (uint32_t t = 0; t < kWordCap && !done; ++t) {
+    uint32_t v = 0;
+    if (c.ground.rng != 0) {
+      v = spawn.next(key) & c.ground.mask;
+      if (v > c.ground.rng) continue;
+    }
+    ground_cell(c, v, sx, sy, x, y);
     bool occ = other.d == nd && other.x == x && other.y == y;
-    if (!occ && npc_depth) occ = npc.find(x, y) >= 0;
-    if (!occ) break;
-    if (t + 1 == kWordCap) err = true;
+    if (npc_depth) occ = occ || npc.find(pack_xy(x, y)) >= 0;
+    done = !occ;
   }
+  if (!done) err = true;
   self.d = nd; self.x = x; self.y = y; self.sx = sx; self.sy = sy;
-  dl.c1 += 1;
+  dl.descend += 1;
 }
 
-// handle_move for `self`; `self_first` = self acted before `other`.
-template <bool kReg>
-__device__ __forceinline__ void handle_move(const Cfg& c, Key key, uint32_t game, uint32_t ep,
-                                            Player& self, Player& other, Npcs<kReg>& npc,
-                                            Stream& spawn, Deltas& dl, int& hit0, int& hit1,
-                                            bool& err) {
-  if (self.move == ORX_MOVE_STAY) return;
+// ---------------------------------------------------------------------------
+// Random words of one tick
+// ---------------------------------------------------------------------------
+// RandomBot.move = Move(1 + randbelow(5)): k = 3, r = w >> 29, accept r < 5.
+// Both players draw from the POLICY stream in order (p1 first).  Fast path:
+// two Philox blocks (8 words); lanes still short take the stream loop.
+__device__ __forceinline__ void random_moves(Key key, uint32_t game, uint32_t ep, int32_t tick,
+                                             int need, int32_t& m0, int32_t& m1, bool& err) {
+  const uint32_t t = tag(PUR_POLICY, 0);
+  const W4 b0 = philox(game, ep, (uint32_t)tick, t | 0u, key);
+  const W4 b1 = philox(game, ep, (uint32_t)tick, t | 1u, key);
+  const uint32_t w[8] = {b0.a, b0.b, b0.c, b0.d, b1.a, b1.b, b1.c, b1.d};
+  int got = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint32_t r = w[i] >> 29;
+    const bool acc = r < 5u;
+    m1 = (acc && got == 1) ? (int32_t)r + 1 : m1;
+    m0 = (acc && got == 0) ? (int32_t)r + 1 : m0;
+    got += (acc && got < 2) ? 1 : 0;
+  }
+  if (got < need) {  // rare: continue the stream at word 8
+    Stream s;
+    s.init(game, ep, (uint32_t)tick, t, 8);
+    for (uint32_t i = 8; i < kWordCap && got < need; ++i) {
+      const uint32_t r = s.next(key) >> 29;
+      if (r >= 5u) continue;
+      if (got == 0) m0 = (int32_t)r + 1; else m1 = (int32_t)r + 1;
+      ++got;
+    }
+    if (got < need) err = true;
+  }
+}
+
+// random.shuffle([p1, p2]) = one randbelow(2): k = 2, r = w >> 30, accept
+// r < 2; player 1 acts first iff r == 1 (updater.py:114).
+__device__ __forceinline__ bool p1_first_draw(Key key, uint32_t game, uint32_t ep, int32_t tick,
+                                              bool& err) {
+  const uint32_t t = tag(PUR_SHUFFLE, 0);
+  const W4 b0 = philox(game, ep, (uint32_t)tick, t | 0u, key);
+  const W4 b1 = philox(game, ep, (uint32_t)tick, t | 1u, key);
+  const uint32_t w[8] = {b0.a, b0.b, b0.c, b0.d, b1.a, b1.b, b1.c, b1.d};
+  int res = -1;
+#pragma unroll
+  for (int i = 7; i >= 0; --i) res = (w[i] >> 31) == 0 ? (int)((w[i] >> 30) & 1u) : res;
+  if (res < 0) {  // rare (1/256): continue the stream at word 8
+    Stream s;
+    s.init(game, ep, (uint32_t)tick, t, 8);
+    for (uint32_t i = 8; i < kWordCap && res < 0; ++i) {
+      const uint32_t r = s.next(key) >> 30;
+      if (r < 2u) res = (int)r;
+    }
+    if (res < 0) { err = true; res = 0; }
+  }
+  return res == 1;
+}
+
+// RandomBot / StaircaseBot moves for both players (policy codes ORX_POLICY_*).
+__device__ __forceinline__ void policy_pair(Key key, uint32_t game, uint32_t ep, int32_t tick,
+                                            int32_t pol1, int32_t pol2, const Player& p1,
+                                            const Player& p2, int32_t& a1, int32_t& a2) {
+  const int need = (pol1 == ORX_POLICY_RANDOM) + (pol2 == ORX_POLICY_RANDOM);
+  int32_t r0 = ORX_MOVE_STAY, r1 = ORX_MOVE_STAY;
+  bool err = false;
+  if (need) random_moves(key, game, ep, tick, need, r0, r1, err);
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int32_t pol = p == 0 ? pol1 : pol2;
+    const Player& me = p == 0 ? p1 : p2;
+    int32_t a = p == 0 ? a1 : a2;
+    if (pol == ORX_POLICY_RANDOM) {
+      a = (p == 1 && pol1 == ORX_POLICY_RANDOM) ? r1 : r0;
+    } else if (pol == ORX_POLICY_STAIRCASE) {
+      const int32_t dx = me.sx - me.x, dy = me.sy - me.y;
+      const int32_t adx = dx < 0 ? -dx : dx, ady = dy < 0 ? -dy : dy;
+      a = adx > ady ? (dx > 0 ? ORX_MOVE_RIGHT : ORX_MOVE_LEFT)
+                    : (dy > 0 ? ORX_MOVE_DOWN : ORX_MOVE_UP);
+    } else if (pol == ORX_POLICY_STAY) {
+      a = ORX_MOVE_STAY;
+    }
+    if (p == 0) a1 = a; else a2 = a;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// The tick
+// ---------------------------------------------------------------------------
+struct NpcMem {  // HBM rows of this game's NPC slots (stride B)
+  uint16_t* pos;
+  int8_t* hp;
+  uint32_t B, i;
+};
+
+// handle_move for `self` (updater.py:180-243).  Returns the NPC slot hit (or
+// -1); combat against the other player is applied here.
+template <int NCAP>
+__device__ __forceinline__ int handle_move(const Cfg& c, Key key, uint32_t game, uint32_t ep,
+                                           Player& self, Player& other, int32_t other_start,
+                                           const Npcs<NCAP>& npc, Stream& spawn, Deltas& dl,
+                                           bool& err) {
+  if (self.move == ORX_MOVE_STAY) return -1;
   int32_t tx, ty;
   calc_pos(self.x, self.y, self.move, tx, ty);
   const bool occ_other = other.d == self.d && other.x == tx && other.y == ty;
   int slot = -1;
-  if (!occ_other && self.d == c.d1) slot = npc.find(tx, ty);
-  if (!occ_other && slot < 0) {
-    if (tx == self.sx && ty == self.sy) {
-      descend(c, key, game, ep, self, other, npc, spawn, dl, err);
-    } else {
-      self.x = tx; self.y = ty;
-    }
-    return;
+  if (NCAP > 0 && self.d == c.d1 && !occ_other) slot = npc.find(pack_xy(tx, ty));
+  const bool free = !occ_other && slot < 0;
+  const bool stairs = free && tx == self.sx && ty == self.sy;
+  if (free && !stairs) { self.x = tx; self.y = ty; }
+  if (!free) {
+    // Block / Parry / Ambush / Flee (updater.py:222-243): without a Modifier
+    // subclass every flag deals og_dmg = attacker.damage - attacker.armor.
+    dl.combat += 1;
+    if (occ_other && c.player_dmg_net > 0) other.hp -= c.player_dmg_net;
   }
-  // Occupied: Block / Parry / Ambush / Flee (updater.py:222-243).  Without a
-  // Modifier subclass every flag deals og_dmg = damage - armor of the attacker.
-  dl.c0 += 1;
-  const int32_t dmg = c.player_dmg_net;
-  if (occ_other) {
-    if (dmg > 0) other.hp -= dmg;
-  } else {
-    if (dmg > 0) {
-      int8_t* h = &npc.ghp[(int64_t)slot * npc.B + npc.i];
-      *h = (int8_t)(*h - dmg);
+  if (stairs) descend(c, key, game, ep, self, other, other_start, npc, spawn, dl, err);
+  return slot;
+}
+
+// handle_combat on NPC defenders, then the death sweep (updater.py:136-145):
+// only NPCs hit this tick can reach health <= 0.
+template <int NCAP>
+__device__ __forceinline__ void npc_hits(const Cfg& c, Npcs<NCAP>& npc, const NpcMem& m, int h0,
+                                      int h1, Deltas& dl) {
+  const int dmg = c.player_dmg_net > 0 ? c.player_dmg_net : 0;
+  for (int j = 0; j < 2; ++j) {
+    const int k = j == 0 ? h0 : h1;
+    if (k < 0) continue;
+    int8_t* h = m.hp + (size_t)k * m.B + m.i;
+    const int8_t nh = (int8_t)(*h - dmg);
+    *h = nh;
+    if (nh <= 0 && ((npc.alive >> k) & 1u)) {
+      npc.alive &= ~(1u << k);
+      npc.set(k, kDeadSlot);
+      dl.npc_death += 1;
     }
-    if (hit0 < 0) hit0 = slot; else hit1 = slot;
   }
 }
 
-// One Updater.update for an in-progress game with validated raw moves a1, a2.
-template <bool kReg>
+// One Updater.update for an in-progress game; p1.move/p2.move = raw moves.
+template <int NCAP>
 __device__ __forceinline__ void tick_game(const Cfg& c, Key key, uint32_t game, uint32_t ep,
-                                          Player& p1, Player& p2, Npcs<kReg>& npc,
-                                          int32_t& tick, int32_t& status, Deltas& dl) {
+                                          Player& p1, Player& p2, Npcs<NCAP>& npc,
+                                          const NpcMem& m, int32_t& tick, int32_t& status,
+                                          Deltas& dl) {
   bool err = false;
-  // illegal moves become Stay (updater.py:89-98)
   int32_t nx, ny;
-  calc_pos(p1.x, p1.y, p1.move, nx, ny);
+  calc_pos(p1.x, p1.y, p1.move, nx, ny);               // updater.py:89-98
   if (blocked(c, nx, ny)) p1.move = ORX_MOVE_STAY;
   calc_pos(p2.x, p2.y, p2.move, nx, ny);
   if (blocked(c, nx, ny)) p2.move = ORX_MOVE_STAY;
 
-  // random.shuffle of the two players: p1 first iff randbelow(2) == 1
-  // (updater.py:114).  The NPC shuffle (:127) draws later words of the same
-  // per-tick stream and only orders Stay-ing NPCs, so it has no observable
-  // effect and is not evaluated.
-  Stream sh;
-  sh.init(game, ep, (uint32_t)tick, PUR_SHUFFLE, 0);
-  const bool p1_first = py_randbelow(sh, key, 2, err) == 1;
+  // The NPC shuffle (updater.py:127) draws later words of the same per-tick
+  // stream and only orders Stay-ing NPCs, so it is unobservable and skipped.
+  const bool p1_first = p1_first_draw(key, game, ep, tick, err);
 
   Stream spawn;
-  spawn.init(game, ep, (uint32_t)tick, PUR_SPAWN, 0);
-  int hit0 = -1, hit1 = -1;
-  // Resolve in initiative order with static register indices: A acts first.
-  Player A = p1_first ? p1 : p2;
-  Player Bp = p1_first ? p2 : p1;
-  handle_move(c, key, game, ep, A, Bp, npc, spawn, dl, hit0, hit1, err);
-  handle_move(c, key, game, ep, Bp, A, npc, spawn, dl, hit0, hit1, err);
-  p1 = p1_first ? A : Bp;
-  p2 = p1_first ? Bp : A;
+  spawn.init(game, ep, (uint32_t)tick, tag(PUR_SPAWN, 0));
+  Player A = pick(p1_first, p1, p2);
+  Player Bp = pick(p1_first, p2, p1);
+  const int32_t a_start = p1_first ? c.d1 : c.d2;
+  const int32_t b_start = p1_first ? c.d2 : c.d1;
+  const int h0 = handle_move(c, key, game, ep, A, Bp, b_start, npc, spawn, dl, err);
+  const int h1 = handle_move(c, key, game, ep, Bp, A, a_start, npc, spawn, dl, err);
+  p1 = pick(p1_first, A, Bp);
+  p2 = pick(p1_first, Bp, A);
+  if (NCAP > 0 && (h0 >= 0 || h1 >= 0)) npc_hits(c, npc, m, h0, h1, dl);
 
-  // NPC death sweep (updater.py:136-145): only NPCs hit this tick can die.
-  if (hit0 >= 0) {
-    const int8_t h0 = npc.ghp[(int64_t)hit0 * npc.B + npc.i];
-    if (h0 <= 0 && ((npc.alive >> hit0) & 1u)) { npc.alive &= ~(1u << hit0); dl.c3 += 1; }
-    if (hit1 >= 0) {
-      const int8_t h1 = npc.ghp[(int64_t)hit1 * npc.B + npc.i];
-      if (h1 <= 0 && ((npc.alive >> hit1) & 1u)) { npc.alive &= ~(1u << hit1); dl.c3 += 1; }
-    }
-  }
-  tick += 1;
+  tick += 1;                                           // updater.py:148-162
   if (p1.hp <= 0)
     status = p2.hp <= 0 ? ORX_TIE : ORX_PLAYER2_WIN;
   else if (p2.hp <= 0)
@@ -401,42 +534,15 @@ __device__ __forceinline__ void tick_game(const Cfg& c, Key key, uint32_t game, 
     status = ORX_IN_PROGRESS;
   if (err) status = ORX_STATUS_RNG_EXHAUSTED;
   if (status != ORX_IN_PROGRESS) {
-    if (status == ORX_PLAYER1_WIN) dl.ret += 1;
-    if (status == ORX_PLAYER2_WIN) dl.ret -= 1;
-    if (status >= ORX_PLAYER1_WIN && status <= ORX_TIE) dl.eps += 1;
-  }
-}
-
-// RandomBot / StaircaseBot for both players (stream POLICY keyed by tick).
-__device__ __forceinline__ void policy_pair(Key key, uint32_t game, uint32_t ep, int32_t tick,
-                                            int32_t pol1, int32_t pol2, const Player& p1,
-                                            const Player& p2, int32_t& a1, int32_t& a2) {
-  Stream s;
-  s.init(game, ep, (uint32_t)tick, PUR_POLICY, 0);
-  bool err = false;
-#pragma unroll
-  for (int p = 0; p < 2; ++p) {
-    const int32_t pol = p == 0 ? pol1 : pol2;
-    const Player& me = p == 0 ? p1 : p2;
-    int32_t a = p == 0 ? a1 : a2;
-    if (pol == ORX_POLICY_RANDOM) {
-      a = 1 + (int32_t)py_randbelow(s, key, 5, err);
-    } else if (pol == ORX_POLICY_STAIRCASE) {
-      const int32_t dx = me.sx - me.x, dy = me.sy - me.y;
-      const int32_t adx = dx < 0 ? -dx : dx, ady = dy < 0 ? -dy : dy;
-      if (adx > ady) a = dx > 0 ? ORX_MOVE_RIGHT : ORX_MOVE_LEFT;
-      else a = dy > 0 ? ORX_MOVE_DOWN : ORX_MOVE_UP;
-    } else if (pol == ORX_POLICY_STAY) {
-      a = ORX_MOVE_STAY;
-    }
-    if (p == 0) a1 = a; else a2 = a;
+    dl.ret += status == ORX_PLAYER1_WIN ? 1 : status == ORX_PLAYER2_WIN ? -1 : 0;
+    dl.eps += (status >= ORX_PLAYER1_WIN && status <= ORX_TIE) ? 1 : 0;
   }
 }
 
 // ---------------------------------------------------------------------------
-// SoA load / store helpers
+// SoA load / store helpers (32-bit lane index: B < 2^31)
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void load_players(const orx_state_t& st, int64_t B, int64_t i,
+__device__ __forceinline__ void load_players(const orx_state_t& st, uint32_t B, uint32_t i,
                                              Player& p1, Player& p2) {
   p1.x = st.p_x[i];           p2.x = st.p_x[B + i];
   p1.y = st.p_y[i];           p2.y = st.p_y[B + i];
@@ -446,9 +552,8 @@ __device__ __forceinline__ void load_players(const orx_state_t& st, int64_t B, i
   p1.sy = st.st_y[i];         p2.sy = st.st_y[B + i];
 }
 
-__device__ __forceinline__ void store_players(const orx_state_t& st, int64_t B, int64_t i,
-                                              const Player& p1, const Player& p2,
-                                              bool stairs) {
+__device__ __forceinline__ void store_players(const orx_state_t& st, uint32_t B, uint32_t i,
+                                              const Player& p1, const Player& p2, bool stairs) {
   st.p_x[i] = p1.x;           st.p_x[B + i] = p2.x;
   st.p_y[i] = p1.y;           st.p_y[B + i] = p2.y;
   st.p_depth[i] = p1.d;       st.p_depth[B + i] = p2.d;
@@ -459,13 +564,39 @@ __device__ __forceinline__ void store_players(const orx_state_t& st, int64_t B, 
   }
 }
 
-__device__ __forceinline__ void flush_deltas(const orx_state_t& st, int64_t B, int64_t i,
+template <int NCAP>
+__device__ __forceinline__ void load_npcs(const orx_state_t& st, const Cfg& c, uint32_t B,
+                                          uint32_t i, Npcs<NCAP>& npc) {
+  npc.clear();
+  if constexpr (NCAP > 0) {
+    npc.alive = st.npc_alive[i];
+#pragma unroll
+    for (int k = 0; k < NCAP; ++k) {
+      const uint32_t v = k < c.K ? (uint32_t)st.npc_pos[(size_t)k * B + i] : kDeadSlot;
+      npc.set(k, ((npc.alive >> k) & 1u) ? v : kDeadSlot);
+    }
+  }
+}
+
+// After a game start: NPC positions and health to HBM.
+template <int NCAP>
+__device__ __forceinline__ void store_new_npcs(const orx_state_t& st, const Cfg& c, uint32_t B,
+                                            uint32_t i, const Npcs<NCAP>& npc) {
+  if constexpr (NCAP > 0) {
+    for (int k = 0; k < c.K; ++k) {
+      st.npc_pos[(size_t)k * B + i] = (uint16_t)npc.get(k);
+      st.npc_health[(size_t)k * B + i] = (int8_t)c.npc_hp;
+    }
+  }
+}
+
+__device__ __forceinline__ void flush_deltas(const orx_state_t& st, uint32_t B, uint32_t i,
                                              const Deltas& dl) {
-  if (st.counters && (dl.c0 | dl.c1 | dl.c2 | dl.c3)) {
-    st.counters[i] += dl.c0;
-    st.counters[B + i] += dl.c1;
-    st.counters[2 * B + i] += dl.c2;
-    st.counters[3 * B + i] += dl.c3;
+  if (st.counters && (dl.combat | dl.descend | dl.dungeon | dl.npc_death)) {
+    st.counters[i] += dl.combat;
+    st.counters[B + i] += dl.descend;
+    st.counters[2 * (size_t)B + i] += dl.dungeon;
+    st.counters[3 * (size_t)B + i] += dl.npc_death;
   }
   if (dl.eps) {
     st.ret_sum[i] += dl.ret;
@@ -482,7 +613,10 @@ __device__ __forceinline__ Cfg make_cfg(const orx_cfg_t& h) {
   c.K = h.n_npcs; c.npc_hp = h.npc_health; c.player_hp = h.player_health;
   c.player_dmg_net = h.player_damage - h.player_armor;
   c.autoreset = h.autoreset;
-  c.n_ground = (h.width - 2) * (h.height - 2) - 1;
+  c.ih = h.height - 2;
+  c.ground.set((h.width - 2) * (h.height - 2) - 1);
+  c.stair_x.set(h.width - 3);
+  c.stair_y.set(h.height - 3);
   return c;
 }
 
@@ -490,52 +624,58 @@ __device__ __forceinline__ bool valid_move(int32_t m) {
   return m >= ORX_MOVE_UP && m <= ORX_MOVE_STAY;
 }
 
+__device__ __forceinline__ uint16_t pack_actions(int32_t a1, int32_t a2) {
+  return (uint16_t)((uint32_t)(uint8_t)a1 | ((uint32_t)(uint8_t)a2 << 8));
+}
+
 // ---------------------------------------------------------------------------
-// Kernels
+// Kernels (NCAP = NPC slot capacity: 0, 8 or 16)
 // ---------------------------------------------------------------------------
+template <int NCAP>
 __global__ void __launch_bounds__(256) reset_kernel(orx_cfg_t hc, orx_state_t st,
-                                                    const uint8_t* __restrict__ mask, int64_t B,
-                                                    Key key, int64_t off) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+                                                    const uint8_t* __restrict__ mask, uint32_t B,
+                                                    Key key, uint32_t off) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= B) return;
   if (mask && !mask[i]) return;
   const Cfg c = make_cfg(hc);
-  const uint32_t game = (uint32_t)(off + i);
-  const uint32_t ep = (uint32_t)st.episode[i];
   Player p1, p2;
-  Npcs<false> npc;
-  npc.load(st, 0, B, i);
-  npc.K = c.K;
+  Npcs<NCAP> npc;
   int32_t tick, status;
-  setup_game(c, key, game, ep, p1, p2, npc, tick, status);
+  setup_game(c, key, off + i, (uint32_t)st.episode[i], p1, p2, npc, tick, status);
   store_players(st, B, i, p1, p2, true);
   st.tick[i] = tick;
   st.status[i] = status;
-  if (c.K) st.npc_alive[i] = npc.alive;
+  if constexpr (NCAP > 0) {
+    st.npc_alive[i] = npc.alive;
+    store_new_npcs(st, c, B, i, npc);
+  }
 }
 
+template <int NCAP>
 __global__ void __launch_bounds__(256) step_kernel(orx_cfg_t hc, orx_state_t st,
-                                                   const int8_t* __restrict__ actions, int64_t B,
-                                                   Key key, int64_t off) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+                                                   const int8_t* __restrict__ actions, uint32_t B,
+                                                   Key key, uint32_t off) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= B) return;
   const Cfg c = make_cfg(hc);
-  const uint32_t game = (uint32_t)(off + i);
+  const uint32_t game = off + i;
   int32_t status = st.status[i];
-  Npcs<false> npc;
+  Npcs<NCAP> npc;
   Player p1, p2;
   if (status != ORX_IN_PROGRESS) {
     if (!c.autoreset) return;
     const uint32_t ep = (uint32_t)st.episode[i] + 1u;
-    npc.load(st, 0, B, i);
-    npc.K = c.K;
     int32_t tick;
     setup_game(c, key, game, ep, p1, p2, npc, tick, status);
     store_players(st, B, i, p1, p2, true);
     st.tick[i] = tick;
     st.status[i] = status;
     st.episode[i] = (int32_t)ep;
-    if (c.K) st.npc_alive[i] = npc.alive;
+    if constexpr (NCAP > 0) {
+      st.npc_alive[i] = npc.alive;
+      store_new_npcs(st, c, B, i, npc);
+    }
     return;
   }
   const uint16_t a = reinterpret_cast<const uint16_t*>(actions)[i];
@@ -548,26 +688,24 @@ __global__ void __launch_bounds__(256) step_kernel(orx_cfg_t hc, orx_state_t st,
   const uint32_t ep = (uint32_t)st.episode[i];
   int32_t tick = st.tick[i];
   load_players(st, B, i, p1, p2);
-  p1.start = c.d1; p2.start = c.d2;
-  npc.load(st, c.K, B, i);
+  load_npcs(st, c, B, i, npc);
+  const NpcMem m{st.npc_pos, st.npc_health, B, i};
   Deltas dl = {0, 0, 0, 0, 0, 0};
-  tick_game(c, key, game, ep, p1, p2, npc, tick, status, dl);
-  store_players(st, B, i, p1, p2, dl.c1 != 0);
+  tick_game(c, key, game, ep, p1, p2, npc, m, tick, status, dl);
+  store_players(st, B, i, p1, p2, dl.descend != 0);
   st.tick[i] = tick;
   st.status[i] = status;
-  if (dl.c3) st.npc_alive[i] = npc.alive;
+  if (NCAP > 0 && dl.npc_death) st.npc_alive[i] = npc.alive;
   flush_deltas(st, B, i, dl);
 }
 
-__global__ void __launch_bounds__(256) policy_kernel(orx_cfg_t hc, orx_state_t st, int32_t pol1,
-                                                     int32_t pol2, int8_t* __restrict__ actions,
-                                                     int64_t B, Key key, int64_t off) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__global__ void __launch_bounds__(256) policy_kernel(orx_state_t st, int32_t pol1, int32_t pol2,
+                                                     int8_t* __restrict__ actions, uint32_t B,
+                                                     Key key, uint32_t off) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= B) return;
-  const uint32_t game = (uint32_t)(off + i);
   Player p1, p2;
-  const bool need_pos = pol1 == ORX_POLICY_STAIRCASE || pol2 == ORX_POLICY_STAIRCASE;
-  if (need_pos) {
+  if (pol1 == ORX_POLICY_STAIRCASE || pol2 == ORX_POLICY_STAIRCASE) {
     p1.x = st.p_x[i]; p2.x = st.p_x[B + i];
     p1.y = st.p_y[i]; p2.y = st.p_y[B + i];
     p1.sx = st.st_x[i]; p2.sx = st.st_x[B + i];
@@ -583,75 +721,71 @@ __global__ void __launch_bounds__(256) policy_kernel(orx_cfg_t hc, orx_state_t s
     a1 = (int8_t)(prev & 0xFF);
     a2 = (int8_t)(prev >> 8);
   }
-  policy_pair(key, game, ep, tick, pol1, pol2, p1, p2, a1, a2);
-  out[i] = (uint16_t)((uint32_t)(uint8_t)a1 | ((uint32_t)(uint8_t)a2 << 8));
+  policy_pair(key, off + i, ep, tick, pol1, pol2, p1, p2, a1, a2);
+  out[i] = pack_actions(a1, a2);
 }
 
 // Fused rollout: n_ticks x (policy, step); state and NPC positions stay in
-// registers; tick t's observation is streamed out to obs/act.
+// registers; tick t's observation row is streamed out to obs/act.
+template <int NCAP>
 __global__ void __launch_bounds__(256) rollout_kernel(orx_cfg_t hc, orx_state_t st, int32_t pol1,
                                                       int32_t pol2, int32_t n_ticks,
                                                       int32_t* __restrict__ obs,
-                                                      int8_t* __restrict__ act, int64_t B,
-                                                      Key key, int64_t off) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+                                                      int8_t* __restrict__ act, uint32_t B,
+                                                      Key key, uint32_t off) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= B) return;
   const Cfg c = make_cfg(hc);
-  const uint32_t game = (uint32_t)(off + i);
+  const uint32_t game = off + i;
   Player p1, p2;
   load_players(st, B, i, p1, p2);
-  p1.start = c.d1; p2.start = c.d2;
   int32_t tick = st.tick[i];
   int32_t status = st.status[i];
   uint32_t ep = (uint32_t)st.episode[i];
-  Npcs<true> npc;
-  npc.load(st, c.K, B, i);
+  Npcs<NCAP> npc;
+  load_npcs(st, c, B, i, npc);
+  const NpcMem m{st.npc_pos, st.npc_health, B, i};
   Deltas dl = {0, 0, 0, 0, 0, 0};
-  bool stairs_dirty = false;
+  bool stairs_dirty = false, npc_dirty = false;
   for (int32_t t = 0; t < n_ticks; ++t) {
     int32_t a1 = ORX_MOVE_STAY, a2 = ORX_MOVE_STAY;
     policy_pair(key, game, ep, tick, pol1, pol2, p1, p2, a1, a2);
-    if (status != ORX_IN_PROGRESS) {
-      if (c.autoreset) {
-        ep += 1;
-        setup_game(c, key, game, ep, p1, p2, npc, tick, status);
-        stairs_dirty = true;
-      }
-    } else if (!valid_move(a1) || !valid_move(a2)) {
-      status = ORX_STATUS_BAD_ACTION;
-    } else {
+    if (status == ORX_IN_PROGRESS) {
       p1.move = a1; p2.move = a2;
-      const int32_t descents = dl.c1;
-      tick_game(c, key, game, ep, p1, p2, npc, tick, status, dl);
-      stairs_dirty |= dl.c1 != descents;
+      const int32_t descents = dl.descend;
+      tick_game(c, key, game, ep, p1, p2, npc, m, tick, status, dl);
+      stairs_dirty |= dl.descend != descents;
+    } else if (c.autoreset) {
+      ep += 1;
+      setup_game(c, key, game, ep, p1, p2, npc, tick, status);
+      if constexpr (NCAP > 0) store_new_npcs(st, c, B, i, npc);
+      stairs_dirty = true;
+      npc_dirty = true;
     }
     if (obs) {
-      int32_t* o = obs + (int64_t)t * ORX_OBS_FIELDS * B + i;
-      o[ORX_OBS_P1_X * B] = p1.x;
-      o[ORX_OBS_P1_Y * B] = p1.y;
-      o[ORX_OBS_P1_DEPTH * B] = p1.d;
-      o[ORX_OBS_P1_HEALTH * B] = p1.hp;
-      o[ORX_OBS_P2_X * B] = p2.x;
-      o[ORX_OBS_P2_Y * B] = p2.y;
-      o[ORX_OBS_P2_DEPTH * B] = p2.d;
-      o[ORX_OBS_P2_HEALTH * B] = p2.hp;
-      o[ORX_OBS_TICK * B] = tick;
-      o[ORX_OBS_STATUS * B] = status;
-      o[ORX_OBS_P1_STAIR_X * B] = p1.sx;
-      o[ORX_OBS_P1_STAIR_Y * B] = p1.sy;
-      o[ORX_OBS_P2_STAIR_X * B] = p2.sx;
-      o[ORX_OBS_P2_STAIR_Y * B] = p2.sy;
+      int32_t* o = obs + (size_t)t * ORX_OBS_FIELDS * B;
+      o[(size_t)ORX_OBS_P1_X * B + i] = p1.x;
+      o[(size_t)ORX_OBS_P1_Y * B + i] = p1.y;
+      o[(size_t)ORX_OBS_P1_DEPTH * B + i] = p1.d;
+      o[(size_t)ORX_OBS_P1_HEALTH * B + i] = p1.hp;
+      o[(size_t)ORX_OBS_P2_X * B + i] = p2.x;
+      o[(size_t)ORX_OBS_P2_Y * B + i] = p2.y;
+      o[(size_t)ORX_OBS_P2_DEPTH * B + i] = p2.d;
+      o[(size_t)ORX_OBS_P2_HEALTH * B + i] = p2.hp;
+      o[(size_t)ORX_OBS_TICK * B + i] = tick;
+      o[(size_t)ORX_OBS_STATUS * B + i] = status;
+      o[(size_t)ORX_OBS_P1_STAIR_X * B + i] = p1.sx;
+      o[(size_t)ORX_OBS_P1_STAIR_Y * B + i] = p1.sy;
+      o[(size_t)ORX_OBS_P2_STAIR_X * B + i] = p2.sx;
+      o[(size_t)ORX_OBS_P2_STAIR_Y * B + i] = p2.sy;
     }
-    if (act) {
-      reinterpret_cast<uint16_t*>(act)[(int64_t)t * B + i] =
-          (uint16_t)((uint32_t)(uint8_t)a1 | ((uint32_t)(uint8_t)a2 << 8));
-    }
+    if (act) reinterpret_cast<uint16_t*>(act)[(size_t)t * B + i] = pack_actions(a1, a2);
   }
   store_players(st, B, i, p1, p2, stairs_dirty);
   st.tick[i] = tick;
   st.status[i] = status;
   st.episode[i] = (int32_t)ep;
-  if (c.K) st.npc_alive[i] = npc.alive;
+  if (NCAP > 0 && (npc_dirty || dl.npc_death)) st.npc_alive[i] = npc.alive;
   flush_deltas(st, B, i, dl);
 }
 
@@ -729,11 +863,14 @@ inline Key make_key(uint64_t seed) { return Key{(uint32_t)seed, (uint32_t)(seed 
 
 int check_sizes(int64_t B, int64_t off) {
   if (B < 0) return fail(ORX_EINVAL, "n_games < 0");
+  if (B > 0x7FFFFFFFLL - kBlock) return fail(ORX_EINVAL, "n_games must be < 2^31");
   if (off < 0 || off + B > ((int64_t)1 << 32))
     return fail(ORX_EINVAL, "global game ids (game_offset + index) must fit 32 bits");
-  if ((B + kBlock - 1) / kBlock > 0x7FFFFFFFLL) return fail(ORX_EINVAL, "n_games too large");
   return ORX_OK;
 }
+
+// NPC slot capacity of the kernel instance for K NPCs.
+inline int ncap_for(int K) { return K == 0 ? 0 : K <= 8 ? 8 : 16; }
 
 }  // namespace
 
@@ -755,8 +892,20 @@ int orx_reset(const orx_cfg_t* cfg, const orx_state_t* st, const uint8_t* mask, 
   if ((r = check_cfg(cfg)) || (r = check_sizes(n_games, game_offset))) return r;
   if (n_games == 0) return ORX_OK;
   if ((r = check_state(cfg, st, false))) return r;
-  hipLaunchKernelGGL(reset_kernel, grid_for(n_games), dim3(kBlock), 0, (hipStream_t)stream, *cfg,
-                     *st, mask, n_games, make_key(seed), game_offset);
+  const uint32_t B = (uint32_t)n_games, off = (uint32_t)game_offset;
+  const hipStream_t s = (hipStream_t)stream;
+  const Key k = make_key(seed);
+  switch (ncap_for(cfg->n_npcs)) {
+    case 0:
+      hipLaunchKernelGGL(reset_kernel<0>, grid_for(B), dim3(kBlock), 0, s, *cfg, *st, mask, B, k, off);
+      break;
+    case 8:
+      hipLaunchKernelGGL(reset_kernel<8>, grid_for(B), dim3(kBlock), 0, s, *cfg, *st, mask, B, k, off);
+      break;
+    default:
+      hipLaunchKernelGGL(reset_kernel<16>, grid_for(B), dim3(kBlock), 0, s, *cfg, *st, mask, B, k, off);
+      break;
+  }
   return launch_status("orx_reset");
 }
 
@@ -767,8 +916,20 @@ int orx_step(const orx_cfg_t* cfg, const orx_state_t* st, const int8_t* actions,
   if (n_games == 0) return ORX_OK;
   if ((r = check_state(cfg, st, true))) return r;
   if (!actions) return fail(ORX_EINVAL, "actions is NULL");
-  hipLaunchKernelGGL(step_kernel, grid_for(n_games), dim3(kBlock), 0, (hipStream_t)stream, *cfg,
-                     *st, actions, n_games, make_key(seed), game_offset);
+  const uint32_t B = (uint32_t)n_games, off = (uint32_t)game_offset;
+  const hipStream_t s = (hipStream_t)stream;
+  const Key k = make_key(seed);
+  switch (ncap_for(cfg->n_npcs)) {
+    case 0:
+      hipLaunchKernelGGL(step_kernel<0>, grid_for(B), dim3(kBlock), 0, s, *cfg, *st, actions, B, k, off);
+      break;
+    case 8:
+      hipLaunchKernelGGL(step_kernel<8>, grid_for(B), dim3(kBlock), 0, s, *cfg, *st, actions, B, k, off);
+      break;
+    default:
+      hipLaunchKernelGGL(step_kernel<16>, grid_for(B), dim3(kBlock), 0, s, *cfg, *st, actions, B, k, off);
+      break;
+  }
   return launch_status("orx_step");
 }
 
@@ -782,8 +943,9 @@ int orx_policy(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p1, i
   if (n_games == 0) return ORX_OK;
   if ((r = check_state(cfg, st, false))) return r;
   if (!actions) return fail(ORX_EINVAL, "actions is NULL");
-  hipLaunchKernelGGL(policy_kernel, grid_for(n_games), dim3(kBlock), 0, (hipStream_t)stream, *cfg,
-                     *st, policy_p1, policy_p2, actions, n_games, make_key(seed), game_offset);
+  const uint32_t B = (uint32_t)n_games, off = (uint32_t)game_offset;
+  hipLaunchKernelGGL(policy_kernel, grid_for(B), dim3(kBlock), 0, (hipStream_t)stream, *st,
+                     policy_p1, policy_p2, actions, B, make_key(seed), off);
   return launch_status("orx_policy");
 }
 
@@ -799,9 +961,23 @@ int orx_rollout(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p1, 
   if (n_ticks < 0) return fail(ORX_EINVAL, "n_ticks < 0");
   if (n_games == 0 || n_ticks == 0) return ORX_OK;
   if ((r = check_state(cfg, st, true))) return r;
-  hipLaunchKernelGGL(rollout_kernel, grid_for(n_games), dim3(kBlock), 0, (hipStream_t)stream,
-                     *cfg, *st, policy_p1, policy_p2, n_ticks, obs, act, n_games, make_key(seed),
-                     game_offset);
+  const uint32_t B = (uint32_t)n_games, off = (uint32_t)game_offset;
+  const hipStream_t s = (hipStream_t)stream;
+  const Key k = make_key(seed);
+  switch (ncap_for(cfg->n_npcs)) {
+    case 0:
+      hipLaunchKernelGGL(rollout_kernel<0>, grid_for(B), dim3(kBlock), 0, s, *cfg, *st, policy_p1,
+                         policy_p2, n_ticks, obs, act, B, k, off);
+      break;
+    case 8:
+      hipLaunchKernelGGL(rollout_kernel<8>, grid_for(B), dim3(kBlock), 0, s, *cfg, *st, policy_p1,
+                         policy_p2, n_ticks, obs, act, B, k, off);
+      break;
+    default:
+      hipLaunchKernelGGL(rollout_kernel<16>, grid_for(B), dim3(kBlock), 0, s, *cfg, *st,
+                         policy_p1, policy_p2, n_ticks, obs, act, B, k, off);
+      break;
+  }
   return launch_status("orx_rollout");
 }
 
