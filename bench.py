@@ -12,12 +12,14 @@ shard across GPUs by global game id (weak scaling, no data-path collective);
 after the timed region the per-game episode returns are all-gathered over
 RCCL (the only collective).
 
-Modes
-  rollout (default): one fused kernel launch per --chunk ticks; state stays in
-          registers and every tick's full observation (14 int32 fields) and
-          actions are streamed to an HBM trajectory buffer.
-  step:   per tick a policy launch then a step launch (orx_policy/orx_step),
-          state read from and written back to HBM every tick.
+Timed path (headline): the fused rollout kernel, one launch per --chunk ticks;
+state stays in registers and EVERY tick's full observation (14 int32 fields:
+both players' x, y, depth, health, staircase, plus tick and status) and both
+actions are written to an HBM trajectory buffer -- nothing is skipped.
+
+Extras (rank 0, 1 GPU): the unfused path (orx_policy + orx_step per tick,
+captured in a HIP graph) at the config batch, and both kernels at a large
+batch (2^21 games) where the chip is full.
 
 Rank 0 prints one JSON line.
 """
@@ -36,20 +38,21 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 OBS_BYTES = 14 * 4      # one tick record: 14 int32 fields
 ACT_BYTES = 2
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic.json")
 
 
-def algorithmic_bytes(mode: str, K: int, ticks: int) -> dict:
-    """Algorithmic HBM bytes of the dominant kernel per game per launch."""
-    npc_read = (4 + 2 * K) if K else 0          # alive mask + K packed positions
-    if mode == "step":
-        read = 2 + 32 + 16 + 12 + npc_read        # actions, players, stairs, tick/status/episode
-        write = 32 + 8                            # players, tick, status
-        return {"per_unit": read + write, "per_launch_per_game": read + write, "units": 1}
-    state_in = 32 + 16 + 12 + npc_read            # players, stairs, tick/status/episode, NPCs
-    state_out = 32 + 12 + (4 if K else 0)         # players, tick/status/episode, alive mask
-    per_tick = OBS_BYTES + ACT_BYTES
-    return {"per_unit": per_tick, "per_launch_per_game": ticks * per_tick + state_in + state_out,
-            "units": ticks}
+def bytes_per_game(kernel: str, K: int, ticks: int = 1) -> int:
+    """Algorithmic HBM bytes per game per launch of a kernel."""
+    npc_read = (4 + 2 * K) if K else 0        # alive mask + K packed u16 positions
+    if kernel == "step":
+        # read: actions 2, players 32, staircases 16, tick/status/episode 12, NPCs
+        # write: players 32, tick 4, status 4
+        return 2 + 32 + 16 + 12 + npc_read + 40
+    if kernel == "policy":
+        return 4 + 4 + 2                       # tick, episode -> 2 int8 actions
+    state_in = 32 + 16 + 12 + npc_read         # players, staircases, tick/status/episode, NPCs
+    state_out = 32 + 12 + (4 if K else 0)      # players, tick/status/episode, alive mask
+    return ticks * (OBS_BYTES + ACT_BYTES) + state_in + state_out
 
 
 def cpu_baseline(cfg_dict: dict, seconds: float) -> dict:
@@ -74,16 +77,94 @@ def cpu_baseline(cfg_dict: dict, seconds: float) -> dict:
                       f"({platform.processor() or platform.machine()}), {el:.1f} s"}
 
 
+def timed_launches(torch, launch, n):
+    """Runs `launch` n times with HIP events around each (on torch's current
+    stream, the stream the engine launches on); returns per-launch seconds."""
+    evs = []
+    for _ in range(n):
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        a.record()
+        launch()
+        b.record()
+        evs.append((a, b))
+    torch.cuda.synchronize()
+    return [a.elapsed_time(b) * 1e-3 for a, b in evs]
+
+
+def extras(torch, cfg, dev, B_cfg, K):
+    """Unfused path at the config batch (HIP graph) and both paths at 2^21 games."""
+    from optimax_rogue_amd import OBS_FIELDS
+    from optimax_rogue_amd.engine import BatchedEngine
+    out = {}
+    # (1) unfused policy+step, 50 ticks captured in one HIP graph, config batch
+    eng = BatchedEngine(cfg, B_cfg, seed=3, device=dev)
+    for _ in range(3):
+        eng.step(eng.policy(1, 1))
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream(device=dev)
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            for _ in range(50):
+                eng.step(eng.policy(1, 1))
+    torch.cuda.current_stream().wait_stream(s)
+    for _ in range(2):
+        g.replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    n_rep = 20
+    for _ in range(n_rep):
+        g.replay()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    out["unfused_graph"] = {"value": B_cfg * 50 * n_rep / el, "unit": "env-steps/s",
+                            "us_per_tick": el / (50 * n_rep) * 1e6,
+                            "note": "orx_policy + orx_step per tick, 50 ticks per HIP graph"}
+    del eng, g
+    torch.cuda.empty_cache()
+    # (2) large batch: the chip full (2^21 games)
+    BL = 1 << 21
+    eng = BatchedEngine(cfg, BL, seed=3, device=dev)
+    for _ in range(2):
+        eng.step(eng.policy(1, 1))
+    step_s = timed_launches(torch, lambda: eng.step(), 30)
+    pol_s = timed_launches(torch, lambda: eng.policy(1, 1), 30)
+    T = 20
+    obs = torch.empty((T, len(OBS_FIELDS), BL), dtype=torch.int32, device=dev)
+    act = torch.empty((T, BL, 2), dtype=torch.int8, device=dev)
+    eng.rollout(T, 1, 1, obs=obs, act=act)
+    roll_s = timed_launches(torch, lambda: eng.rollout(T, 1, 1, obs=obs, act=act), 5)
+    med = lambda v: sorted(v)[len(v) // 2]
+    sb = bytes_per_game("step", K) * BL
+    rb = bytes_per_game("rollout", K, T) * BL
+    out["large_batch"] = {
+        "games": BL,
+        "step_kernel": {"avg_us": med(step_s) * 1e6, "achieved_GBps": sb / med(step_s) / 1e9,
+                        "frac": sb / med(step_s) / 1e9 / HBM_PEAK_GBS,
+                        "bytes_per_env_step": bytes_per_game("step", K)},
+        "policy_kernel": {"avg_us": med(pol_s) * 1e6},
+        "rollout_kernel": {"avg_us": med(roll_s) * 1e6, "ticks": T,
+                           "env_steps_per_s": BL * T / med(roll_s),
+                           "achieved_GBps": rb / med(roll_s) / 1e9,
+                           "frac": rb / med(roll_s) / 1e9 / HBM_PEAK_GBS},
+    }
+    del eng, obs, act
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2000, help="ticks in the timed region")
     ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--batch", type=int, default=65536, help="games per GPU")
-    ap.add_argument("--mode", choices=["rollout", "step"], default="rollout")
     ap.add_argument("--chunk", type=int, default=50, help="ticks per rollout launch")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true")
     args = ap.parse_args()
 
     import torch
@@ -91,49 +172,33 @@ def main():
 
     from optimax_rogue_amd import EnvConfig, OBS_FIELDS
     from optimax_rogue_amd.engine import BatchedEngine
+    from optimax_rogue_amd.parallel import env_rank, gather_returns, init
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    rank, world, local = env_rank()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    init("nccl" if world > 1 else None, dev)
 
     cfg = EnvConfig.c3()
     B = args.batch
     eng = BatchedEngine(cfg, B, seed=3, game_offset=rank * B, device=dev)
     chunk = max(1, min(args.chunk, args.steps))
-    obs = act = None
-    if args.mode == "rollout":
-        obs = torch.empty((chunk, len(OBS_FIELDS), B), dtype=torch.int32, device=dev)
-        act = torch.empty((chunk, B, 2), dtype=torch.int8, device=dev)
+    obs = torch.empty((chunk, len(OBS_FIELDS), B), dtype=torch.int32, device=dev)
+    act = torch.empty((chunk, B, 2), dtype=torch.int8, device=dev)
 
     def run(n_ticks, events=None):
-        if args.mode == "rollout":
-            left = n_ticks
-            while left > 0:
-                t = min(chunk, left)
-                if events is not None:
-                    e0 = torch.cuda.Event(enable_timing=True)
-                    e1 = torch.cuda.Event(enable_timing=True)
-                    e0.record()
-                eng.rollout(t, 1, 1, obs=obs, act=act)
-                if events is not None:
-                    e1.record()
-                    events.append((e0, e1, t))
-                left -= t
-        else:
-            for _ in range(n_ticks):
-                eng.policy(1, 1)
-                if events is not None:
-                    e0 = torch.cuda.Event(enable_timing=True)
-                    e1 = torch.cuda.Event(enable_timing=True)
-                    e0.record()
-                eng.step()
-                if events is not None:
-                    e1.record()
-                    events.append((e0, e1, 1))
+        left = n_ticks
+        while left > 0:
+            t = min(chunk, left)
+            if events is not None:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record()
+            eng.rollout(t, 1, 1, obs=obs, act=act)
+            if events is not None:
+                e1.record()
+                events.append((e0, e1, t))
+            left -= t
 
     run(args.warmup)
     torch.cuda.synchronize()
@@ -152,34 +217,34 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # dominant kernel: average launch duration from HIP events on its stream
-    durs = [a.elapsed_time(b) * 1e-3 for a, b, _ in events]
-    full = [(d, n) for d, (_, _, n) in zip(durs, events) if n == chunk or args.mode == "step"]
-    avg_launch_s = sum(d for d, _ in full) / max(1, len(full))
-    ab = algorithmic_bytes(args.mode, cfg.n_npcs, chunk if args.mode == "rollout" else 1)
-    bytes_per_launch = ab["per_launch_per_game"] * B
+    # dominant kernel: average duration of the full-chunk rollout launches
+    durs = [(a.elapsed_time(b) * 1e-3, n) for a, b, n in events]
+    full = [d for d, n in durs if n == chunk]
+    avg_launch_s = sum(full) / max(1, len(full))
+    bytes_per_launch = bytes_per_game("rollout", cfg.n_npcs, chunk) * B
     achieved_gbs = bytes_per_launch / avg_launch_s / 1e9
 
     # the only collective: all-gather of per-game episode returns (RCCL / xGMI)
-    rets = eng.episode_returns()
-    gather_ms = None
-    if world > 1:
-        outs = [torch.empty_like(rets) for _ in range(world)]
-        torch.cuda.synchronize()
-        g0 = time.perf_counter()
-        dist.all_gather(outs, rets)
-        torch.cuda.synchronize()
-        gather_ms = (time.perf_counter() - g0) * 1e3
-        allrets = torch.cat(outs, dim=1)
-    else:
-        allrets = rets
+    torch.cuda.synchronize()
+    g0 = time.perf_counter()
+    allrets = gather_returns(eng.episode_returns(), B * world)
+    torch.cuda.synchronize()
+    gather_ms = (time.perf_counter() - g0) * 1e3 if world > 1 else None
     episodes = int(allrets[1].sum().item())
     mean_ret = float(allrets[0].sum().item()) / max(1, episodes)
 
-    total_steps = B * world * args.steps
-    value = total_steps / elapsed
-    result = None
+    value = B * world * args.steps / elapsed
     if rank == 0:
+        traffic = None
+        if os.path.exists(TRAFFIC_FILE):
+            tr = json.load(open(TRAFFIC_FILE)).get("rollout_kernel", {})
+            if tr.get("batch") == B and tr.get("ticks") == chunk:
+                traffic = tr.get("hbm_bytes_per_launch")
+        extra = None
+        if not args.no_extras and world == 1:
+            del obs, act
+            torch.cuda.empty_cache()
+            extra = extras(torch, cfg, dev, B, cfg.n_npcs)
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(cfg.to_dict(), args.cpu_seconds)
@@ -195,25 +260,25 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "int32",
-            "data": "synthetic (Philox-seeded dungeons, RandomBot actions)",
+            "data": "synthetic (Philox-seeded dungeons and RandomBot actions)",
             "config": {
                 "workload": "C3: 65536 games/GPU, 64x64 grid, 8 NPCs/game, 2x RandomBot, "
-                            "Unreachable despawn, max_ticks 1000, autoreset",
+                            "Unreachable despawn, max_ticks 1000, autoreset; every tick's "
+                            "observation + actions written to HBM",
                 "batch_per_gpu": B, "global_batch": B * world, "grid": "64x64",
-                "n_npcs": cfg.n_npcs, "mode": args.mode,
-                "ticks_per_launch": chunk if args.mode == "rollout" else 1,
+                "n_npcs": cfg.n_npcs, "ticks_per_launch": chunk,
                 "parallelism": f"games sharded by global id over {world} GPU(s)",
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "rollout_kernel" if args.mode == "rollout" else "step_kernel",
+                "kernel": "rollout_kernel<8>",
                 "achieved": achieved_gbs,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved_gbs / HBM_PEAK_GBS,
-                "traffic": None,
+                "traffic": traffic,
                 "bytes_per_launch": bytes_per_launch,
-                "bytes_per_env_step": ab["per_unit"],
+                "bytes_per_env_step": OBS_BYTES + ACT_BYTES,
                 "avg_launch_us": avg_launch_s * 1e6,
                 "launches": len(full),
             },
@@ -221,6 +286,7 @@ def main():
             "episodes_finished": episodes,
             "mean_return_p1": mean_ret,
             "returns_gather_ms": gather_ms,
+            "extras": extra,
         }
         print(json.dumps(result), flush=True)
     if world > 1:

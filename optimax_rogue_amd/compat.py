@@ -1,0 +1,200 @@
+"""Reference-schema views of batched games, for code written against
+optimax_rogue's GameState (bots, spectators, tools).
+
+``game_state(snapshot, i, cfg)`` materializes game ``i`` of an engine snapshot
+as an object with the reference's attribute surface:
+
+  GameState  optimax_rogue/game/state.py:14-62   (tick, player_1_iden/2, world,
+             entities, pos_lookup, iden_lookup, player_1/2, view_for, view_spec)
+  World      optimax_rogue/game/world.py:101-135 (dungeons dict, get_at_depth)
+  Dungeon    optimax_rogue/game/world.py:19-66   (tiles[W, H] int32, width,
+             height, is_blocked, get_unblocked, staircase)
+  Entity     optimax_rogue/game/entities.py:17-74 (iden, depth, x, y, health,
+             base stats, max_health/damage/armor attribles with .value)
+
+so that ``Bot.move(game_state)`` implementations (optimax_rogue_bots/bot.py:6-38,
+randombot.py, staircasebot.py) run unchanged via ``BotDriver``.
+
+World contents: the dungeons of the players' current depths (the engine keeps
+no other dungeon; a bot's view, GameState.view_for, only ever holds its own
+depth).  This is the slow, per-game compatibility path; the throughput path
+is the on-device policy kernels (Policy.Random / Policy.Staircase).
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+from .enums import Move, Tile, UpdateResult
+
+
+class _Attrible:
+    def __init__(self, value: int):
+        self.value = value
+
+
+class EntityView:
+    def __init__(self, iden, depth, x, y, health, base_max_health, base_damage, base_armor):
+        self.iden, self.depth, self.x, self.y = int(iden), int(depth), int(x), int(y)
+        self.health = int(health)
+        self.base_max_health, self.base_damage, self.base_armor = (
+            int(base_max_health), int(base_damage), int(base_armor))
+        self.max_health = _Attrible(self.base_max_health)
+        self.damage = _Attrible(self.base_damage)
+        self.armor = _Attrible(self.base_armor)
+        self.modifiers: list = []
+        self.items: dict = {}
+
+    def on_tick(self, game_state) -> None:  # attribles are constant (no Modifier exists)
+        pass
+
+    def __repr__(self):
+        return f"[Entity @ ({self.x}, {self.y})]"
+
+
+class DungeonView:
+    """EmptyDungeonGenerator layout (worldgen.py:33-43) with its staircase."""
+
+    def __init__(self, width: int, height: int, sx: int, sy: int):
+        t = np.full((width, height), Tile.Ground.value, np.int32)
+        t[[0, -1], :] = Tile.Wall.value
+        t[:, [0, -1]] = Tile.Wall.value
+        t[sx, sy] = Tile.StaircaseDown.value
+        self.tiles = t
+
+    @property
+    def width(self):
+        return self.tiles.shape[0]
+
+    @property
+    def height(self):
+        return self.tiles.shape[1]
+
+    def is_blocked(self, x: int, y: int) -> bool:
+        if x < 0 or x >= self.width or y < 0 or y >= self.height:
+            return True
+        return self.tiles[x, y] == Tile.Wall
+
+    def get_unblocked(self) -> np.ndarray:
+        return self.tiles != Tile.Wall
+
+    def staircase(self):
+        resx, resy = tuple(np.argwhere(self.tiles == Tile.StaircaseDown)[0])
+        return int(resx), int(resy)
+
+
+class WorldView:
+    def __init__(self, dungeons: Dict[int, DungeonView]):
+        self.dungeons = dungeons
+
+    def get_at_depth(self, ind: int) -> DungeonView:
+        return self.dungeons[ind]
+
+    def shallow_copy_with_layers(self, *layers) -> "WorldView":
+        return WorldView({lyr: self.dungeons[lyr] for lyr in layers})
+
+
+class GameStateView:
+    def __init__(self, is_authoritative: bool, tick: int, world: WorldView,
+                 entities: List[EntityView], player_1_iden: int = 1, player_2_iden: int = 2):
+        self.is_authoritative = is_authoritative
+        self.tick = int(tick)
+        self.player_1_iden, self.player_2_iden = player_1_iden, player_2_iden
+        self.world = world
+        self.entities = entities
+        self.pos_lookup = {(e.depth, e.x, e.y): e for e in entities}
+        self.iden_lookup = {e.iden: e for e in entities}
+
+    @property
+    def player_1(self) -> EntityView:
+        return self.iden_lookup[self.player_1_iden]
+
+    @property
+    def player_2(self) -> EntityView:
+        return self.iden_lookup[self.player_2_iden]
+
+    def on_tick(self) -> None:
+        pass
+
+    def view_for(self, entity: EntityView, reduce_tick: bool = False) -> "GameStateView":
+        """GameState.view_for (state.py:53-58): the entity's depth only."""
+        return GameStateView(False, self.tick - 1 if reduce_tick else self.tick,
+                             self.world.shallow_copy_with_layers(entity.depth),
+                             [e for e in self.entities if e.depth == entity.depth],
+                             self.player_1_iden, self.player_2_iden)
+
+    def view_spec(self) -> "GameStateView":
+        return GameStateView(False, self.tick, self.world, self.entities, self.player_1_iden,
+                             self.player_2_iden)
+
+
+def game_state(snap: dict, i: int, cfg) -> GameStateView:
+    """Game ``i`` of a BatchedEngine.snapshot() in the reference schema."""
+    W, H = int(cfg.width), int(cfg.height)
+    ents = []
+    dungeons = {}
+    for p in range(2):
+        d = int(snap["p_depth"][p][i])
+        ents.append(EntityView(1 + p, d, snap["p_x"][p][i], snap["p_y"][p][i],
+                               snap["p_health"][p][i], cfg.player_health, cfg.player_damage,
+                               cfg.player_armor))
+        if d not in dungeons:
+            dungeons[d] = DungeonView(W, H, int(snap["st_x"][p][i]), int(snap["st_y"][p][i]))
+    K = int(cfg.n_npcs)
+    if K:
+        alive = int(snap["npc_alive"][i])
+        npc_depth = int(cfg.p1_depth) if int(cfg.start_mode) == 2 else 0
+        for k in range(K):
+            if (alive >> k) & 1:
+                v = int(snap["npc_pos"][k][i])
+                ents.append(EntityView(3 + k, npc_depth, v & 0xFF, v >> 8, snap["npc_health"][k][i],
+                                       cfg.npc_health, cfg.npc_damage, cfg.npc_armor))
+    return GameStateView(True, int(snap["tick"][i]), WorldView(dungeons), ents)
+
+
+class BotDriver:
+    """Drives batched games with per-game ``Bot`` objects (the reference's
+    optimax_rogue_bots/bot.py interface): each step builds every game's
+    ``view_for`` its bot's entity, calls ``bot.move`` and steps the engine;
+    ``bot.finished`` is called when a game ends (optimax_rogue_bots/main.py:118-155).
+    """
+
+    def __init__(self, engine, bots_p1: Sequence, bots_p2: Sequence):
+        if len(bots_p1) != engine.B or len(bots_p2) != engine.B:
+            raise ValueError("one bot per game and player")
+        self.engine = engine
+        self.bots = (list(bots_p1), list(bots_p2))
+        self._started = False
+
+    def _views(self, snap):
+        for i in range(self.engine.B):
+            gs = game_state(snap, i, self.engine.cfg)
+            yield i, gs
+
+    def step(self) -> np.ndarray:
+        import torch
+        snap = self.engine.snapshot()
+        acts = np.full((self.engine.B, 2), Move.Stay.value, np.int8)
+        for i, gs in self._views(snap):
+            for p in range(2):
+                bot = self.bots[p][i]
+                view = gs.view_for(gs.iden_lookup[1 + p])
+                if not self._started:
+                    bot.started(view)
+                mv = bot.move(view)
+                bot.on_move(view, mv)
+                acts[i, p] = int(mv)
+        self._started = True
+        self.engine.actions.copy_(torch.from_numpy(acts))
+        status = self.engine.step().cpu().numpy()
+        done = np.nonzero((status >= UpdateResult.Player1Win) & (status <= UpdateResult.Tie)
+                          & (snap["status"] == UpdateResult.InProgress))[0]
+        if len(done):
+            after = self.engine.snapshot()
+            for i in done:
+                gs = game_state(after, int(i), self.engine.cfg)
+                for p in range(2):
+                    self.bots[p][i].finished(gs.view_for(gs.iden_lookup[1 + p]),
+                                             UpdateResult(int(status[i])))
+        return status

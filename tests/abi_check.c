@@ -1,0 +1,30 @@
+/* Plain-C consumer of the C-ABI (include/orx.h): proves the boundary is
+ * callable without C++, torch or HIP headers -- the way a cgo / JNI / N-API /
+ * ctypes binding sees it.  Built and run by tests/test_abi.py (no GPU calls). */
+#include <stddef.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "orx.h"
+
+int main(void) {
+  if (orx_abi_version() != ORX_ABI_VERSION) { printf("abi mismatch\n"); return 1; }
+  orx_cfg_t c;
+  memset(&c, 0, sizeof c);
+  c.width = 64; c.height = 64; c.despawn = ORX_DESPAWN_UNREACHABLE; c.max_ticks = 1000;
+  c.start_mode = ORX_START_TOGETHER; c.n_npcs = 8; c.npc_health = 3; c.npc_damage = 1;
+  c.player_health = 10; c.player_damage = 2; c.player_armor = 1; c.autoreset = 1;
+  if (orx_validate_cfg(&c) != ORX_OK) { printf("valid cfg rejected: %s\n", orx_last_error()); return 2; }
+  c.width = 3;
+  if (orx_validate_cfg(&c) != ORX_EINVAL) { printf("bad cfg accepted\n"); return 3; }
+  if (strlen(orx_last_error()) == 0) { printf("no error message\n"); return 4; }
+  c.width = 64;
+  /* zero games: no device work, no pointers needed */
+  if (orx_step(&c, NULL, NULL, 0, 1, 0, NULL) != ORX_OK) { printf("empty step failed\n"); return 5; }
+  if (orx_rollout(&c, NULL, ORX_POLICY_RANDOM, ORX_POLICY_RANDOM, 5, NULL, NULL, 0, 1, 0, NULL) != ORX_OK) return 6;
+  if (orx_step(&c, NULL, NULL, 16, 1, 0, NULL) != ORX_EINVAL) { printf("NULL state accepted\n"); return 7; }
+  printf("sizeof(orx_cfg_t)=%zu sizeof(orx_state_t)=%zu off_flags=%zu off_npc_alive=%zu\n",
+         sizeof(orx_cfg_t), sizeof(orx_state_t), offsetof(orx_cfg_t, flags),
+         offsetof(orx_state_t, npc_alive));
+  return 0;
+}

@@ -1,0 +1,108 @@
+"""CPU: the C-ABI library loads, exports every symbol include/orx.h declares,
+its POD layouts match the ctypes mirrors, and it is callable from plain C.
+No compute runs here (no GPU)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "orx.h")
+
+
+def header_text():
+    return open(HEADER).read()
+
+
+def declared_functions():
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(orx_\w+)\s*\(", header_text(), re.M)))
+
+
+def struct_fields(name):
+    body = re.search(r"typedef struct %s \{(.*?)\} %s_t;" % (name, name), header_text(), re.S).group(1)
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    return re.findall(r"(\w+)\s*;", body)
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from optimax_rogue_amd import _lib
+    from optimax_rogue_amd import build
+    build.build()
+    return _lib.load()
+
+
+def test_library_exports_every_declared_symbol(lib):
+    decl = declared_functions()
+    assert decl == sorted(["orx_abi_version", "orx_last_error", "orx_validate_cfg", "orx_reset",
+                           "orx_step", "orx_policy", "orx_rollout"])
+    from optimax_rogue_amd import _lib
+    assert sorted(_lib.EXPORTS) == decl
+    for name in decl:
+        assert hasattr(lib, name), name
+    out = subprocess.run(["nm", "-D", "--defined-only", os.path.join(ROOT, "optimax_rogue_amd",
+                                                                     "liborx.so")],
+                         capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r" T (orx_\w+)", out))
+    assert set(decl) <= exported
+
+
+def test_struct_layouts_match_header():
+    from optimax_rogue_amd._lib import OrxState
+    from optimax_rogue_amd.config import CFG_FIELDS, OrxCfg
+    from oracle.oracle import CFG_FIELDS as ORACLE_FIELDS
+    assert list(CFG_FIELDS) == struct_fields("orx_cfg") == list(ORACLE_FIELDS)
+    assert [f for f, _ in OrxState._fields_] == struct_fields("orx_state")
+    assert ctypes.sizeof(OrxCfg) == 4 * len(CFG_FIELDS)
+    assert ctypes.sizeof(OrxState) == 8 * len(OrxState._fields_)
+
+
+def test_enum_values_match_header():
+    from optimax_rogue_amd import enums
+    t = header_text()
+    val = lambda n: int(re.search(r"#define %s (-?\d+)" % n, t).group(1))
+    assert [m.value for m in enums.Move] == [val("ORX_MOVE_UP"), val("ORX_MOVE_RIGHT"),
+                                             val("ORX_MOVE_DOWN"), val("ORX_MOVE_LEFT"),
+                                             val("ORX_MOVE_STAY")]
+    assert [r.value for r in enums.UpdateResult] == [val("ORX_IN_PROGRESS"), val("ORX_PLAYER1_WIN"),
+                                                     val("ORX_PLAYER2_WIN"), val("ORX_TIE")]
+    assert enums.STATUS_BAD_ACTION == val("ORX_STATUS_BAD_ACTION")
+    assert enums.MAX_NPCS == val("ORX_MAX_NPCS")
+    assert len(enums.OBS_FIELDS) == val("ORX_OBS_FIELDS")
+
+
+def test_validate_cfg(lib):
+    from optimax_rogue_amd import EnvConfig
+    ok = [EnvConfig.c1(), EnvConfig.c3(), EnvConfig.c5(), EnvConfig(width=4, height=4),
+          EnvConfig(start_mode=2, p1_depth=0, p2_depth=1000, n_npcs=16, width=40, height=10)]
+    bad = [EnvConfig(width=3), EnvConfig(despawn=3), EnvConfig(start_mode=2, p1_depth=5,
+                                                                p2_depth=5),
+           EnvConfig(n_npcs=17), EnvConfig(n_npcs=2, width=300), EnvConfig(max_ticks=-1),
+           EnvConfig(width=4, height=4, n_npcs=2), EnvConfig(flags=1),
+           EnvConfig(n_npcs=1, npc_health=0)]
+    for c in ok:
+        assert lib.orx_validate_cfg(ctypes.byref(c.to_c())) == 0, c
+    for c in bad:
+        assert lib.orx_validate_cfg(ctypes.byref(c.to_c())) == -22, c
+        assert lib.orx_last_error()
+
+
+def test_plain_c_consumer(lib, tmp_path):
+    exe = tmp_path / "abi_check"
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "abi_check.c"), "-o", str(exe),
+                    "-L", os.path.join(ROOT, "optimax_rogue_amd"), "-lorx",
+                    "-Wl,-rpath," + os.path.join(ROOT, "optimax_rogue_amd")], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "sizeof(orx_cfg_t)=64" in r.stdout
+
+
+def test_engine_refuses_cpu():
+    import torch
+    from optimax_rogue_amd import EnvConfig
+    from optimax_rogue_amd.engine import BatchedEngine
+    with pytest.raises(RuntimeError):
+        BatchedEngine(EnvConfig(), 8, device=torch.device("cpu"))

@@ -1,0 +1,71 @@
+"""GPU: the host-side mirror of the reference interface (BatchedUpdater,
+compat views, BotDriver) on the HIP engine."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+class ToStairsBot:
+    """A Bot (optimax_rogue_bots/bot.py interface) that walks to the staircase
+    of its view, horizontal axis first when strictly farther."""
+
+    def __init__(self, iden):
+        self.iden = iden
+        self.finished_with = None
+
+    def started(self, gs):
+        pass
+
+    def on_move(self, gs, mv):
+        pass
+
+    def finished(self, gs, result):
+        self.finished_with = int(result)
+
+    def move(self, gs):
+        me = gs.iden_lookup[self.iden]
+        sx, sy = gs.world.dungeons[me.depth].staircase()
+        dx, dy = sx - me.x, sy - me.y
+        if abs(dx) > abs(dy):
+            return 2 if dx > 0 else 4
+        return 3 if dy > 0 else 1
+
+
+def test_batched_updater_matches_oracle(oracle_lib):
+    import torch
+    from optimax_rogue_amd import DungeonDespawningStrategy
+    from optimax_rogue_amd.updater import BatchedUpdater
+    B = 512
+    upd = BatchedUpdater((9, 9), DungeonDespawningStrategy.Unused, 60, n_games=B, seed=5,
+                         n_npcs=2, device=torch.device("cuda", 0))
+    o = oracle_lib.Oracle(upd.engine.cfg.to_dict(), B, 5)
+    o.reset()
+    rng = np.random.default_rng(1)
+    for t in range(100):
+        a = rng.integers(1, 6, size=(B, 2)).astype(np.int8)
+        res = upd.update(a[:, 0], a[:, 1]).cpu().numpy()
+        o.step(a)
+        assert np.array_equal(res, o.export()["status"]), t
+    gs = upd.game_state(3)
+    assert gs.tick == int(o.export()["tick"][3])
+
+
+def test_bot_driver(oracle_lib):
+    import torch
+    from optimax_rogue_amd import EnvConfig
+    from optimax_rogue_amd.compat import BotDriver
+    from optimax_rogue_amd.engine import BatchedEngine
+    B = 64
+    cfg = EnvConfig(width=8, height=8, max_ticks=30, autoreset=0)
+    eng = BatchedEngine(cfg, B, seed=2, device=torch.device("cuda", 0))
+    ref = BatchedEngine(cfg, B, seed=2, device=torch.device("cuda", 0))
+    bots = [[ToStairsBot(1 + p) for _ in range(B)] for p in range(2)]
+    drv = BotDriver(eng, bots[0], bots[1])
+    for t in range(35):
+        drv.step()
+        ref.step(ref.policy(2, 2))
+        s1, s2 = eng.snapshot(), ref.snapshot()
+        for k in ("p_x", "p_y", "p_depth", "tick", "status"):
+            assert np.array_equal(s1[k], s2[k]), (t, k)
+    assert all(b.finished_with in (2, 3, 4) for b in bots[0])   # every game ended
