@@ -1,0 +1,28 @@
+"""Launch sequence for rocprofv3 counter passes (profiles/README.md):
+  rollout_kernel<8>: C3, B=65536, 50 ticks with obs/act  (x3)
+  step_kernel<8> + policy_kernel: C3, B=2^21             (x5)"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+
+from optimax_rogue_amd import EnvConfig
+from optimax_rogue_amd.engine import BatchedEngine
+
+dev = torch.device("cuda", 0)
+B, T = 65536, 50
+e = BatchedEngine(EnvConfig.c3(), B, seed=3, device=dev)
+obs = torch.empty((T, 14, B), dtype=torch.int32, device=dev)
+act = torch.empty((T, B, 2), dtype=torch.int8, device=dev)
+e.rollout(T, 1, 1, obs=obs, act=act)
+for _ in range(3):
+    e.rollout(T, 1, 1, obs=obs, act=act)
+torch.cuda.synchronize()
+del e, obs, act
+BL = 1 << 21
+e = BatchedEngine(EnvConfig.c3(), BL, seed=3, device=dev)
+for _ in range(6):
+    e.step(e.policy(1, 1))
+torch.cuda.synchronize()
+print("done")
