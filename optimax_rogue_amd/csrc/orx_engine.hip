@@ -122,6 +122,7 @@ struct NpBound {
 struct Player {
   int32_t x, y, d, hp, sx, sy;
   int32_t move;   // validated move for this tick
+  int32_t tx, ty; // target cell of `move` from the pre-tick position
 };
 
 // Field-wise select: a conditional copy of the whole struct would be lowered
@@ -135,6 +136,8 @@ __device__ __forceinline__ Player pick(bool c, const Player& a, const Player& b)
   r.sx = c ? a.sx : b.sx;
   r.sy = c ? a.sy : b.sy;
   r.move = c ? a.move : b.move;
+  r.tx = c ? a.tx : b.tx;
+  r.ty = c ? a.ty : b.ty;
   return r;
 }
 
@@ -184,6 +187,22 @@ struct Npcs {
     const int sh = (k & 1) * 16;
     wr(k >> 1, (rd(k >> 1) & ~(0xFFFFu << sh)) | ((v & 0xFFFFu) << sh));
   }
+  // True iff some slot holds `key`: zero-halfword test on (slots ^ key),
+  // (v - 0x00010001) & ~v & 0x80008000 is nonzero iff a 16-bit half is zero.
+  __device__ __forceinline__ bool any(uint32_t key) const {
+    if constexpr (NCAP == 0) {
+      return false;
+    } else {
+      const uint32_t k2 = key | (key << 16);
+      uint32_t z = 0;
+#pragma unroll
+      for (int r = 0; r < kRegs; ++r) {
+        const uint32_t x = rd(r) ^ k2;
+        z |= (x - 0x00010001u) & ~x & 0x80008000u;
+      }
+      return z != 0;
+    }
+  }
   // Slot holding `key` (a live NPC), or -1.
   __device__ __forceinline__ int find(uint32_t key) const {
     if constexpr (NCAP == 0) {
@@ -207,9 +226,15 @@ __device__ __forceinline__ uint32_t pack_xy(int32_t x, int32_t y) {
   return (uint32_t)(x & 0xFF) | ((uint32_t)(y & 0xFF) << 8);
 }
 
+// calculate_pos (updater.py:340-351) as two 2-bit lookup tables indexed by the
+// move (1..5): entry = delta + 1.  Up (0,-1), Right (+1,0), Down (0,+1),
+// Left (-1,0), Stay (0,0).
+constexpr uint32_t kDx = (1u << 2) | (2u << 4) | (1u << 6) | (0u << 8) | (1u << 10);
+constexpr uint32_t kDy = (0u << 2) | (1u << 4) | (2u << 6) | (1u << 8) | (1u << 10);
 __device__ __forceinline__ void calc_pos(int32_t x, int32_t y, int32_t m, int32_t& nx, int32_t& ny) {
-  nx = x + (m == ORX_MOVE_RIGHT) - (m == ORX_MOVE_LEFT);
-  ny = y + (m == ORX_MOVE_DOWN) - (m == ORX_MOVE_UP);
+  const uint32_t sh = (uint32_t)m << 1;
+  nx = x + (int32_t)((kDx >> sh) & 3u) - 1;
+  ny = y + (int32_t)((kDy >> sh) & 3u) - 1;
 }
 
 __device__ __forceinline__ bool blocked(const Cfg& c, int32_t x, int32_t y) {
@@ -366,26 +391,28 @@ __device__ __forceinline__ void random_moves(Key key, uint32_t game, uint32_t ep
   const uint32_t t = tag(PUR_POLICY, 0);
   const W4 b0 = philox(game, ep, (uint32_t)tick, t | 0u, key);
   const W4 b1 = philox(game, ep, (uint32_t)tick, t | 1u, key);
-  const uint32_t w[8] = {b0.a, b0.b, b0.c, b0.d, b1.a, b1.b, b1.c, b1.d};
-  int got = 0;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const uint32_t r = w[i] >> 29;
-    const bool acc = r < 5u;
-    m1 = (acc && got == 1) ? (int32_t)r + 1 : m1;
-    m0 = (acc && got == 0) ? (int32_t)r + 1 : m0;
-    got += (acc && got < 2) ? 1 : 0;
-  }
+  // r_i = w_i >> 29 packed as 3-bit fields; a field is rejected iff r >= 5,
+  // i.e. bit2 & (bit1 | bit0).  acc has bit 3i set for accepted words.
+  const uint32_t pk = (b0.a >> 29) | ((b0.b >> 29) << 3) | ((b0.c >> 29) << 6) |
+                      ((b0.d >> 29) << 9) | ((b1.a >> 29) << 12) | ((b1.b >> 29) << 15) |
+                      ((b1.c >> 29) << 18) | ((b1.d >> 29) << 21);
+  constexpr uint32_t kF = 0x249249u;  // bit 0 of each 3-bit field
+  const uint32_t acc = ~((pk >> 2) & (pk | (pk >> 1))) & kF;
+  const uint32_t acc2 = acc & (acc - 1u);
+  m0 = (int32_t)((pk >> (__ffs(acc) - 1)) & 7u) + 1;
+  m1 = (int32_t)((pk >> (__ffs(acc2) - 1)) & 7u) + 1;
+  const int got = acc == 0 ? 0 : acc2 == 0 ? 1 : 2;
   if (got < need) {  // rare: continue the stream at word 8
+    int g = got;
     Stream s;
     s.init(game, ep, (uint32_t)tick, t, 8);
-    for (uint32_t i = 8; i < kWordCap && got < need; ++i) {
+    for (uint32_t i = 8; i < kWordCap && g < need; ++i) {
       const uint32_t r = s.next(key) >> 29;
       if (r >= 5u) continue;
-      if (got == 0) m0 = (int32_t)r + 1; else m1 = (int32_t)r + 1;
-      ++got;
+      if (g == 0) m0 = (int32_t)r + 1; else m1 = (int32_t)r + 1;
+      ++g;
     }
-    if (got < need) err = true;
+    if (g < need) err = true;
   }
 }
 
@@ -396,10 +423,13 @@ __device__ __forceinline__ bool p1_first_draw(Key key, uint32_t game, uint32_t e
   const uint32_t t = tag(PUR_SHUFFLE, 0);
   const W4 b0 = philox(game, ep, (uint32_t)tick, t | 0u, key);
   const W4 b1 = philox(game, ep, (uint32_t)tick, t | 1u, key);
-  const uint32_t w[8] = {b0.a, b0.b, b0.c, b0.d, b1.a, b1.b, b1.c, b1.d};
-  int res = -1;
-#pragma unroll
-  for (int i = 7; i >= 0; --i) res = (w[i] >> 31) == 0 ? (int)((w[i] >> 30) & 1u) : res;
+  // top two bits of each word as 2-bit fields; accepted iff the field's high
+  // bit is clear; the result is the field's low bit (word bit 30).
+  const uint32_t pk = (b0.a >> 30) | ((b0.b >> 30) << 2) | ((b0.c >> 30) << 4) |
+                      ((b0.d >> 30) << 6) | ((b1.a >> 30) << 8) | ((b1.b >> 30) << 10) |
+                      ((b1.c >> 30) << 12) | ((b1.d >> 30) << 14);
+  const uint32_t acc = ~(pk >> 1) & 0x5555u;
+  int res = acc ? (int)((pk >> (__ffs(acc) - 1)) & 1u) : -1;
   if (res < 0) {  // rare (1/256): continue the stream at word 8
     Stream s;
     s.init(game, ep, (uint32_t)tick, t, 8);
@@ -456,11 +486,11 @@ __device__ __forceinline__ int handle_move(const Cfg& c, Key key, uint32_t game,
                                            const Npcs<NCAP>& npc, Stream& spawn, Deltas& dl,
                                            bool& err) {
   if (self.move == ORX_MOVE_STAY) return -1;
-  int32_t tx, ty;
-  calc_pos(self.x, self.y, self.move, tx, ty);
+  const int32_t tx = self.tx, ty = self.ty;
   const bool occ_other = other.d == self.d && other.x == tx && other.y == ty;
   int slot = -1;
-  if (NCAP > 0 && self.d == c.d1 && !occ_other) slot = npc.find(pack_xy(tx, ty));
+  if (NCAP > 0 && self.d == c.d1 && !occ_other && npc.any(pack_xy(tx, ty)))
+    slot = npc.find(pack_xy(tx, ty));
   const bool free = !occ_other && slot < 0;
   const bool stairs = free && tx == self.sx && ty == self.sy;
   if (free && !stairs) { self.x = tx; self.y = ty; }
@@ -501,11 +531,10 @@ __device__ __forceinline__ void tick_game(const Cfg& c, Key key, uint32_t game, 
                                           const NpcMem& m, int32_t& tick, int32_t& status,
                                           Deltas& dl) {
   bool err = false;
-  int32_t nx, ny;
-  calc_pos(p1.x, p1.y, p1.move, nx, ny);               // updater.py:89-98
-  if (blocked(c, nx, ny)) p1.move = ORX_MOVE_STAY;
-  calc_pos(p2.x, p2.y, p2.move, nx, ny);
-  if (blocked(c, nx, ny)) p2.move = ORX_MOVE_STAY;
+  calc_pos(p1.x, p1.y, p1.move, p1.tx, p1.ty);         // updater.py:89-98
+  if (blocked(c, p1.tx, p1.ty)) p1.move = ORX_MOVE_STAY;
+  calc_pos(p2.x, p2.y, p2.move, p2.tx, p2.ty);
+  if (blocked(c, p2.tx, p2.ty)) p2.move = ORX_MOVE_STAY;
 
   // The NPC shuffle (updater.py:127) draws later words of the same per-tick
   // stream and only orders Stay-ing NPCs, so it is unobservable and skipped.
@@ -763,21 +792,12 @@ __global__ void __launch_bounds__(256) rollout_kernel(orx_cfg_t hc, orx_state_t 
       npc_dirty = true;
     }
     if (obs) {
+      // uniform row base + 32-bit lane offset: saddr-form stores, no 64-bit VALU math
       int32_t* o = obs + (size_t)t * ORX_OBS_FIELDS * B;
-      o[(size_t)ORX_OBS_P1_X * B + i] = p1.x;
-      o[(size_t)ORX_OBS_P1_Y * B + i] = p1.y;
-      o[(size_t)ORX_OBS_P1_DEPTH * B + i] = p1.d;
-      o[(size_t)ORX_OBS_P1_HEALTH * B + i] = p1.hp;
-      o[(size_t)ORX_OBS_P2_X * B + i] = p2.x;
-      o[(size_t)ORX_OBS_P2_Y * B + i] = p2.y;
-      o[(size_t)ORX_OBS_P2_DEPTH * B + i] = p2.d;
-      o[(size_t)ORX_OBS_P2_HEALTH * B + i] = p2.hp;
-      o[(size_t)ORX_OBS_TICK * B + i] = tick;
-      o[(size_t)ORX_OBS_STATUS * B + i] = status;
-      o[(size_t)ORX_OBS_P1_STAIR_X * B + i] = p1.sx;
-      o[(size_t)ORX_OBS_P1_STAIR_Y * B + i] = p1.sy;
-      o[(size_t)ORX_OBS_P2_STAIR_X * B + i] = p2.sx;
-      o[(size_t)ORX_OBS_P2_STAIR_Y * B + i] = p2.sy;
+      const int32_t vals[ORX_OBS_FIELDS] = {p1.x, p1.y, p1.d, p1.hp, p2.x, p2.y, p2.d, p2.hp,
+                                            tick, status, p1.sx, p1.sy, p2.sx, p2.sy};
+#pragma unroll
+      for (int f = 0; f < ORX_OBS_FIELDS; ++f) (o + (size_t)f * B)[i] = vals[f];
     }
     if (act) reinterpret_cast<uint16_t*>(act)[(size_t)t * B + i] = pack_actions(a1, a2);
   }
