@@ -165,6 +165,10 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL, default) or gloo (multi-rank rehearsal on one GPU)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="every rank uses cuda:0 (rehearsing N ranks on a 1-GPU box)")
     args = ap.parse_args()
 
     import torch
@@ -175,9 +179,12 @@ def main():
     from optimax_rogue_amd.parallel import env_rank, gather_returns, init
 
     rank, world, local = env_rank()
+    if args.same_device:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    init("nccl" if world > 1 else None, dev)
+    init(args.dist_backend if world > 1 else None, dev)
+    coll_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
 
     cfg = EnvConfig.c3()
     B = args.batch
@@ -213,7 +220,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 

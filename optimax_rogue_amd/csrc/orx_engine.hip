@@ -383,19 +383,30 @@ __device__ __forceinline__ void descend(const Cfg& c, Key key, uint32_t game, ui
 // ---------------------------------------------------------------------------
 // Random words of one tick
 // ---------------------------------------------------------------------------
-// RandomBot.move = Move(1 + randbelow(5)): k = 3, r = w >> 29, accept r < 5.
-// Both players draw from the POLICY stream in order (p1 first).  Fast path:
-// two Philox blocks (8 words); lanes still short take the stream loop.
-__device__ __forceinline__ void random_moves(Key key, uint32_t game, uint32_t ep, int32_t tick,
-                                             int need, int32_t& m0, int32_t& m1, bool& err) {
-  const uint32_t t = tag(PUR_POLICY, 0);
-  const W4 b0 = philox(game, ep, (uint32_t)tick, t | 0u, key);
-  const W4 b1 = philox(game, ep, (uint32_t)tick, t | 1u, key);
-  // r_i = w_i >> 29 packed as 3-bit fields; a field is rejected iff r >= 5,
-  // i.e. bit2 & (bit1 | bit0).  acc has bit 3i set for accepted words.
-  const uint32_t pk = (b0.a >> 29) | ((b0.b >> 29) << 3) | ((b0.c >> 29) << 6) |
-                      ((b0.d >> 29) << 9) | ((b1.a >> 29) << 12) | ((b1.b >> 29) << 15) |
-                      ((b1.c >> 29) << 18) | ((b1.d >> 29) << 21);
+// The per-tick streams are consumed through two packed forms (8 words = two
+// Philox blocks; lanes still short after 8 words take the generic stream loop):
+//  * POLICY: RandomBot.move = Move(1 + randbelow(5)), k = 3: r = w >> 29 as
+//    3-bit fields, rejected iff r >= 5 (bit2 & (bit1 | bit0)); p1 then p2.
+//  * SHUFFLE: random.shuffle([p1, p2]) = randbelow(2), k = 2: r = w >> 30 as
+//    2-bit fields, accepted iff the high bit is clear; player 1 acts first iff
+//    the first accepted r == 1 (updater.py:114).
+// pack_words(b0, b1, 29 + s, 3 - s) with s = 0 (policy) or 1 (shuffle).
+__device__ __forceinline__ uint32_t pack_words(const W4& b0, const W4& b1, uint32_t sh,
+                                               uint32_t width) {
+  return (b0.a >> sh) | ((b0.b >> sh) << width) | ((b0.c >> sh) << (2 * width)) |
+         ((b0.d >> sh) << (3 * width)) | ((b1.a >> sh) << (4 * width)) |
+         ((b1.b >> sh) << (5 * width)) | ((b1.c >> sh) << (6 * width)) |
+         ((b1.d >> sh) << (7 * width));
+}
+
+__device__ __forceinline__ W4 tick_block(Key key, uint32_t game, uint32_t ep, int32_t tick,
+                                         uint32_t purpose, uint32_t blk) {
+  return philox(game, ep, (uint32_t)tick, tag(purpose, 0) | blk, key);
+}
+
+__device__ __forceinline__ void moves_from_packed(uint32_t pk, int need, Key key, uint32_t game,
+                                                  uint32_t ep, int32_t tick, int32_t& m0,
+                                                  int32_t& m1, bool& err) {
   constexpr uint32_t kF = 0x249249u;  // bit 0 of each 3-bit field
   const uint32_t acc = ~((pk >> 2) & (pk | (pk >> 1))) & kF;
   const uint32_t acc2 = acc & (acc - 1u);
@@ -405,7 +416,7 @@ __device__ __forceinline__ void random_moves(Key key, uint32_t game, uint32_t ep
   if (got < need) {  // rare: continue the stream at word 8
     int g = got;
     Stream s;
-    s.init(game, ep, (uint32_t)tick, t, 8);
+    s.init(game, ep, (uint32_t)tick, tag(PUR_POLICY, 0), 8);
     for (uint32_t i = 8; i < kWordCap && g < need; ++i) {
       const uint32_t r = s.next(key) >> 29;
       if (r >= 5u) continue;
@@ -416,23 +427,13 @@ __device__ __forceinline__ void random_moves(Key key, uint32_t game, uint32_t ep
   }
 }
 
-// random.shuffle([p1, p2]) = one randbelow(2): k = 2, r = w >> 30, accept
-// r < 2; player 1 acts first iff r == 1 (updater.py:114).
-__device__ __forceinline__ bool p1_first_draw(Key key, uint32_t game, uint32_t ep, int32_t tick,
-                                              bool& err) {
-  const uint32_t t = tag(PUR_SHUFFLE, 0);
-  const W4 b0 = philox(game, ep, (uint32_t)tick, t | 0u, key);
-  const W4 b1 = philox(game, ep, (uint32_t)tick, t | 1u, key);
-  // top two bits of each word as 2-bit fields; accepted iff the field's high
-  // bit is clear; the result is the field's low bit (word bit 30).
-  const uint32_t pk = (b0.a >> 30) | ((b0.b >> 30) << 2) | ((b0.c >> 30) << 4) |
-                      ((b0.d >> 30) << 6) | ((b1.a >> 30) << 8) | ((b1.b >> 30) << 10) |
-                      ((b1.c >> 30) << 12) | ((b1.d >> 30) << 14);
+__device__ __forceinline__ bool first_from_packed(uint32_t pk, Key key, uint32_t game, uint32_t ep,
+                                                  int32_t tick, bool& err) {
   const uint32_t acc = ~(pk >> 1) & 0x5555u;
   int res = acc ? (int)((pk >> (__ffs(acc) - 1)) & 1u) : -1;
   if (res < 0) {  // rare (1/256): continue the stream at word 8
     Stream s;
-    s.init(game, ep, (uint32_t)tick, t, 8);
+    s.init(game, ep, (uint32_t)tick, tag(PUR_SHUFFLE, 0), 8);
     for (uint32_t i = 8; i < kWordCap && res < 0; ++i) {
       const uint32_t r = s.next(key) >> 30;
       if (r < 2u) res = (int)r;
@@ -442,14 +443,28 @@ __device__ __forceinline__ bool p1_first_draw(Key key, uint32_t game, uint32_t e
   return res == 1;
 }
 
+__device__ __forceinline__ uint32_t policy_packed(Key key, uint32_t game, uint32_t ep, int32_t tick) {
+  return pack_words(tick_block(key, game, ep, tick, PUR_POLICY, 0),
+                    tick_block(key, game, ep, tick, PUR_POLICY, 1), 29, 3);
+}
+
+__device__ __forceinline__ bool p1_first_draw(Key key, uint32_t game, uint32_t ep, int32_t tick,
+                                              bool& err) {
+  const uint32_t pk = pack_words(tick_block(key, game, ep, tick, PUR_SHUFFLE, 0),
+                                 tick_block(key, game, ep, tick, PUR_SHUFFLE, 1), 30, 2);
+  return first_from_packed(pk, key, game, ep, tick, err);
+}
+
 // RandomBot / StaircaseBot moves for both players (policy codes ORX_POLICY_*).
+// pk_pol: policy_packed() of this tick (ignored when no player is random).
 __device__ __forceinline__ void policy_pair(Key key, uint32_t game, uint32_t ep, int32_t tick,
-                                            int32_t pol1, int32_t pol2, const Player& p1,
-                                            const Player& p2, int32_t& a1, int32_t& a2) {
+                                            int32_t pol1, int32_t pol2, uint32_t pk_pol,
+                                            const Player& p1, const Player& p2, int32_t& a1,
+                                            int32_t& a2) {
   const int need = (pol1 == ORX_POLICY_RANDOM) + (pol2 == ORX_POLICY_RANDOM);
   int32_t r0 = ORX_MOVE_STAY, r1 = ORX_MOVE_STAY;
   bool err = false;
-  if (need) random_moves(key, game, ep, tick, need, r0, r1, err);
+  if (need) moves_from_packed(pk_pol, need, key, game, ep, tick, r0, r1, err);
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
     const int32_t pol = p == 0 ? pol1 : pol2;
@@ -478,45 +493,53 @@ struct NpcMem {  // HBM rows of this game's NPC slots (stride B)
   uint32_t B, i;
 };
 
-// handle_move for `self` (updater.py:180-243).  Returns the NPC slot hit (or
-// -1); combat against the other player is applied here.
+// handle_move for `self` (updater.py:180-243), branch-free except for the
+// rare descend.  Returns true if the target cell holds an NPC (the slot is
+// resolved in npc_hits); combat against the other player is applied here.
 template <int NCAP>
-__device__ __forceinline__ int handle_move(const Cfg& c, Key key, uint32_t game, uint32_t ep,
-                                           Player& self, Player& other, int32_t other_start,
-                                           const Npcs<NCAP>& npc, Stream& spawn, Deltas& dl,
-                                           bool& err) {
-  if (self.move == ORX_MOVE_STAY) return -1;
+__device__ __forceinline__ bool handle_move(const Cfg& c, Key key, uint32_t game, uint32_t ep,
+                                            Player& self, Player& other, int32_t other_start,
+                                            const Npcs<NCAP>& npc, Stream& spawn, Deltas& dl,
+                                            bool& err) {
+  const bool moving = self.move != ORX_MOVE_STAY;
   const int32_t tx = self.tx, ty = self.ty;
-  const bool occ_other = other.d == self.d && other.x == tx && other.y == ty;
-  int slot = -1;
-  if (NCAP > 0 && self.d == c.d1 && !occ_other && npc.any(pack_xy(tx, ty)))
-    slot = npc.find(pack_xy(tx, ty));
-  const bool free = !occ_other && slot < 0;
+  const bool occ_other = moving && other.d == self.d && other.x == tx && other.y == ty;
+  const bool hit_npc = NCAP > 0 && moving && !occ_other && self.d == c.d1 &&
+                       npc.any(pack_xy(tx, ty));
+  const bool free = moving && !occ_other && !hit_npc;
   const bool stairs = free && tx == self.sx && ty == self.sy;
-  if (free && !stairs) { self.x = tx; self.y = ty; }
-  if (!free) {
-    // Block / Parry / Ambush / Flee (updater.py:222-243): without a Modifier
-    // subclass every flag deals og_dmg = attacker.damage - attacker.armor.
-    dl.combat += 1;
-    if (occ_other && c.player_dmg_net > 0) other.hp -= c.player_dmg_net;
-  }
+  const bool step = free && !stairs;
+  self.x = step ? tx : self.x;
+  self.y = step ? ty : self.y;
+  // Block / Parry / Ambush / Flee (updater.py:222-243): without a Modifier
+  // subclass every flag deals og_dmg = attacker.damage - attacker.armor.
+  dl.combat += (occ_other || hit_npc) ? 1 : 0;
+  other.hp -= (occ_other && c.player_dmg_net > 0) ? c.player_dmg_net : 0;
   if (stairs) descend(c, key, game, ep, self, other, other_start, npc, spawn, dl, err);
-  return slot;
+  return hit_npc;
 }
 
 // handle_combat on NPC defenders, then the death sweep (updater.py:136-145):
 // only NPCs hit this tick can reach health <= 0.
 template <int NCAP>
 __device__ __forceinline__ void npc_hits(const Cfg& c, Npcs<NCAP>& npc, const NpcMem& m, int h0,
-                                      int h1, Deltas& dl) {
+                                         int h1, bool writer, Deltas& dl) {
   const int dmg = c.player_dmg_net > 0 ? c.player_dmg_net : 0;
+  int8_t* p0 = m.hp + (size_t)(h0 >= 0 ? h0 : h1) * m.B + m.i;
+  int8_t* p1 = m.hp + (size_t)(h1 >= 0 ? h1 : h0) * m.B + m.i;
+  int v0 = *p0, v1 = *p1;
+  if (h0 >= 0) v0 -= dmg;
+  if (h1 >= 0) { v1 = (h1 == h0) ? v0 - dmg : v1 - dmg; if (h1 == h0) v0 = v1; }
+  if (writer) {
+    if (h0 >= 0) *p0 = (int8_t)v0;
+    if (h1 >= 0 && h1 != h0) *p1 = (int8_t)v1;
+  }
+  const int ks[2] = {h0, h1};
+  const int vs[2] = {v0, v1};
+#pragma unroll
   for (int j = 0; j < 2; ++j) {
-    const int k = j == 0 ? h0 : h1;
-    if (k < 0) continue;
-    int8_t* h = m.hp + (size_t)k * m.B + m.i;
-    const int8_t nh = (int8_t)(*h - dmg);
-    *h = nh;
-    if (nh <= 0 && ((npc.alive >> k) & 1u)) {
+    const int k = ks[j];
+    if (k >= 0 && (int8_t)vs[j] <= 0 && ((npc.alive >> k) & 1u)) {
       npc.alive &= ~(1u << k);
       npc.set(k, kDeadSlot);
       dl.npc_death += 1;
@@ -527,30 +550,34 @@ __device__ __forceinline__ void npc_hits(const Cfg& c, Npcs<NCAP>& npc, const Np
 // One Updater.update for an in-progress game; p1.move/p2.move = raw moves.
 template <int NCAP>
 __device__ __forceinline__ void tick_game(const Cfg& c, Key key, uint32_t game, uint32_t ep,
-                                          Player& p1, Player& p2, Npcs<NCAP>& npc,
-                                          const NpcMem& m, int32_t& tick, int32_t& status,
-                                          Deltas& dl) {
-  bool err = false;
+                                          bool p1_first, bool writer, Player& p1, Player& p2,
+                                          Npcs<NCAP>& npc, const NpcMem& m, int32_t& tick,
+                                          int32_t& status, bool& err, Deltas& dl) {
   calc_pos(p1.x, p1.y, p1.move, p1.tx, p1.ty);         // updater.py:89-98
   if (blocked(c, p1.tx, p1.ty)) p1.move = ORX_MOVE_STAY;
   calc_pos(p2.x, p2.y, p2.move, p2.tx, p2.ty);
   if (blocked(c, p2.tx, p2.ty)) p2.move = ORX_MOVE_STAY;
 
-  // The NPC shuffle (updater.py:127) draws later words of the same per-tick
-  // stream and only orders Stay-ing NPCs, so it is unobservable and skipped.
-  const bool p1_first = p1_first_draw(key, game, ep, tick, err);
-
+  // p1_first: the player shuffle (updater.py:114).  The NPC shuffle (:127)
+  // draws later words of the same per-tick stream and only orders Stay-ing
+  // NPCs, so it is unobservable and skipped.
   Stream spawn;
   spawn.init(game, ep, (uint32_t)tick, tag(PUR_SPAWN, 0));
   Player A = pick(p1_first, p1, p2);
   Player Bp = pick(p1_first, p2, p1);
   const int32_t a_start = p1_first ? c.d1 : c.d2;
   const int32_t b_start = p1_first ? c.d2 : c.d1;
-  const int h0 = handle_move(c, key, game, ep, A, Bp, b_start, npc, spawn, dl, err);
-  const int h1 = handle_move(c, key, game, ep, Bp, A, a_start, npc, spawn, dl, err);
+  const bool hA = handle_move(c, key, game, ep, A, Bp, b_start, npc, spawn, dl, err);
+  const bool hB = handle_move(c, key, game, ep, Bp, A, a_start, npc, spawn, dl, err);
+  if (NCAP > 0 && (hA || hB)) {
+    // NPCs never move and are swept only after both moves: the slots found at
+    // the targets now are the ones that were attacked.
+    const int h0 = hA ? npc.find(pack_xy(A.tx, A.ty)) : -1;
+    const int h1 = hB ? npc.find(pack_xy(Bp.tx, Bp.ty)) : -1;
+    npc_hits(c, npc, m, h0, h1, writer, dl);
+  }
   p1 = pick(p1_first, A, Bp);
   p2 = pick(p1_first, Bp, A);
-  if (NCAP > 0 && (h0 >= 0 || h1 >= 0)) npc_hits(c, npc, m, h0, h1, dl);
 
   tick += 1;                                           // updater.py:148-162
   if (p1.hp <= 0)
@@ -720,7 +747,9 @@ __global__ void __launch_bounds__(256) step_kernel(orx_cfg_t hc, orx_state_t st,
   load_npcs(st, c, B, i, npc);
   const NpcMem m{st.npc_pos, st.npc_health, B, i};
   Deltas dl = {0, 0, 0, 0, 0, 0};
-  tick_game(c, key, game, ep, p1, p2, npc, m, tick, status, dl);
+  bool err = false;
+  const bool p1_first = p1_first_draw(key, game, ep, tick, err);
+  tick_game(c, key, game, ep, p1_first, true, p1, p2, npc, m, tick, status, err, dl);
   store_players(st, B, i, p1, p2, dl.descend != 0);
   st.tick[i] = tick;
   st.status[i] = status;
@@ -750,12 +779,16 @@ __global__ void __launch_bounds__(256) policy_kernel(orx_state_t st, int32_t pol
     a1 = (int8_t)(prev & 0xFF);
     a2 = (int8_t)(prev >> 8);
   }
-  policy_pair(key, off + i, ep, tick, pol1, pol2, p1, p2, a1, a2);
+  const uint32_t pk = need_rng ? policy_packed(key, off + i, ep, tick) : 0u;
+  policy_pair(key, off + i, ep, tick, pol1, pol2, pk, p1, p2, a1, a2);
   out[i] = pack_actions(a1, a2);
 }
 
 // Fused rollout: n_ticks x (policy, step); state and NPC positions stay in
 // registers; tick t's observation row is streamed out to obs/act.
+// (Splitting a game's two random streams over two lanes -- two waves per SIMD
+// at 65,536 games -- was measured 22% slower: the replicated game logic costs
+// more than the halved Philox saves.)
 template <int NCAP>
 __global__ void __launch_bounds__(256) rollout_kernel(orx_cfg_t hc, orx_state_t st, int32_t pol1,
                                                       int32_t pol2, int32_t n_ticks,
@@ -776,13 +809,17 @@ __global__ void __launch_bounds__(256) rollout_kernel(orx_cfg_t hc, orx_state_t 
   const NpcMem m{st.npc_pos, st.npc_health, B, i};
   Deltas dl = {0, 0, 0, 0, 0, 0};
   bool stairs_dirty = false, npc_dirty = false;
+  const bool any_random = pol1 == ORX_POLICY_RANDOM || pol2 == ORX_POLICY_RANDOM;
   for (int32_t t = 0; t < n_ticks; ++t) {
+    const uint32_t pk_pol = any_random ? policy_packed(key, game, ep, tick) : 0u;
     int32_t a1 = ORX_MOVE_STAY, a2 = ORX_MOVE_STAY;
-    policy_pair(key, game, ep, tick, pol1, pol2, p1, p2, a1, a2);
+    policy_pair(key, game, ep, tick, pol1, pol2, pk_pol, p1, p2, a1, a2);
     if (status == ORX_IN_PROGRESS) {
       p1.move = a1; p2.move = a2;
       const int32_t descents = dl.descend;
-      tick_game(c, key, game, ep, p1, p2, npc, m, tick, status, dl);
+      bool err = false;
+      const bool p1_first = p1_first_draw(key, game, ep, tick, err);
+      tick_game(c, key, game, ep, p1_first, true, p1, p2, npc, m, tick, status, err, dl);
       stairs_dirty |= dl.descend != descents;
     } else if (c.autoreset) {
       ep += 1;
@@ -792,7 +829,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(orx_cfg_t hc, orx_state_t 
       npc_dirty = true;
     }
     if (obs) {
-      // uniform row base + 32-bit lane offset: saddr-form stores, no 64-bit VALU math
+      // uniform row base + 32-bit lane index
       int32_t* o = obs + (size_t)t * ORX_OBS_FIELDS * B;
       const int32_t vals[ORX_OBS_FIELDS] = {p1.x, p1.y, p1.d, p1.hp, p2.x, p2.y, p2.d, p2.hp,
                                             tick, status, p1.sx, p1.sy, p2.sx, p2.sy};

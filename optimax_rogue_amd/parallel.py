@@ -55,9 +55,11 @@ def gather_returns(local: torch.Tensor, global_batch: int,
         return local
     world = dist.get_world_size(group)
     width = -(-int(global_batch) // world)
-    padded = torch.zeros((local.shape[0], width), dtype=local.dtype, device=local.device)
-    padded[:, : local.shape[1]] = local
+    # gloo collectives run on host tensors; nccl (RCCL) on device tensors
+    dev = local.device if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    padded = torch.zeros((local.shape[0], width), dtype=local.dtype, device=dev)
+    padded[:, : local.shape[1]] = local.to(dev)
     outs = [torch.empty_like(padded) for _ in range(world)]
     dist.all_gather(outs, padded, group=group)
     parts = [outs[r][:, : shard(global_batch, r, world)[1]] for r in range(world)]
-    return torch.cat(parts, dim=1)
+    return torch.cat(parts, dim=1).to(local.device)
