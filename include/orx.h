@@ -83,6 +83,18 @@ extern "C" {
 #define ORX_CNT_NPC_DEATH 3     /* EntityDeathUpdate sweeps  updater.py:136  */
 #define ORX_NCOUNTERS 4
 
+/* update events (orx_step_events), int32 records {type, iden, a, b}:
+ *   COMBAT   {1, attacker, defender, CombatFlag}  EntityCombatUpdate   updates.py:71-139
+ *   DEATH    {2, npc iden, 0, 0}                  EntityDeathUpdate    updates.py:167-184
+ *   POSITION {3, iden, new depth, x | y << 16}    EntityPositionUpdate updates.py:186-220
+ *   DUNGEON  {4, 0, depth, 0}                     DungeonCreatedUpdate updates.py:308-335
+ * Entity idens: player 1 = 1, player 2 = 2, NPC slot k = 3 + k.           */
+#define ORX_EV_COMBAT 1
+#define ORX_EV_DEATH 2
+#define ORX_EV_POSITION 3
+#define ORX_EV_DUNGEON 4
+#define ORX_MAX_EVENTS 8 /* per game per tick (at most 6 occur)            */
+
 #define ORX_MAX_NPCS 16 /* NPCs per game (alive mask is 32-bit; registers)  */
 #define ORX_MAX_GRID_NPC 256 /* NPC (x,y) pack into 8+8 bits when K > 0    */
 
@@ -178,6 +190,14 @@ int orx_reset(const orx_cfg_t* cfg, const orx_state_t* st, const uint8_t* mask,
  * else left unchanged. */
 int orx_step(const orx_cfg_t* cfg, const orx_state_t* st, const int8_t* actions,
              int64_t n_games, uint64_t seed, int64_t game_offset, void* stream);
+
+/* orx_step plus the update-event list of the tick: for game b,
+ * events[(b * ORX_MAX_EVENTS + j) * 4 + 0..3], j < n_events[b], in the order
+ * Updater.update appends them to its result list (updater.py:133-145).
+ * Steps that reset a game (autoreset) or reject an action record none. */
+int orx_step_events(const orx_cfg_t* cfg, const orx_state_t* st, const int8_t* actions,
+                    int32_t* events, int32_t* n_events, int64_t n_games, uint64_t seed,
+                    int64_t game_offset, void* stream);
 
 /* Writes actions[b][p] from the stock bots.  Replaces
  * RandomBot.move    optimax_rogue_bots/randombot.py:20-21

@@ -32,7 +32,7 @@ class OrxError(RuntimeError):
 _lib = None
 
 EXPORTS = ("orx_abi_version", "orx_last_error", "orx_validate_cfg", "orx_reset", "orx_step",
-           "orx_policy", "orx_rollout")
+           "orx_step_events", "orx_policy", "orx_rollout")
 
 
 def load() -> ctypes.CDLL:
@@ -58,6 +58,8 @@ def load() -> ctypes.CDLL:
     L.orx_reset.argtypes = [P(OrxCfg), P(OrxState), vp, i64, u64, i64, vp]
     L.orx_step.restype = ctypes.c_int
     L.orx_step.argtypes = [P(OrxCfg), P(OrxState), vp, i64, u64, i64, vp]
+    L.orx_step_events.restype = ctypes.c_int
+    L.orx_step_events.argtypes = [P(OrxCfg), P(OrxState), vp, vp, vp, i64, u64, i64, vp]
     L.orx_policy.restype = ctypes.c_int
     L.orx_policy.argtypes = [P(OrxCfg), P(OrxState), i32, i32, vp, i64, u64, i64, vp]
     L.orx_rollout.restype = ctypes.c_int

@@ -154,6 +154,23 @@ struct Deltas {  // counter / return increments, flushed once per launch
   int32_t combat, descend, dungeon, npc_death, ret, eps;
 };
 
+// Update-event sink (orx_step_events): records {type, iden, a, b} in the
+// order the reference appends GameStateUpdates (updater.py:133-145).  With
+// EV = false every emit compiles away.
+template <bool EV>
+struct Events {
+  int32_t* base;  // this game's [ORX_MAX_EVENTS][4]
+  int32_t n;
+  __device__ __forceinline__ void emit(int32_t type, int32_t iden, int32_t a, int32_t b) {
+    if constexpr (EV) {
+      if (n < ORX_MAX_EVENTS) {
+        base[4 * n] = type; base[4 * n + 1] = iden; base[4 * n + 2] = a; base[4 * n + 3] = b;
+      }
+      ++n;
+    }
+  }
+};
+
 // NPC slots in registers: packed (x | y << 8) u16 pairs; dead slot = 0xFFFF,
 // which no legal target can equal (targets are interior cells, x, y <= 254).
 template <int NCAP>
@@ -341,10 +358,11 @@ __device__ __forceinline__ void setup_game(const Cfg& c, Key key, uint32_t game,
 //   Unused:      World == {p1.d, p2.d}, so nd is present iff other.d == nd;
 //                a fresh copy is generation 1 iff the other player already
 //                passed through nd (other.start <= nd < other.d).
-template <int NCAP>
+template <int NCAP, bool EV>
 __device__ __forceinline__ void descend(const Cfg& c, Key key, uint32_t game, uint32_t ep,
                                      Player& self, const Player& other, int32_t other_start,
-                                     const Npcs<NCAP>& npc, Stream& spawn, Deltas& dl, bool& err) {
+                                     const Npcs<NCAP>& npc, Stream& spawn, Deltas& dl, bool& err,
+                                     int32_t self_iden, Events<EV>& ev) {
   const int32_t nd = self.d + 1;
   bool present;
   uint32_t gen = 0;
@@ -360,7 +378,10 @@ __device__ __forceinline__ void descend(const Cfg& c, Key key, uint32_t game, ui
   } else {
     dungeon_stair(c, key, game, ep, nd, gen, sx, sy, err);
   }
-  if (!present) dl.dungeon += 1;
+  if (!present) {
+    dl.dungeon += 1;
+    ev.emit(ORX_EV_DUNGEON, 0, nd, 0);                 // updater.py:278-280
+  }
   const bool npc_depth = NCAP > 0 && nd == c.d1 && npc.alive;
   int32_t x = 0, y = 0;
   bool done = false;
@@ -378,6 +399,7 @@ __device__ __forceinline__ void descend(const Cfg& c, Key key, uint32_t game, ui
   if (!done) err = true;
   self.d = nd; self.x = x; self.y = y; self.sx = sx; self.sy = sy;
   dl.descend += 1;
+  ev.emit(ORX_EV_POSITION, self_iden, nd, (x & 0xFFFF) | (y << 16));  // updater.py:287-290
 }
 
 // ---------------------------------------------------------------------------
@@ -496,11 +518,12 @@ struct NpcMem {  // HBM rows of this game's NPC slots (stride B)
 // handle_move for `self` (updater.py:180-243), branch-free except for the
 // rare descend.  Returns true if the target cell holds an NPC (the slot is
 // resolved in npc_hits); combat against the other player is applied here.
-template <int NCAP>
+template <int NCAP, bool EV>
 __device__ __forceinline__ bool handle_move(const Cfg& c, Key key, uint32_t game, uint32_t ep,
                                             Player& self, Player& other, int32_t other_start,
                                             const Npcs<NCAP>& npc, Stream& spawn, Deltas& dl,
-                                            bool& err) {
+                                            bool& err, int32_t self_iden, bool self_first,
+                                            Events<EV>& ev) {
   const bool moving = self.move != ORX_MOVE_STAY;
   const int32_t tx = self.tx, ty = self.ty;
   const bool occ_other = moving && other.d == self.d && other.x == tx && other.y == ty;
@@ -515,15 +538,28 @@ __device__ __forceinline__ bool handle_move(const Cfg& c, Key key, uint32_t game
   // subclass every flag deals og_dmg = attacker.damage - attacker.armor.
   dl.combat += (occ_other || hit_npc) ? 1 : 0;
   other.hp -= (occ_other && c.player_dmg_net > 0) ? c.player_dmg_net : 0;
-  if (stairs) descend(c, key, game, ep, self, other, other_start, npc, spawn, dl, err);
+  if constexpr (EV) {
+    if (occ_other) {
+      int32_t ox, oy;
+      calc_pos(other.x, other.y, other.move, ox, oy);
+      const int32_t flag = other.move == ORX_MOVE_STAY        ? ORX_FLAG_BLOCK
+                           : (ox == tx && oy == ty)            ? ORX_FLAG_PARRY
+                           : !self_first                       ? ORX_FLAG_AMBUSH
+                                                               : ORX_FLAG_FLEE;
+      ev.emit(ORX_EV_COMBAT, self_iden, 3 - self_iden, flag);
+    }
+    if (hit_npc) ev.emit(ORX_EV_COMBAT, self_iden, 3 + npc.find(pack_xy(tx, ty)), ORX_FLAG_BLOCK);
+    if (step) ev.emit(ORX_EV_POSITION, self_iden, self.d, (tx & 0xFFFF) | (ty << 16));
+  }
+  if (stairs) descend(c, key, game, ep, self, other, other_start, npc, spawn, dl, err, self_iden, ev);
   return hit_npc;
 }
 
 // handle_combat on NPC defenders, then the death sweep (updater.py:136-145):
 // only NPCs hit this tick can reach health <= 0.
-template <int NCAP>
+template <int NCAP, bool EV>
 __device__ __forceinline__ void npc_hits(const Cfg& c, Npcs<NCAP>& npc, const NpcMem& m, int h0,
-                                         int h1, bool writer, Deltas& dl) {
+                                         int h1, bool writer, Deltas& dl, Events<EV>& ev) {
   const int dmg = c.player_dmg_net > 0 ? c.player_dmg_net : 0;
   int8_t* p0 = m.hp + (size_t)(h0 >= 0 ? h0 : h1) * m.B + m.i;
   int8_t* p1 = m.hp + (size_t)(h1 >= 0 ? h1 : h0) * m.B + m.i;
@@ -534,8 +570,10 @@ __device__ __forceinline__ void npc_hits(const Cfg& c, Npcs<NCAP>& npc, const Np
     if (h0 >= 0) *p0 = (int8_t)v0;
     if (h1 >= 0 && h1 != h0) *p1 = (int8_t)v1;
   }
-  const int ks[2] = {h0, h1};
-  const int vs[2] = {v0, v1};
+  // the sweep walks GameState.entities backwards: higher slot first
+  const bool swap = h1 > h0;
+  const int ks[2] = {swap ? h1 : h0, swap ? h0 : h1};
+  const int vs[2] = {swap ? v1 : v0, swap ? v0 : v1};
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int k = ks[j];
@@ -543,16 +581,18 @@ __device__ __forceinline__ void npc_hits(const Cfg& c, Npcs<NCAP>& npc, const Np
       npc.alive &= ~(1u << k);
       npc.set(k, kDeadSlot);
       dl.npc_death += 1;
+      ev.emit(ORX_EV_DEATH, 3 + k, 0, 0);
     }
   }
 }
 
 // One Updater.update for an in-progress game; p1.move/p2.move = raw moves.
-template <int NCAP>
+template <int NCAP, bool EV>
 __device__ __forceinline__ void tick_game(const Cfg& c, Key key, uint32_t game, uint32_t ep,
                                           bool p1_first, bool writer, Player& p1, Player& p2,
                                           Npcs<NCAP>& npc, const NpcMem& m, int32_t& tick,
-                                          int32_t& status, bool& err, Deltas& dl) {
+                                          int32_t& status, bool& err, Deltas& dl,
+                                          Events<EV>& ev) {
   calc_pos(p1.x, p1.y, p1.move, p1.tx, p1.ty);         // updater.py:89-98
   if (blocked(c, p1.tx, p1.ty)) p1.move = ORX_MOVE_STAY;
   calc_pos(p2.x, p2.y, p2.move, p2.tx, p2.ty);
@@ -567,14 +607,17 @@ __device__ __forceinline__ void tick_game(const Cfg& c, Key key, uint32_t game, 
   Player Bp = pick(p1_first, p2, p1);
   const int32_t a_start = p1_first ? c.d1 : c.d2;
   const int32_t b_start = p1_first ? c.d2 : c.d1;
-  const bool hA = handle_move(c, key, game, ep, A, Bp, b_start, npc, spawn, dl, err);
-  const bool hB = handle_move(c, key, game, ep, Bp, A, a_start, npc, spawn, dl, err);
+  const int32_t a_iden = p1_first ? 1 : 2;
+  const bool hA = handle_move(c, key, game, ep, A, Bp, b_start, npc, spawn, dl, err, a_iden, true,
+                              ev);
+  const bool hB = handle_move(c, key, game, ep, Bp, A, a_start, npc, spawn, dl, err, 3 - a_iden,
+                              false, ev);
   if (NCAP > 0 && (hA || hB)) {
     // NPCs never move and are swept only after both moves: the slots found at
     // the targets now are the ones that were attacked.
     const int h0 = hA ? npc.find(pack_xy(A.tx, A.ty)) : -1;
     const int h1 = hB ? npc.find(pack_xy(Bp.tx, Bp.ty)) : -1;
-    npc_hits(c, npc, m, h0, h1, writer, dl);
+    npc_hits(c, npc, m, h0, h1, writer, dl, ev);
   }
   p1 = pick(p1_first, A, Bp);
   p2 = pick(p1_first, Bp, A);
@@ -708,10 +751,12 @@ __global__ void __launch_bounds__(256) reset_kernel(orx_cfg_t hc, orx_state_t st
   }
 }
 
-template <int NCAP>
+template <int NCAP, bool EV>
 __global__ void __launch_bounds__(256) step_kernel(orx_cfg_t hc, orx_state_t st,
                                                    const int8_t* __restrict__ actions, uint32_t B,
-                                                   Key key, uint32_t off) {
+                                                   Key key, uint32_t off,
+                                                   int32_t* __restrict__ events,
+                                                   int32_t* __restrict__ n_events) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= B) return;
   const Cfg c = make_cfg(hc);
@@ -720,6 +765,7 @@ __global__ void __launch_bounds__(256) step_kernel(orx_cfg_t hc, orx_state_t st,
   Npcs<NCAP> npc;
   Player p1, p2;
   if (status != ORX_IN_PROGRESS) {
+    if (EV) n_events[i] = 0;
     if (!c.autoreset) return;
     const uint32_t ep = (uint32_t)st.episode[i] + 1u;
     int32_t tick;
@@ -739,6 +785,7 @@ __global__ void __launch_bounds__(256) step_kernel(orx_cfg_t hc, orx_state_t st,
   p2.move = (int8_t)(a >> 8);
   if (!valid_move(p1.move) || !valid_move(p2.move)) {
     st.status[i] = ORX_STATUS_BAD_ACTION;
+    if (EV) n_events[i] = 0;
     return;
   }
   const uint32_t ep = (uint32_t)st.episode[i];
@@ -747,14 +794,16 @@ __global__ void __launch_bounds__(256) step_kernel(orx_cfg_t hc, orx_state_t st,
   load_npcs(st, c, B, i, npc);
   const NpcMem m{st.npc_pos, st.npc_health, B, i};
   Deltas dl = {0, 0, 0, 0, 0, 0};
+  Events<EV> ev{EV ? events + (size_t)i * ORX_MAX_EVENTS * 4 : nullptr, 0};
   bool err = false;
   const bool p1_first = p1_first_draw(key, game, ep, tick, err);
-  tick_game(c, key, game, ep, p1_first, true, p1, p2, npc, m, tick, status, err, dl);
+  tick_game(c, key, game, ep, p1_first, true, p1, p2, npc, m, tick, status, err, dl, ev);
   store_players(st, B, i, p1, p2, dl.descend != 0);
   st.tick[i] = tick;
   st.status[i] = status;
   if (NCAP > 0 && dl.npc_death) st.npc_alive[i] = npc.alive;
   flush_deltas(st, B, i, dl);
+  if (EV) n_events[i] = ev.n;
 }
 
 __global__ void __launch_bounds__(256) policy_kernel(orx_state_t st, int32_t pol1, int32_t pol2,
@@ -819,7 +868,8 @@ __global__ void __launch_bounds__(256) rollout_kernel(orx_cfg_t hc, orx_state_t 
       const int32_t descents = dl.descend;
       bool err = false;
       const bool p1_first = p1_first_draw(key, game, ep, tick, err);
-      tick_game(c, key, game, ep, p1_first, true, p1, p2, npc, m, tick, status, err, dl);
+      Events<false> ev{nullptr, 0};
+      tick_game(c, key, game, ep, p1_first, true, p1, p2, npc, m, tick, status, err, dl, ev);
       stairs_dirty |= dl.descend != descents;
     } else if (c.autoreset) {
       ep += 1;
@@ -966,28 +1016,47 @@ int orx_reset(const orx_cfg_t* cfg, const orx_state_t* st, const uint8_t* mask, 
   return launch_status("orx_reset");
 }
 
-int orx_step(const orx_cfg_t* cfg, const orx_state_t* st, const int8_t* actions, int64_t n_games,
-             uint64_t seed, int64_t game_offset, void* stream) {
+static int launch_step(const orx_cfg_t* cfg, const orx_state_t* st, const int8_t* actions,
+                       int32_t* events, int32_t* n_events, int64_t n_games, uint64_t seed,
+                       int64_t game_offset, void* stream, const char* name) {
   int r;
   if ((r = check_cfg(cfg)) || (r = check_sizes(n_games, game_offset))) return r;
   if (n_games == 0) return ORX_OK;
   if ((r = check_state(cfg, st, true))) return r;
   if (!actions) return fail(ORX_EINVAL, "actions is NULL");
+  const bool ev = events != nullptr;
+  if (ev != (n_events != nullptr)) return fail(ORX_EINVAL, "events and n_events go together");
   const uint32_t B = (uint32_t)n_games, off = (uint32_t)game_offset;
   const hipStream_t s = (hipStream_t)stream;
   const Key k = make_key(seed);
-  switch (ncap_for(cfg->n_npcs)) {
-    case 0:
-      hipLaunchKernelGGL(step_kernel<0>, grid_for(B), dim3(kBlock), 0, s, *cfg, *st, actions, B, k, off);
-      break;
-    case 8:
-      hipLaunchKernelGGL(step_kernel<8>, grid_for(B), dim3(kBlock), 0, s, *cfg, *st, actions, B, k, off);
-      break;
-    default:
-      hipLaunchKernelGGL(step_kernel<16>, grid_for(B), dim3(kBlock), 0, s, *cfg, *st, actions, B, k, off);
-      break;
+#define ORX_STEP(NC, E)                                                                       \
+  hipLaunchKernelGGL((step_kernel<NC, E>), grid_for(B), dim3(kBlock), 0, s, *cfg, *st, actions, \
+                     B, k, off, events, n_events)
+  switch (ncap_for(cfg->n_npcs) * 2 + (ev ? 1 : 0)) {
+    case 0: ORX_STEP(0, false); break;
+    case 1: ORX_STEP(0, true); break;
+    case 16: ORX_STEP(8, false); break;
+    case 17: ORX_STEP(8, true); break;
+    case 32: ORX_STEP(16, false); break;
+    default: ORX_STEP(16, true); break;
   }
-  return launch_status("orx_step");
+#undef ORX_STEP
+  return launch_status(name);
+}
+
+int orx_step(const orx_cfg_t* cfg, const orx_state_t* st, const int8_t* actions, int64_t n_games,
+             uint64_t seed, int64_t game_offset, void* stream) {
+  return launch_step(cfg, st, actions, nullptr, nullptr, n_games, seed, game_offset, stream,
+                     "orx_step");
+}
+
+int orx_step_events(const orx_cfg_t* cfg, const orx_state_t* st, const int8_t* actions,
+                    int32_t* events, int32_t* n_events, int64_t n_games, uint64_t seed,
+                    int64_t game_offset, void* stream) {
+  if (n_games > 0 && (!events || !n_events))
+    return fail(ORX_EINVAL, "orx_step_events needs events and n_events");
+  return launch_step(cfg, st, actions, events, n_events, n_games, seed, game_offset, stream,
+                     "orx_step_events");
 }
 
 int orx_policy(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p1, int32_t policy_p2,

@@ -17,7 +17,7 @@ import torch
 
 from . import _lib
 from .config import EnvConfig
-from .enums import N_COUNTERS, OBS_FIELDS, Policy
+from .enums import MAX_EVENTS, N_COUNTERS, OBS_FIELDS, Policy
 
 STATE_FIELDS = ("p_x", "p_y", "p_depth", "p_health", "st_x", "st_y", "tick", "status", "episode",
                 "ret_sum", "ep_count", "counters", "npc_pos", "npc_health", "npc_alive")
@@ -100,16 +100,26 @@ class BatchedEngine:
                 raise ValueError("mask must have n_games elements")
         self._call("orx_reset", _ptr(m8), self.B, self.seed, self.game_offset, self._stream())
 
-    def step(self, actions: Optional[torch.Tensor] = None) -> torch.Tensor:
+    def step(self, actions: Optional[torch.Tensor] = None, events: bool = False):
         """Updater.update for every game: actions[b] = (player 1, player 2) Move
-        values.  Returns the status tensor (UpdateResult codes, asynchronous)."""
+        values.  Returns the status tensor (UpdateResult codes, asynchronous);
+        with ``events=True`` returns ``(status, events, n_events)``: the tick's
+        update-event records int32 [n_games, MAX_EVENTS, 4] and their counts
+        (include/orx.h ORX_EV_*), in the reference's GameStateUpdate order."""
         a = self.actions if actions is None else actions
         if a.dtype != torch.int8 or a.shape != (self.B, 2) or not a.is_contiguous() \
                 or a.device != self.device:
             raise ValueError("actions must be a contiguous int8 [n_games, 2] tensor on "
                              f"{self.device}")
-        self._call("orx_step", _ptr(a), self.B, self.seed, self.game_offset, self._stream())
-        return self.status
+        if not events:
+            self._call("orx_step", _ptr(a), self.B, self.seed, self.game_offset, self._stream())
+            return self.status
+        if getattr(self, "_ev", None) is None:
+            self._ev = torch.zeros((self.B, MAX_EVENTS, 4), dtype=torch.int32, device=self.device)
+            self._nev = torch.zeros(self.B, dtype=torch.int32, device=self.device)
+        self._call("orx_step_events", _ptr(a), _ptr(self._ev), _ptr(self._nev), self.B, self.seed,
+                   self.game_offset, self._stream())
+        return self.status, self._ev, self._nev
 
     def policy(self, p1: int = Policy.Random, p2: int = Policy.Random,
                out: Optional[torch.Tensor] = None) -> torch.Tensor:

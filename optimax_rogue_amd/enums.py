@@ -68,3 +68,7 @@ MAX_NPCS = 16
 OBS_FIELDS = ("p1_x", "p1_y", "p1_depth", "p1_health", "p2_x", "p2_y", "p2_depth",
               "p2_health", "tick", "status", "p1_stair_x", "p1_stair_y", "p2_stair_x",
               "p2_stair_y")
+
+# update-event records of orx_step_events (include/orx.h ORX_EV_*)
+EV_COMBAT, EV_DEATH, EV_POSITION, EV_DUNGEON = 1, 2, 3, 4
+MAX_EVENTS = 8

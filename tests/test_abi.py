@@ -37,7 +37,7 @@ def lib():
 def test_library_exports_every_declared_symbol(lib):
     decl = declared_functions()
     assert decl == sorted(["orx_abi_version", "orx_last_error", "orx_validate_cfg", "orx_reset",
-                           "orx_step", "orx_policy", "orx_rollout"])
+                           "orx_step", "orx_step_events", "orx_policy", "orx_rollout"])
     from optimax_rogue_amd import _lib
     assert sorted(_lib.EXPORTS) == decl
     for name in decl:
@@ -71,6 +71,9 @@ def test_enum_values_match_header():
     assert enums.STATUS_BAD_ACTION == val("ORX_STATUS_BAD_ACTION")
     assert enums.MAX_NPCS == val("ORX_MAX_NPCS")
     assert len(enums.OBS_FIELDS) == val("ORX_OBS_FIELDS")
+    assert (enums.EV_COMBAT, enums.EV_DEATH, enums.EV_POSITION, enums.EV_DUNGEON) == (
+        val("ORX_EV_COMBAT"), val("ORX_EV_DEATH"), val("ORX_EV_POSITION"), val("ORX_EV_DUNGEON"))
+    assert enums.MAX_EVENTS == val("ORX_MAX_EVENTS")
 
 
 def test_validate_cfg(lib):

@@ -33,6 +33,23 @@ def test_golden_step_by_step(name):
 
 
 @pytest.mark.parametrize("name", case_names())
+def test_golden_update_events(name):
+    """orx_step_events: every tick's update events (type, entity, args, order)
+    equal the GameStateUpdate list the reference returned."""
+    import torch
+    fx = Fixture(name)
+    eng = _engine(fx.cfg, fx.G, fx.seed, fx.game_offset)
+    acts = torch.from_numpy(fx.actions).to(eng.device)
+    for t in range(fx.T):
+        _, ev, n = eng.step(acts[t].contiguous(), events=True)
+        ev, n = ev.cpu().numpy(), n.cpu().numpy()
+        for g in range(fx.G):
+            got = [tuple(int(v) for v in r) for r in ev[g, : n[g]]]
+            assert got == fx.events(t, g), (name, t, g, got, fx.events(t, g))
+    compare_state(eng.snapshot(), fx.state(fx.T), fx.K, f"{name} final")
+
+
+@pytest.mark.parametrize("name", case_names())
 def test_golden_step_given_actions(name):
     """step kernel driven by the fixture's recorded actions (uploaded once)."""
     import torch
