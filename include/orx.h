@@ -217,6 +217,15 @@ int orx_rollout(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p1,
                 int64_t n_games, uint64_t seed, int64_t game_offset,
                 void* stream);
 
+/* Staircase (sx[j], sy[j]) of dungeon `depths[j]`, generation `gens[j]`, of
+ * episode `episodes[j]` of global game `game_ids[j]`: the keyed
+ * EmptyDungeonGenerator.spawn_dungeon (worldgen.py:33-43).  Used to
+ * materialize World.dungeons (world.py:101-135) for depths no player stands
+ * on; device arrays of length n. */
+int orx_dungeon_stairs(const orx_cfg_t* cfg, const uint32_t* game_ids, const int32_t* episodes,
+                       const int32_t* depths, const int32_t* gens, int32_t* sx, int32_t* sy,
+                       int64_t n, uint64_t seed, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

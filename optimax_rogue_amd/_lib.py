@@ -32,7 +32,7 @@ class OrxError(RuntimeError):
 _lib = None
 
 EXPORTS = ("orx_abi_version", "orx_last_error", "orx_validate_cfg", "orx_reset", "orx_step",
-           "orx_step_events", "orx_policy", "orx_rollout")
+           "orx_step_events", "orx_policy", "orx_rollout", "orx_dungeon_stairs")
 
 
 def load() -> ctypes.CDLL:
@@ -64,6 +64,8 @@ def load() -> ctypes.CDLL:
     L.orx_policy.argtypes = [P(OrxCfg), P(OrxState), i32, i32, vp, i64, u64, i64, vp]
     L.orx_rollout.restype = ctypes.c_int
     L.orx_rollout.argtypes = [P(OrxCfg), P(OrxState), i32, i32, i32, vp, vp, i64, u64, i64, vp]
+    L.orx_dungeon_stairs.restype = ctypes.c_int
+    L.orx_dungeon_stairs.argtypes = [P(OrxCfg), vp, vp, vp, vp, vp, vp, i64, u64, vp]
     v = L.orx_abi_version()
     if v != ABI_VERSION:
         raise RuntimeError(f"liborx.so ABI {v} != expected {ABI_VERSION}")

@@ -22,11 +22,38 @@ is the on-device policy kernels (Policy.Random / Policy.Staircase).
 """
 from __future__ import annotations
 
+import json
+import struct
 from typing import Dict, List, Optional, Sequence
 
 import numpy as np
 
-from .enums import Move, Tile, UpdateResult
+from .enums import DungeonDespawningStrategy, Move, StartMode, Tile, UpdateResult
+
+# serializer registry names (serializer.py:91-95: module + '.' + underscore(class))
+GAME_STATE_IDEN = "optimax_rogue.game.state.game_state"
+ENTITY_IDEN = "optimax_rogue.game.entities.entity"
+
+
+def ascii85(data: bytes) -> bytes:
+    """The reference's a85 flavour (a85encode.py:6-28): zero-pad to a multiple
+    of 4 bytes, every 4-byte big-endian group -> 5 base-85 digits + 33, no 'z'
+    shortcut, nothing truncated."""
+    if len(data) % 4:
+        data = data + b"\0" * (4 - len(data) % 4)
+    out = bytearray()
+    for (v,) in struct.iter_unpack(">I", data):
+        digits = []
+        for _ in range(5):
+            v, r = divmod(v, 85)
+            digits.append(33 + r)
+        out.extend(reversed(digits))
+    return bytes(out)
+
+
+def _json(obj) -> bytes:
+    # JsonSerializer.serialize (serializer.py:46-52): sorted keys, default separators
+    return json.dumps(obj, sort_keys=True).encode("ascii")
 
 
 class _Attrible:
@@ -48,6 +75,23 @@ class EntityView:
 
     def on_tick(self, game_state) -> None:  # attribles are constant (no Modifier exists)
         pass
+
+    def to_prims(self) -> dict:
+        """Entity.to_prims (entities.py:76-88); no modifiers or items exist."""
+        return {"iden": self.iden, "x": self.x, "y": self.y, "depth": self.depth,
+                "health": self.health, "base_max_health": self.base_max_health,
+                "base_damage": self.base_damage, "base_armor": self.base_armor,
+                "modifiers": [], "items": {}}
+
+    def serialize(self) -> bytes:
+        """serializer.serialize(entity) (serializer.py:150-156)."""
+        return _json({"iden": ENTITY_IDEN, "prims": self.to_prims()})
+
+    def __eq__(self, other):  # Entity.__eq__ (entities.py:97-128)
+        return isinstance(other, EntityView) and all(
+            getattr(self, f) == getattr(other, f) for f in (
+                "iden", "depth", "x", "y", "health", "base_max_health", "base_damage",
+                "base_armor"))
 
     def __repr__(self):
         return f"[Entity @ ({self.x}, {self.y})]"
@@ -83,6 +127,14 @@ class DungeonView:
         resx, resy = tuple(np.argwhere(self.tiles == Tile.StaircaseDown)[0])
         return int(resx), int(resy)
 
+    def to_prims(self) -> bytes:
+        """Dungeon.to_prims (world.py:73-81): W, H big-endian u32, uint8 tiles x-major."""
+        return (struct.pack(">II", self.width, self.height) +
+                self.tiles.astype(np.uint8).reshape(-1).tobytes())
+
+    def __eq__(self, other):
+        return isinstance(other, DungeonView) and np.array_equal(self.tiles, other.tiles)
+
 
 class WorldView:
     def __init__(self, dungeons: Dict[int, DungeonView]):
@@ -93,6 +145,21 @@ class WorldView:
 
     def shallow_copy_with_layers(self, *layers) -> "WorldView":
         return WorldView({lyr: self.dungeons[lyr] for lyr in layers})
+
+    def to_prims(self) -> bytes:
+        """World.to_prims (world.py:142-151): count, then per dungeon (dict order)
+        depth u32, length u64, Dungeon.to_prims."""
+        out = [struct.pack(">I", len(self.dungeons))]
+        for depth, dung in self.dungeons.items():
+            d = dung.to_prims()
+            out.append(struct.pack(">IQ", depth, len(d)))
+            out.append(d)
+        return b"".join(out)
+
+    def __eq__(self, other):  # World.__eq__ (world.py:167-175): dict order ignored
+        return (isinstance(other, WorldView) and len(self.dungeons) == len(other.dungeons)
+                and all(d in other.dungeons and dg == other.dungeons[d]
+                        for d, dg in self.dungeons.items()))
 
 
 class GameStateView:
@@ -128,19 +195,75 @@ class GameStateView:
         return GameStateView(False, self.tick, self.world, self.entities, self.player_1_iden,
                              self.player_2_iden)
 
+    def to_prims(self) -> bytes:
+        """GameState.to_prims (state.py:94-112): auth byte, tick / player idens
+        (big-endian u32), World (u64 length + bytes), entity count u32, then per
+        entity u32 length + serializer.serialize(entity)."""
+        w = self.world.to_prims()
+        out = [struct.pack(">BIII", 1 if self.is_authoritative else 0, self.tick,
+                           self.player_1_iden, self.player_2_iden),
+               struct.pack(">Q", len(w)), w, struct.pack(">I", len(self.entities))]
+        for e in self.entities:
+            b = e.serialize()
+            out.append(struct.pack(">I", len(b)))
+            out.append(b)
+        return b"".join(out)
 
-def game_state(snap: dict, i: int, cfg) -> GameStateView:
-    """Game ``i`` of a BatchedEngine.snapshot() in the reference schema."""
+    def serialize(self) -> bytes:
+        """serializer.serialize(game_state): the JSON envelope with the a85 body
+        (serializer.py:71-78, 134-156) -- what SyncPacket carries."""
+        return _json({"iden": GAME_STATE_IDEN,
+                      "prims": ascii85(self.to_prims()).decode("ascii")})
+
+    def __eq__(self, other):  # GameState.__eq__ (state.py:134-152)
+        return (isinstance(other, GameStateView)
+                and self.is_authoritative == other.is_authoritative
+                and self.tick == other.tick and self.player_1_iden == other.player_1_iden
+                and self.player_2_iden == other.player_2_iden and self.world == other.world
+                and self.entities == other.entities)
+
+
+def world_depths(cfg, d1: int, d2: int) -> List[int]:
+    """Depths of World.dungeons for players at (d1, d2), in insertion order.
+
+    Unreachable despawn (updater.py:253-254): a depth exists iff some player
+    has stood on it (start <= depth <= current) and not both players are
+    deeper; Together starts create depths in increasing order, so that is the
+    dict order.  Unused (:255-256): exactly the players' depths.  (For
+    Separated starts the insertion order interleaves the two fronts by time;
+    the set is exact, the order listed here is increasing.)"""
+    sep = int(cfg.start_mode) == StartMode.Separated
+    s1, s2 = (int(cfg.p1_depth), int(cfg.p2_depth)) if sep else (0, 0)
+    if int(cfg.despawn) == DungeonDespawningStrategy.Unreachable:
+        lo = min(d1, d2)
+        return sorted(set(range(max(s1, lo), d1 + 1)) | set(range(max(s2, lo), d2 + 1)))
+    return [d1] if d1 == d2 else [d1, d2]
+
+
+def game_state(snap: dict, i: int, cfg, extra_stairs: Optional[Dict[int, tuple]] = None
+               ) -> GameStateView:
+    """Game ``i`` of a BatchedEngine.snapshot() in the reference schema.
+
+    The world holds the players' current dungeons; with ``extra_stairs``
+    ({depth: (sx, sy)}, from ``BatchedEngine.game_states``) it holds every
+    dungeon of World.dungeons (``world_depths``)."""
     W, H = int(cfg.width), int(cfg.height)
     ents = []
     dungeons = {}
+    cur = {}
     for p in range(2):
         d = int(snap["p_depth"][p][i])
         ents.append(EntityView(1 + p, d, snap["p_x"][p][i], snap["p_y"][p][i],
                                snap["p_health"][p][i], cfg.player_health, cfg.player_damage,
                                cfg.player_armor))
-        if d not in dungeons:
-            dungeons[d] = DungeonView(W, H, int(snap["st_x"][p][i]), int(snap["st_y"][p][i]))
+        cur.setdefault(d, (int(snap["st_x"][p][i]), int(snap["st_y"][p][i])))
+    if extra_stairs is None:
+        for d, (sx, sy) in cur.items():
+            dungeons[d] = DungeonView(W, H, sx, sy)
+    else:
+        for d in world_depths(cfg, int(snap["p_depth"][0][i]), int(snap["p_depth"][1][i])):
+            sx, sy = cur[d] if d in cur else extra_stairs[d]
+            dungeons[d] = DungeonView(W, H, sx, sy)
     K = int(cfg.n_npcs)
     if K:
         alive = int(snap["npc_alive"][i])

@@ -896,6 +896,25 @@ __global__ void __launch_bounds__(256) rollout_kernel(orx_cfg_t hc, orx_state_t 
   flush_deltas(st, B, i, dl);
 }
 
+// Staircases of arbitrary (game, episode, depth, generation) dungeons, for
+// materializing World.dungeons (compat views, wire codec).
+__global__ void __launch_bounds__(256) stairs_kernel(orx_cfg_t hc, const uint32_t* __restrict__ games,
+                                                     const int32_t* __restrict__ episodes,
+                                                     const int32_t* __restrict__ depths,
+                                                     const int32_t* __restrict__ gens,
+                                                     int32_t* __restrict__ sx,
+                                                     int32_t* __restrict__ sy, uint32_t n,
+                                                     Key key) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const Cfg c = make_cfg(hc);
+  bool err = false;
+  int32_t x, y;
+  dungeon_stair(c, key, games[i], (uint32_t)episodes[i], depths[i], (uint32_t)gens[i], x, y, err);
+  sx[i] = err ? -1 : x;
+  sy[i] = err ? -1 : y;
+}
+
 // ---------------------------------------------------------------------------
 // Host side of the C-ABI
 // ---------------------------------------------------------------------------
@@ -1105,6 +1124,20 @@ int orx_rollout(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p1, 
       break;
   }
   return launch_status("orx_rollout");
+}
+
+int orx_dungeon_stairs(const orx_cfg_t* cfg, const uint32_t* game_ids, const int32_t* episodes,
+                       const int32_t* depths, const int32_t* gens, int32_t* sx, int32_t* sy,
+                       int64_t n, uint64_t seed, void* stream) {
+  int r;
+  if ((r = check_cfg(cfg))) return r;
+  if (n < 0 || n > 0x7FFFFFFFLL - kBlock) return fail(ORX_EINVAL, "bad n");
+  if (n == 0) return ORX_OK;
+  if (!game_ids || !episodes || !depths || !gens || !sx || !sy)
+    return fail(ORX_EINVAL, "a pointer is NULL");
+  hipLaunchKernelGGL(stairs_kernel, grid_for(n), dim3(kBlock), 0, (hipStream_t)stream, *cfg,
+                     game_ids, episodes, depths, gens, sx, sy, (uint32_t)n, make_key(seed));
+  return launch_status("orx_dungeon_stairs");
 }
 
 }  // extern "C"

@@ -180,6 +180,47 @@ class BatchedEngine:
                 a = a.astype(np.int32)
             dst.copy_(torch.from_numpy(a.reshape(dst.shape)))
 
+    def dungeon_stairs(self, games, episodes, depths, gens) -> np.ndarray:
+        """Staircases of (local game, episode, depth, generation) dungeons via
+        orx_dungeon_stairs; returns int32 [n, 2]."""
+        n = len(games)
+        if n == 0:
+            return np.zeros((0, 2), np.int32)
+        t = lambda a, dt: torch.as_tensor(np.asarray(a), dtype=dt).to(self.device).contiguous()
+        g = t(np.asarray(games, np.int64) + self.game_offset, torch.int64).to(torch.int32)
+        e, d, gn = t(episodes, torch.int32), t(depths, torch.int32), t(gens, torch.int32)
+        sx = torch.empty(n, dtype=torch.int32, device=self.device)
+        sy = torch.empty_like(sx)
+        with torch.cuda.device(self.device):
+            code = self.lib.orx_dungeon_stairs(ctypes.byref(self._ccfg), _ptr(g), _ptr(e), _ptr(d),
+                                               _ptr(gn), _ptr(sx), _ptr(sy), n, self.seed,
+                                               self._stream())
+        _lib.check("orx_dungeon_stairs", code)
+        return torch.stack([sx, sy], 1).cpu().numpy()
+
+    def game_states(self, indices=None, full_world: bool = True, snap: Optional[dict] = None):
+        """Reference-schema views (compat.GameStateView) of the given games; with
+        ``full_world`` every dungeon of World.dungeons is materialized (depths
+        no player stands on are regenerated on the GPU)."""
+        from .compat import game_state, world_depths
+        snap = self.snapshot() if snap is None else snap
+        idx = range(self.B) if indices is None else indices
+        extra = {}
+        if full_world:
+            req = []
+            for i in idx:
+                d1, d2 = int(snap["p_depth"][0][i]), int(snap["p_depth"][1][i])
+                for d in world_depths(self.cfg, d1, d2):
+                    if d not in (d1, d2):
+                        req.append((i, d))
+            st = self.dungeon_stairs([r[0] for r in req],
+                                     [int(snap["episode"][r[0]]) for r in req],
+                                     [r[1] for r in req], [0] * len(req))
+            for (i, d), (x, y) in zip(req, st):
+                extra.setdefault(i, {})[d] = (int(x), int(y))
+        return [game_state(snap, i, self.cfg, extra.get(i, {}) if full_world else None)
+                for i in idx]
+
     def episode_returns(self) -> torch.Tensor:
         """(ret_sum, ep_count) stacked as int32 [2, n_games] (device)."""
         return torch.stack([self.ret_sum, self.ep_count])

@@ -402,7 +402,20 @@ def run_case(R, name, spec):
             ent_len[t, g] = len(r["entities"])
             ents.extend(r["entities"])
 
+    import optimax_rogue.networking.serializer as ser
+    ser_ticks = sorted(set([0, T // 4, T // 2, (3 * T) // 4, T]))
+    ser_blobs, ser_len = [], np.zeros((len(ser_ticks), G), np.int32)
+
+    def record_ser(t):
+        if t in ser_ticks:
+            j = ser_ticks.index(t)
+            for g, h in enumerate(hs):
+                b = ser.serialize(h.gs)
+                ser_len[j, g] = len(b)
+                ser_blobs.append(b)
+
     record(0)
+    record_ser(0)
     for t in range(T):
         for g, h in enumerate(hs):
             a = h.policy()
@@ -411,13 +424,16 @@ def run_case(R, name, spec):
             ev_len[t, g] = len(evs)
             events.extend(evs)
         record(t + 1)
+        record_ser(t + 1)
 
     out = {"cfg_json": np.frombuffer(json.dumps(cfg).encode(), np.uint8),
            "seed": np.array([seed], np.uint64), "game_offset": np.array([off], np.int64),
            "actions": actions, "world_len": world_len,
            "world": np.array(world, np.int32).reshape(-1, 3),
            "event_len": ev_len, "events": np.array(events, np.int32).reshape(-1, 4),
-           "entity_len": ent_len, "entities": np.array(ents, np.int32).reshape(-1, 5)}
+           "entity_len": ent_len, "entities": np.array(ents, np.int32).reshape(-1, 5),
+           "ser_ticks": np.array(ser_ticks, np.int32), "ser_len": ser_len,
+           "ser_bytes": np.frombuffer(b"".join(ser_blobs), np.uint8)}
     for k in SNAP_KEYS_I32:
         a = np.array(snaps[k])
         if a.ndim == 3:  # [T+1, G, F] -> [T+1, F, G] (engine SoA layout)

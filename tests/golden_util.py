@@ -41,6 +41,14 @@ class Fixture:
         nl = self.z["entity_len"]
         self._ent_off = np.concatenate([[0], np.cumsum(nl.ravel())])
 
+    def serialized(self, t: int, g: int) -> bytes:
+        """serializer.serialize(GameState) of game g after t steps (t must be in
+        ser_ticks)."""
+        j = list(self.z["ser_ticks"]).index(t)
+        lens = self.z["ser_len"]
+        start = int(lens[:j].sum() + lens[j, :g].sum())
+        return bytes(self.z["ser_bytes"][start:start + int(lens[j, g])])
+
     def state(self, t: int) -> dict:
         """Engine-layout state after t steps (t = 0: after the initial reset)."""
         return {k: self.z[k][t] for k in STATE_KEYS}

@@ -37,7 +37,8 @@ def lib():
 def test_library_exports_every_declared_symbol(lib):
     decl = declared_functions()
     assert decl == sorted(["orx_abi_version", "orx_last_error", "orx_validate_cfg", "orx_reset",
-                           "orx_step", "orx_step_events", "orx_policy", "orx_rollout"])
+                           "orx_step", "orx_step_events", "orx_policy", "orx_rollout",
+                           "orx_dungeon_stairs"])
     from optimax_rogue_amd import _lib
     assert sorted(_lib.EXPORTS) == decl
     for name in decl:

@@ -80,3 +80,52 @@ def test_reference_randombot_on_views(oracle_lib):
     for i in range(4):
         gs = game_state(snap, i, cfg)
         assert Move(int(bot.move(gs.view_for(gs.iden_lookup[1])))) in list(Move)
+
+
+def oracle_view(o, g, cfg):
+    """GameStateView from the oracle's own world dict (exact insertion order)
+    and entity list."""
+    from optimax_rogue_amd.compat import DungeonView, EntityView, GameStateView, WorldView
+    dungeons = {d: DungeonView(cfg.width, cfg.height, sx, sy) for d, sx, sy in o.world(g)}
+    ents = []
+    for iden, depth, x, y, hp, dmg, arm in o.entities(g):
+        base = cfg.player_health if iden <= 2 else cfg.npc_health
+        ents.append(EntityView(iden, depth, x, y, hp, base, dmg, arm))
+    return GameStateView(True, int(o.export()["tick"][g]), WorldView(dungeons), ents)
+
+
+@pytest.mark.parametrize("name", __import__("golden_util").case_names())
+def test_wire_codec_matches_reference_bytes(oracle_lib, name):
+    """GameState -> serializer.serialize bytes (JSON envelope, a85 body, world
+    and entity encodings) equal the reference's bytes at the sampled ticks."""
+    from golden_util import Fixture
+    fx = Fixture(name)
+    cfg = EnvConfig.from_dict(fx.cfg)
+    o = oracle_lib.Oracle(fx.cfg, fx.G, fx.seed, fx.game_offset)
+    o.reset(episode=np.zeros(fx.G, np.int32))
+    ticks = set(int(t) for t in fx.z["ser_ticks"])
+    for t in range(fx.T + 1):
+        if t in ticks:
+            for g in range(fx.G):
+                assert oracle_view(o, g, cfg).serialize() == fx.serialized(t, g), (name, t, g)
+        if t < fx.T:
+            o.step(o.policy(*fx.policy))
+
+
+def test_world_depths_rule(oracle_lib):
+    """compat.world_depths (the derived World.dungeons set) equals the oracle's
+    explicit dict for every fixture tick (order too, for Together starts)."""
+    from golden_util import Fixture, case_names
+    from optimax_rogue_amd.compat import world_depths
+    for name in case_names():
+        fx = Fixture(name)
+        cfg = EnvConfig.from_dict(fx.cfg)
+        for t in range(0, fx.T + 1, 7):
+            s = fx.state(t)
+            for g in range(fx.G):
+                want = [w[0] for w in fx.world(t, g)]
+                got = world_depths(cfg, int(s["p_depth"][0][g]), int(s["p_depth"][1][g]))
+                if cfg.start_mode == 1 and cfg.despawn == 1:
+                    assert got == want, (name, t, g)
+                else:
+                    assert sorted(got) == sorted(want), (name, t, g)

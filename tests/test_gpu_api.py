@@ -69,3 +69,36 @@ def test_bot_driver(oracle_lib):
         for k in ("p_x", "p_y", "p_depth", "tick", "status"):
             assert np.array_equal(s1[k], s2[k]), (t, k)
     assert all(b.finished_with in (2, 3, 4) for b in bots[0])   # every game ended
+
+
+@pytest.mark.parametrize("name", __import__("golden_util").case_names())
+def test_engine_game_states_codec(name, oracle_lib):
+    """Engine state -> full reference-schema GameState (World.dungeons
+    regenerated on the GPU) -> serializer bytes equal to the reference's for
+    Together/Unreachable games; GameState.__eq__-equal (dict order ignored)
+    for the others."""
+    import torch
+    from golden_util import Fixture
+    from optimax_rogue_amd import EnvConfig
+    from optimax_rogue_amd.engine import BatchedEngine
+    from test_compat import oracle_view
+    fx = Fixture(name)
+    cfg = EnvConfig.from_dict(fx.cfg)
+    eng = BatchedEngine(cfg, fx.G, seed=fx.seed, game_offset=fx.game_offset,
+                        device=torch.device("cuda", 0))
+    o = oracle_lib.Oracle(fx.cfg, fx.G, fx.seed, fx.game_offset)
+    o.reset(episode=np.zeros(fx.G, np.int32))
+    exact = cfg.start_mode == 1 and cfg.despawn == 1
+    ticks = set(int(t) for t in fx.z["ser_ticks"])
+    acts = torch.from_numpy(fx.actions).to(eng.device)
+    for t in range(fx.T + 1):
+        if t in ticks:
+            views = eng.game_states()
+            for g in range(fx.G):
+                if exact:
+                    assert views[g].serialize() == fx.serialized(t, g), (name, t, g)
+                else:
+                    assert views[g] == oracle_view(o, g, cfg), (name, t, g)
+        if t < fx.T:
+            eng.step(acts[t].contiguous())
+            o.step(fx.actions[t])
