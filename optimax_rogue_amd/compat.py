@@ -143,6 +143,12 @@ class WorldView:
     def get_at_depth(self, ind: int) -> DungeonView:
         return self.dungeons[ind]
 
+    def set_at_depth(self, ind: int, dung: DungeonView) -> None:
+        self.dungeons[ind] = dung
+
+    def del_at_depth(self, ind: int) -> None:
+        del self.dungeons[ind]
+
     def shallow_copy_with_layers(self, *layers) -> "WorldView":
         return WorldView({lyr: self.dungeons[lyr] for lyr in layers})
 
@@ -183,6 +189,22 @@ class GameStateView:
 
     def on_tick(self) -> None:
         pass
+
+    # GameState mutators (state.py:64-88), used by update.apply()
+    def move_entity(self, entity, newdepth, newx, newy):
+        del self.pos_lookup[(entity.depth, entity.x, entity.y)]
+        entity.depth, entity.x, entity.y = int(newdepth), int(newx), int(newy)
+        self.pos_lookup[(entity.depth, entity.x, entity.y)] = entity
+
+    def add_entity(self, entity):
+        self.entities.append(entity)
+        self.pos_lookup[(entity.depth, entity.x, entity.y)] = entity
+        self.iden_lookup[entity.iden] = entity
+
+    def remove_entity(self, entity):
+        del self.pos_lookup[(entity.depth, entity.x, entity.y)]
+        del self.iden_lookup[entity.iden]
+        self.entities.remove(entity)
 
     def view_for(self, entity: EntityView, reduce_tick: bool = False) -> "GameStateView":
         """GameState.view_for (state.py:53-58): the entity's depth only."""

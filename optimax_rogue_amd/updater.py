@@ -86,4 +86,65 @@ class BatchedUpdater:
         return game_state(self.engine.snapshot(), i, self.engine.cfg)
 
 
-__all__ = ["BatchedUpdater", "Move"]
+class GameUpdater:
+    """Per-game ``Updater`` front end: ``update(game_state, m1, m2) ->
+    (UpdateResult, [GameStateUpdate])`` with the reference's contract
+    (updater.py:76-162): it mutates ``game_state`` in place and returns the
+    update list a server broadcasts.  Backed by a one-game BatchedEngine
+    (global game id ``game_id``); ``game_state`` must be the object returned by
+    ``setup_game()`` (a compat.GameStateView, replicated by applying the
+    updates exactly as a client would).  One kernel launch per call: the
+    compatibility path, not the throughput path."""
+
+    def __init__(self, dgen, despawn_strat: DungeonDespawningStrategy,
+                 max_ticks: Optional[int] = None, *, seed: int = 0, game_id: int = 0,
+                 game_start="together", n_npcs: int = 0, device: Optional[torch.device] = None):
+        self._b = BatchedUpdater(dgen, despawn_strat, max_ticks, n_games=1, seed=seed,
+                                 game_offset=game_id, game_start=game_start, n_npcs=n_npcs,
+                                 device=device, autoreset=False)
+        self.engine = self._b.engine
+        self.current_update_order = 0
+        self.max_ticks = max_ticks
+        self.despawn_strat = self._b.despawn_strat
+
+    def setup_game(self):
+        """GameStartGenerator.setup_game: the engine's game as a full GameState view."""
+        self.engine.reset()
+        return self.engine.game_states([0])[0]
+
+    def update(self, game_state, player1_move, player2_move):
+        from .compat import DungeonView
+        from .updates import from_events
+        eng = self.engine
+        Move(int(player1_move)), Move(int(player2_move))  # ValueError like Move(...) would
+        pre = {e.iden: e.depth for e in game_state.entities}
+        eng.actions[0, 0] = int(player1_move)
+        eng.actions[0, 1] = int(player2_move)
+        status, ev, n = eng.step(events=True)
+        rows = [tuple(int(v) for v in r) for r in ev[0, : int(n[0])].cpu().numpy()]
+        snap = eng.snapshot()
+        cfg = eng.cfg
+
+        def dungeon_for(depth):
+            for p in range(2):
+                if int(snap["p_depth"][p][0]) == depth:
+                    return DungeonView(cfg.width, cfg.height, int(snap["st_x"][p][0]),
+                                       int(snap["st_y"][p][0]))
+            raise KeyError(depth)
+
+        ups = from_events(rows, self.current_update_order,
+                          cfg.player_damage - cfg.player_armor, pre, dungeon_for)
+        self.current_update_order += len(ups)
+        for u in ups:
+            u.apply(game_state)
+        # despawn (updater.py:295-296) and tick (:148) replicate the server side
+        from .compat import world_depths
+        keep = set(world_depths(cfg, int(snap["p_depth"][0][0]), int(snap["p_depth"][1][0])))
+        for d in [d for d in game_state.world.dungeons if d not in keep]:
+            game_state.world.del_at_depth(d)
+        game_state.tick = int(snap["tick"][0])
+        from .enums import UpdateResult
+        return UpdateResult(int(status[0].item())), ups
+
+
+__all__ = ["BatchedUpdater", "GameUpdater", "Move"]

@@ -102,3 +102,50 @@ def test_engine_game_states_codec(name, oracle_lib):
         if t < fx.T:
             eng.step(acts[t].contiguous())
             o.step(fx.actions[t])
+
+
+def _as_record(u):
+    from optimax_rogue_amd import updates as U
+    if isinstance(u, U.EntityCombatUpdate):
+        (flag,) = tuple(u.tags)
+        return (1, u.attacker_iden, u.defender_iden, int(flag))
+    if isinstance(u, U.EntityDeathUpdate):
+        return (2, u.entity_iden, 0, 0)
+    if isinstance(u, U.EntityPositionUpdate):
+        return (3, u.entity_iden, u.depth, (u.posx & 0xFFFF) | (u.posy << 16))
+    return (4, 0, u.depth, 0)
+
+
+@pytest.mark.parametrize("name,g", [("small_npc_random", 0), ("small_npc_random", 5),
+                                    ("stairs_unreachable", 2), ("duel_5", 1),
+                                    ("separated_unused", 3)])
+def test_game_updater_drop_in(name, g):
+    """GameUpdater.update(gs, m1, m2) -> (UpdateResult, updates) over one
+    fixture game: the returned updates equal the reference's, applying them
+    keeps the caller's GameState equal to the engine's, and the results match."""
+    import torch
+    from golden_util import Fixture
+    from optimax_rogue_amd import DungeonDespawningStrategy, UpdateResult
+    from optimax_rogue_amd.updater import GameUpdater
+    fx = Fixture(name)
+    c = fx.cfg
+    start = "together" if c["start_mode"] == 1 else ("separated", c["p1_depth"], c["p2_depth"])
+    upd = GameUpdater((c["width"], c["height"]), DungeonDespawningStrategy(c["despawn"]),
+                      c["max_ticks"] or None, seed=fx.seed, game_id=fx.game_offset + g,
+                      game_start=start, n_npcs=c["n_npcs"], device=torch.device("cuda", 0))
+    gs = upd.setup_game()
+    s0 = fx.state(0)
+    assert (gs.player_1.x, gs.player_1.y) == (s0["p_x"][0][g], s0["p_y"][0][g])
+    order = 0
+    for t in range(fx.T):
+        if fx.state(t)["status"][g] != 1:
+            break   # the reference game is over (the fixture autoresets; GameUpdater does not)
+        res, ups = upd.update(gs, fx.actions[t, g, 0], fx.actions[t, g, 1])
+        assert [_as_record(u) for u in ups] == fx.events(t, g), (name, t)
+        assert [u.order for u in ups] == list(range(order, order + len(ups)))
+        order += len(ups)
+        assert int(res) == fx.state(t + 1)["status"][g]
+        assert gs == upd.engine.game_states([0])[0], (name, t)
+        ents = [(e.iden, e.depth, e.x, e.y, e.health) for e in gs.entities]
+        assert ents == fx.entities(t + 1, g), (name, t)
+        assert sorted(gs.world.dungeons) == sorted(w[0] for w in fx.world(t + 1, g))
