@@ -45,6 +45,7 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "../../include/orx.h"
@@ -56,6 +57,7 @@ namespace {
 // ---------------------------------------------------------------------------
 enum : uint32_t { PUR_INIT = 1, PUR_DUNGEON = 2, PUR_SHUFFLE = 3, PUR_SPAWN = 4, PUR_POLICY = 5 };
 constexpr uint32_t kWordCap = 4096;  // per stream; exceeding it stops the game
+constexpr int32_t kStartTick = 1;     // GameState.tick of a fresh game (worldgen.py:87,133)
 constexpr uint32_t kDeadSlot = 0xFFFFu;
 
 struct Key {
@@ -72,8 +74,9 @@ __device__ __forceinline__ W4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint
   for (int r = 0; r < 10; ++r) {
     const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
     const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
-    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
-    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+    // three-input xor in one v_bitop3_b32 (the compiler emits two v_xor here)
+    const uint32_t n0 = __builtin_amdgcn_bitop3_b32((uint32_t)(p1 >> 32), c1, k0, 0x96);
+    const uint32_t n2 = __builtin_amdgcn_bitop3_b32((uint32_t)(p0 >> 32), c3, k1, 0x96);
     c1 = (uint32_t)p1;
     c3 = (uint32_t)p0;
     c0 = n0;
@@ -345,7 +348,7 @@ __device__ __forceinline__ void setup_game(const Cfg& c, Key key, uint32_t game,
   if (placed < total) err = true;
   p1.hp = c.player_hp;
   p2.hp = c.player_hp;
-  tick = 1;
+  tick = kStartTick;
   status = err ? ORX_STATUS_RNG_EXHAUSTED : ORX_IN_PROGRESS;
 }
 
@@ -470,23 +473,22 @@ __device__ __forceinline__ uint32_t policy_packed(Key key, uint32_t game, uint32
                     tick_block(key, game, ep, tick, PUR_POLICY, 1), 29, 3);
 }
 
-__device__ __forceinline__ bool p1_first_draw(Key key, uint32_t game, uint32_t ep, int32_t tick,
-                                              bool& err) {
-  const uint32_t pk = pack_words(tick_block(key, game, ep, tick, PUR_SHUFFLE, 0),
-                                 tick_block(key, game, ep, tick, PUR_SHUFFLE, 1), 30, 2);
-  return first_from_packed(pk, key, game, ep, tick, err);
+__device__ __forceinline__ uint32_t shuffle_packed(Key key, uint32_t game, uint32_t ep,
+                                                   int32_t tick) {
+  return pack_words(tick_block(key, game, ep, tick, PUR_SHUFFLE, 0),
+                    tick_block(key, game, ep, tick, PUR_SHUFFLE, 1), 30, 2);
 }
 
-// RandomBot / StaircaseBot moves for both players (policy codes ORX_POLICY_*).
-// pk_pol: policy_packed() of this tick (ignored when no player is random).
-__device__ __forceinline__ void policy_pair(Key key, uint32_t game, uint32_t ep, int32_t tick,
-                                            int32_t pol1, int32_t pol2, uint32_t pk_pol,
-                                            const Player& p1, const Player& p2, int32_t& a1,
-                                            int32_t& a2) {
-  const int need = (pol1 == ORX_POLICY_RANDOM) + (pol2 == ORX_POLICY_RANDOM);
-  int32_t r0 = ORX_MOVE_STAY, r1 = ORX_MOVE_STAY;
-  bool err = false;
-  if (need) moves_from_packed(pk_pol, need, key, game, ep, tick, r0, r1, err);
+__device__ __forceinline__ bool p1_first_draw(Key key, uint32_t game, uint32_t ep, int32_t tick,
+                                              bool& err) {
+  return first_from_packed(shuffle_packed(key, game, ep, tick), key, game, ep, tick, err);
+}
+
+// RandomBot / StaircaseBot moves for both players (policy codes ORX_POLICY_*)
+// given the RandomBot draws r0 (first random player), r1 (second).
+__device__ __forceinline__ void assign_moves(int32_t pol1, int32_t pol2, int32_t r0, int32_t r1,
+                                             const Player& p1, const Player& p2, int32_t& a1,
+                                             int32_t& a2) {
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
     const int32_t pol = p == 0 ? pol1 : pol2;
@@ -504,6 +506,18 @@ __device__ __forceinline__ void policy_pair(Key key, uint32_t game, uint32_t ep,
     }
     if (p == 0) a1 = a; else a2 = a;
   }
+}
+
+// pk_pol: policy_packed() of this tick (ignored when no player is random).
+__device__ __forceinline__ void policy_pair(Key key, uint32_t game, uint32_t ep, int32_t tick,
+                                            int32_t pol1, int32_t pol2, uint32_t pk_pol,
+                                            const Player& p1, const Player& p2, int32_t& a1,
+                                            int32_t& a2) {
+  const int need = (pol1 == ORX_POLICY_RANDOM) + (pol2 == ORX_POLICY_RANDOM);
+  int32_t r0 = ORX_MOVE_STAY, r1 = ORX_MOVE_STAY;
+  bool err = false;
+  if (need) moves_from_packed(pk_pol, need, key, game, ep, tick, r0, r1, err);
+  assign_moves(pol1, pol2, r0, r1, p1, p2, a1, a2);
 }
 
 // ---------------------------------------------------------------------------
@@ -838,12 +852,54 @@ __global__ void __launch_bounds__(256) policy_kernel(orx_state_t st, int32_t pol
 // (Splitting a game's two random streams over two lanes -- two waves per SIMD
 // at 65,536 games -- was measured 22% slower: the replicated game logic costs
 // more than the halved Philox saves.)
-template <int NCAP>
-__global__ void __launch_bounds__(256) rollout_kernel(orx_cfg_t hc, orx_state_t st, int32_t pol1,
-                                                      int32_t pol2, int32_t n_ticks,
+
+// One tick's trajectory rows: obs[t][f][i] (ORX_OBS_* fields) and act[t][i].
+// FAST (both present): buffer stores -- one resource per tick row block, the
+// field stride in the scalar offset, so the lane's address is one VGPR
+// computed once; otherwise per-pointer checks and flat stores.
+constexpr int32_t kBufferDword3 = 0x00020000;  // gfx9 raw buffer, 32-bit elements
+template <bool FAST>
+__device__ __forceinline__ void store_traj(int32_t* obs, int8_t* act, int32_t t, uint32_t B,
+                                           uint32_t i, const Player& p1, const Player& p2,
+                                           int32_t tick, int32_t status, int32_t a1, int32_t a2) {
+  const int32_t vals[ORX_OBS_FIELDS] = {p1.x, p1.y, p1.d, p1.hp, p2.x, p2.y, p2.d, p2.hp,
+                                        tick, status, p1.sx, p1.sy, p2.sx, p2.sy};
+  if constexpr (FAST) {
+    const auto ro = __builtin_amdgcn_make_buffer_rsrc(obs + (size_t)t * ORX_OBS_FIELDS * B, 0,
+                                                      (int32_t)(ORX_OBS_FIELDS * B * 4u),
+                                                      kBufferDword3);
+    // running scalar offset: left to itself the compiler hoists the 14 field
+    // offsets out of the tick loop into SGPRs and spills them
+    int32_t so = 0;
+    const int32_t b4 = (int32_t)(B * 4u);
+#pragma unroll
+    for (int f = 0; f < ORX_OBS_FIELDS; ++f) {
+      __builtin_amdgcn_raw_buffer_store_b32(vals[f], ro, (int32_t)(i * 4u), so, 0);
+      asm volatile("s_add_u32 %0, %0, %1" : "+s"(so) : "s"(b4));
+    }
+    const auto ra = __builtin_amdgcn_make_buffer_rsrc(act + (size_t)t * 2 * B, 0, (int32_t)(B * 2u),
+                                                      kBufferDword3);
+    __builtin_amdgcn_raw_buffer_store_b16(pack_actions(a1, a2), ra, (int32_t)(i * 2u), 0, 0);
+  } else {
+    if (obs) {
+      int32_t* o = obs + (size_t)t * ORX_OBS_FIELDS * B;  // uniform row base + lane index
+#pragma unroll
+      for (int f = 0; f < ORX_OBS_FIELDS; ++f) (o + (size_t)f * B)[i] = vals[f];
+    }
+    if (act) reinterpret_cast<uint16_t*>(act)[(size_t)t * B + i] = pack_actions(a1, a2);
+  }
+}
+
+// FAST: both players are RandomBots and obs/act are both given (compile-time,
+// the common case: no per-tick uniform branches on policy codes or pointers).
+template <int NCAP, bool FAST>
+__global__ void __launch_bounds__(256) rollout_kernel(orx_cfg_t hc, orx_state_t st, int32_t pol1_,
+                                                      int32_t pol2_, int32_t n_ticks,
                                                       int32_t* __restrict__ obs,
                                                       int8_t* __restrict__ act, uint32_t B,
                                                       Key key, uint32_t off) {
+  const int32_t pol1 = FAST ? (int32_t)ORX_POLICY_RANDOM : pol1_;
+  const int32_t pol2 = FAST ? (int32_t)ORX_POLICY_RANDOM : pol2_;
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= B) return;
   const Cfg c = make_cfg(hc);
@@ -859,17 +915,204 @@ __global__ void __launch_bounds__(256) rollout_kernel(orx_cfg_t hc, orx_state_t 
   Deltas dl = {0, 0, 0, 0, 0, 0};
   bool stairs_dirty = false, npc_dirty = false;
   const bool any_random = pol1 == ORX_POLICY_RANDOM || pol2 == ORX_POLICY_RANDOM;
+#ifndef ORX_DIAG
+#define ORX_DIAG 0  // diagnostic builds only (results wrong): 1 no policy RNG, 2 no
+#endif              // initiative RNG, 4 no move logic, 8 no reset, 16 no trajectory
   for (int32_t t = 0; t < n_ticks; ++t) {
-    const uint32_t pk_pol = any_random ? policy_packed(key, game, ep, tick) : 0u;
+    const uint32_t pk_pol = (ORX_DIAG & 1) ? ((uint32_t)tick * 0x9E3779B9u) ^ (game * 0x85EBCA6Bu)
+                            : any_random ? policy_packed(key, game, ep, tick) : 0u;
+    // initiative words drawn beside the policy words (one basic block: the
+    // four Philox chains interleave) although only in-progress games use them
+    const uint32_t pk_shf = (ORX_DIAG & 2) ? 0u : shuffle_packed(key, game, ep, tick);
     int32_t a1 = ORX_MOVE_STAY, a2 = ORX_MOVE_STAY;
     policy_pair(key, game, ep, tick, pol1, pol2, pk_pol, p1, p2, a1, a2);
     if (status == ORX_IN_PROGRESS) {
       p1.move = a1; p2.move = a2;
       const int32_t descents = dl.descend;
       bool err = false;
-      const bool p1_first = p1_first_draw(key, game, ep, tick, err);
+      const bool p1_first = (ORX_DIAG & 2) ? (((uint32_t)tick ^ game) & 1u) != 0
+                                           : first_from_packed(pk_shf, key, game, ep, tick, err);
       Events<false> ev{nullptr, 0};
-      tick_game(c, key, game, ep, p1_first, true, p1, p2, npc, m, tick, status, err, dl, ev);
+      if (ORX_DIAG & 4) {
+        tick += 1;
+        p1.x ^= p1_first;
+        status = (c.max_ticks && tick >= c.max_ticks) ? ORX_TIE : ORX_IN_PROGRESS;
+      } else {
+        tick_game(c, key, game, ep, p1_first, true, p1, p2, npc, m, tick, status, err, dl, ev);
+      }
+      stairs_dirty |= dl.descend != descents;
+    } else if (c.autoreset) {
+      ep += 1;
+      if (ORX_DIAG & 8) {
+        tick = kStartTick;
+        status = ORX_IN_PROGRESS;
+      } else {
+        setup_game(c, key, game, ep, p1, p2, npc, tick, status);
+        if constexpr (NCAP > 0) store_new_npcs(st, c, B, i, npc);
+      }
+      stairs_dirty = true;
+      npc_dirty = true;
+    }
+    if (!(ORX_DIAG & 16)) store_traj<FAST>(obs, act, t, B, i, p1, p2, tick, status, a1, a2);
+  }
+  store_players(st, B, i, p1, p2, stairs_dirty);
+  st.tick[i] = tick;
+  st.status[i] = status;
+  st.episode[i] = (int32_t)ep;
+  if (NCAP > 0 && (npc_dirty || dl.npc_death)) st.npc_alive[i] = npc.alive;
+  flush_deltas(st, B, i, dl);
+}
+
+// Producer/consumer form of rollout_kernel for batches that put at most a few
+// waves on a SIMD (the headline 65,536 games = one wave per SIMD, which
+// cannot hide its own latencies).  A 128-thread workgroup owns 64 games:
+// wave 0 draws the RandomBot moves and the initiative bits -- they depend only
+// on (game, episode, tick), never on the board -- and wave 1 resolves the
+// ticks.  (Splitting the draws over two producer waves measured slower: three
+// waves per SIMD contend for issue.)  The waves are decoupled through LDS rings of kRing ticks with one
+// progress counter per wave (no barrier in the loop): a producer runs ahead
+// on a predicted key sequence -- tick+1 while in progress, the game ends when
+// max_ticks is reached, then (episode+1, kStartTick) under autoreset -- which
+// is exact except after a player death.  Every slot carries the key it was
+// drawn for; the consumer checks it and on a mismatch draws the words itself
+// and posts its true key, from which the producers re-predict.  Results are
+// therefore identical to rollout_kernel whatever the timing.
+constexpr int kRing = 8;                 // ticks a producer may run ahead
+
+// producer word: bits 0-2 first RandomBot move, 3-5 second, 6 p1 first,
+// 7 RNG exhausted
+__device__ __forceinline__ uint32_t pc_word(Key key, uint32_t game, uint32_t ep, int32_t tick,
+                                            int need) {
+  int32_t r0 = ORX_MOVE_STAY, r1 = ORX_MOVE_STAY;
+  bool perr = false, err = false;
+  if (need)
+    moves_from_packed(policy_packed(key, game, ep, tick), need, key, game, ep, tick, r0, r1, perr);
+  const bool first = p1_first_draw(key, game, ep, tick, err);
+  return (uint32_t)r0 | ((uint32_t)r1 << 3) | (first ? 64u : 0u) | (err ? 128u : 0u);
+}
+
+struct KeyPred {   // predicted (episode, tick) at the start of an iteration
+  uint32_t ep;
+  int32_t tick;
+  bool ended;      // status != InProgress: the iteration is a reset (or frozen)
+  __device__ __forceinline__ void advance(const Cfg& c) {
+    if (!ended) {
+      tick += 1;
+      ended = c.max_ticks && tick >= c.max_ticks;
+    } else if (c.autoreset) {
+      ep += 1;
+      tick = kStartTick;
+      ended = false;
+    }
+  }
+};
+
+__device__ __forceinline__ uint32_t lds_acquire(uint32_t* p) {
+  return __builtin_amdgcn_readfirstlane(
+      __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+}
+__device__ __forceinline__ void lds_release(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+template <int NCAP, bool FAST>
+__global__ void __launch_bounds__(128) rollout_pc_kernel(
+    orx_cfg_t hc, orx_state_t st, int32_t pol1_, int32_t pol2_, int32_t n_ticks,
+    int32_t* __restrict__ obs, int8_t* __restrict__ act, uint32_t B, Key key, uint32_t off) {
+  const int32_t pol1 = FAST ? (int32_t)ORX_POLICY_RANDOM : pol1_;
+  const int32_t pol2 = FAST ? (int32_t)ORX_POLICY_RANDOM : pol2_;
+  struct Slot {
+    uint32_t word, ep;
+    int32_t tick, pad;
+  };
+  __shared__ Slot ring[kRing][64];
+  __shared__ int32_t rec_t[64];            // consumer's posted true key: iteration,
+  __shared__ uint32_t rec_ep[64];          // episode, tick, ended
+  __shared__ int32_t rec_tick[64];
+  __shared__ uint32_t rec_ended[64];
+  __shared__ uint32_t produced, consumed;  // iterations written / read
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = threadIdx.x >> 6;  // wave-uniform role
+  const uint32_t i = blockIdx.x * 64u + lane;
+  const bool valid = i < B;                 // no early return: every wave runs every iteration
+  const Cfg c = make_cfg(hc);
+  const uint32_t game = off + i;
+  const int need = (pol1 == ORX_POLICY_RANDOM) + (pol2 == ORX_POLICY_RANDOM);
+  if (wave == 0) {
+    rec_t[lane] = -1;
+    if (lane == 0) { produced = 0; consumed = 0; }
+  }
+  __syncthreads();
+
+  if (wave == 0) {
+    KeyPred pk{0, 0, false};
+    if (valid) {
+      pk.ep = (uint32_t)st.episode[i];
+      pk.tick = st.tick[i];
+      pk.ended = st.status[i] != ORX_IN_PROGRESS;
+    }
+    int32_t seen = -1;
+    for (int32_t t = 0; t < n_ticks; ++t) {
+      if (t >= kRing)  // slot t % kRing is free once iteration t - kRing was read
+        while ((int32_t)lds_acquire(&consumed) <= t - kRing) __builtin_amdgcn_s_sleep(1);
+      if (valid) {
+        const int32_t rt = __hip_atomic_load(&rec_t[lane], __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (rt != seen) {  // rare: re-predict from the consumer's posted key
+          seen = rt;
+          pk.ep = rec_ep[lane];
+          pk.tick = rec_tick[lane];
+          pk.ended = rec_ended[lane] != 0;
+          for (int32_t k = rt; k < t; ++k) pk.advance(c);
+        }
+        ring[(uint32_t)t % kRing][lane] =
+            Slot{pc_word(key, game, pk.ep, pk.tick, need), pk.ep, pk.tick, 0};
+        pk.advance(c);
+      }
+      if (lane == 0) lds_release(&produced, (uint32_t)t + 1);
+    }
+    return;
+  }
+
+  // consumer
+  Player p1, p2;
+  int32_t tick = 0, status = ORX_IN_PROGRESS;
+  uint32_t ep = 0;
+  Npcs<NCAP> npc;
+  Deltas dl = {0, 0, 0, 0, 0, 0};
+  bool stairs_dirty = false, npc_dirty = false;
+  if (valid) {
+    load_players(st, B, i, p1, p2);
+    tick = st.tick[i];
+    status = st.status[i];
+    ep = (uint32_t)st.episode[i];
+    load_npcs(st, c, B, i, npc);
+  }
+  const NpcMem m{st.npc_pos, st.npc_health, B, i};
+  int32_t avail = 0;  // iterations known to be produced by both producers
+  for (int32_t t = 0; t < n_ticks; ++t) {
+    if (t >= avail)
+      while ((avail = (int32_t)lds_acquire(&produced)) <= t) __builtin_amdgcn_s_sleep(1);
+    const Slot sl = valid ? ring[(uint32_t)t % kRing][lane] : Slot{0, 0, 0, 0};
+    if (lane == 0) lds_release(&consumed, (uint32_t)t + 1);
+    if (!valid) continue;
+    uint32_t w = sl.word;
+    if (sl.ep != ep || sl.tick != tick) {
+      // rare (after a death): draw here, post the true key
+      w = pc_word(key, game, ep, tick, need);
+      rec_ep[lane] = ep;
+      rec_tick[lane] = tick;
+      rec_ended[lane] = status != ORX_IN_PROGRESS;
+      __hip_atomic_store(&rec_t[lane], t, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    int32_t a1 = ORX_MOVE_STAY, a2 = ORX_MOVE_STAY;
+    assign_moves(pol1, pol2, (int32_t)(w & 7u), (int32_t)((w >> 3) & 7u), p1, p2, a1, a2);
+    if (status == ORX_IN_PROGRESS) {
+      p1.move = a1; p2.move = a2;
+      const int32_t descents = dl.descend;
+      bool err = (w & 128u) != 0;
+      Events<false> ev{nullptr, 0};
+      tick_game(c, key, game, ep, (w & 64u) != 0, true, p1, p2, npc, m, tick, status, err, dl, ev);
       stairs_dirty |= dl.descend != descents;
     } else if (c.autoreset) {
       ep += 1;
@@ -878,22 +1121,16 @@ __global__ void __launch_bounds__(256) rollout_kernel(orx_cfg_t hc, orx_state_t 
       stairs_dirty = true;
       npc_dirty = true;
     }
-    if (obs) {
-      // uniform row base + 32-bit lane index
-      int32_t* o = obs + (size_t)t * ORX_OBS_FIELDS * B;
-      const int32_t vals[ORX_OBS_FIELDS] = {p1.x, p1.y, p1.d, p1.hp, p2.x, p2.y, p2.d, p2.hp,
-                                            tick, status, p1.sx, p1.sy, p2.sx, p2.sy};
-#pragma unroll
-      for (int f = 0; f < ORX_OBS_FIELDS; ++f) (o + (size_t)f * B)[i] = vals[f];
-    }
-    if (act) reinterpret_cast<uint16_t*>(act)[(size_t)t * B + i] = pack_actions(a1, a2);
+    store_traj<FAST>(obs, act, t, B, i, p1, p2, tick, status, a1, a2);
   }
-  store_players(st, B, i, p1, p2, stairs_dirty);
-  st.tick[i] = tick;
-  st.status[i] = status;
-  st.episode[i] = (int32_t)ep;
-  if (NCAP > 0 && (npc_dirty || dl.npc_death)) st.npc_alive[i] = npc.alive;
-  flush_deltas(st, B, i, dl);
+  if (valid) {
+    store_players(st, B, i, p1, p2, stairs_dirty);
+    st.tick[i] = tick;
+    st.status[i] = status;
+    st.episode[i] = (int32_t)ep;
+    if (NCAP > 0 && (npc_dirty || dl.npc_death)) st.npc_alive[i] = npc.alive;
+    flush_deltas(st, B, i, dl);
+  }
 }
 
 // Staircases of arbitrary (game, episode, depth, generation) dungeons, for
@@ -984,6 +1221,20 @@ int launch_status(const char* what) {
 constexpr int kBlock = 256;
 
 inline dim3 grid_for(int64_t B) { return dim3((unsigned)((B + kBlock - 1) / kBlock)); }
+
+// rollout form: ORX_ROLLOUT=plain|pc overrides (diagnostics); by default the
+// producer/consumer kernel runs up to kPcMaxGames games (4 waves per SIMD for
+// the plain kernel), where the plain kernel cannot hide its own latencies.
+constexpr int64_t kPcMaxGames = 4 * 65536;
+inline bool use_pc_rollout(int64_t B) {
+  static const int forced = [] {
+    const char* e = getenv("ORX_ROLLOUT");
+    if (!e) return -1;
+    return strcmp(e, "pc") == 0 ? 1 : strcmp(e, "plain") == 0 ? 0 : -1;
+  }();
+  if (forced >= 0) return forced == 1;
+  return B <= kPcMaxGames;
+}
 
 inline Key make_key(uint64_t seed) { return Key{(uint32_t)seed, (uint32_t)(seed >> 32)}; }
 
@@ -1109,20 +1360,24 @@ int orx_rollout(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p1, 
   const uint32_t B = (uint32_t)n_games, off = (uint32_t)game_offset;
   const hipStream_t s = (hipStream_t)stream;
   const Key k = make_key(seed);
-  switch (ncap_for(cfg->n_npcs)) {
-    case 0:
-      hipLaunchKernelGGL(rollout_kernel<0>, grid_for(B), dim3(kBlock), 0, s, *cfg, *st, policy_p1,
-                         policy_p2, n_ticks, obs, act, B, k, off);
-      break;
-    case 8:
-      hipLaunchKernelGGL(rollout_kernel<8>, grid_for(B), dim3(kBlock), 0, s, *cfg, *st, policy_p1,
-                         policy_p2, n_ticks, obs, act, B, k, off);
-      break;
-    default:
-      hipLaunchKernelGGL(rollout_kernel<16>, grid_for(B), dim3(kBlock), 0, s, *cfg, *st,
-                         policy_p1, policy_p2, n_ticks, obs, act, B, k, off);
-      break;
+  // the buffer-addressed fast path needs one tick's obs rows below 2 GiB
+  const bool rr = policy_p1 == ORX_POLICY_RANDOM && policy_p2 == ORX_POLICY_RANDOM && obs && act &&
+                  (uint64_t)B * ORX_OBS_FIELDS * 4u < (1ull << 31);
+  const bool pc = use_pc_rollout(B);
+  const int nc = ncap_for(cfg->n_npcs);
+#define ORX_ROLLOUT(N, R)                                                                       \
+  if (nc == N && rr == R) {                                                                     \
+    if (pc)                                                                                     \
+      hipLaunchKernelGGL((rollout_pc_kernel<N, R>), dim3((B + 63) / 64),                        \
+                         dim3(128), 0, s, *cfg, *st, policy_p1, policy_p2,                       \
+                         n_ticks, obs, act, B, k, off);                                          \
+    else                                                                                        \
+      hipLaunchKernelGGL((rollout_kernel<N, R>), grid_for(B), dim3(kBlock), 0, s, *cfg, *st,    \
+                         policy_p1, policy_p2, n_ticks, obs, act, B, k, off);                   \
   }
+  ORX_ROLLOUT(0, false) ORX_ROLLOUT(0, true) ORX_ROLLOUT(8, false) ORX_ROLLOUT(8, true)
+  ORX_ROLLOUT(16, false) ORX_ROLLOUT(16, true)
+#undef ORX_ROLLOUT
   return launch_status("orx_rollout");
 }
 

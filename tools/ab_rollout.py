@@ -1,0 +1,70 @@
+"""A/B timing of liborx builds (diagnostics): for every library path given,
+a fresh child process times the C3 headline rollout (65,536 games, 50-tick
+launches with obs+act) and, with --large, 2^21 games x 20 ticks.
+
+    python tools/ab_rollout.py optimax_rogue_amd/liborx.so /tmp/liborx_b.so \
+        optimax_rogue_amd/liborx.so@ORX_ROLLOUT=plain
+
+An argument ``path@VAR=value[@...]`` runs that library with environment
+variables set; ``@OBS=0`` drops the trajectory outputs.
+"""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def child(arg, large):
+    lib, *envs = arg.split("@")
+    with_obs = True
+    for env in envs:
+        k, _, v = env.partition("=")
+        if k == "OBS":          # OBS=0: no trajectory output
+            with_obs = v != "0"
+        else:
+            os.environ[k] = v
+    sys.path.insert(0, ROOT)
+    import torch
+    from optimax_rogue_amd import _lib, EnvConfig
+    _lib.LIB_PATH = os.path.abspath(lib)
+    from optimax_rogue_amd.engine import BatchedEngine
+    from optimax_rogue_amd.enums import OBS_FIELDS
+    dev = torch.device("cuda", 0)
+    out = {"lib": arg}
+    shapes = [(65536, 50, 40)] + ([(1 << 21, 20, 6)] if large else [])
+    for B, T, reps in shapes:
+        e = BatchedEngine(EnvConfig.c3(), B, seed=1, device=dev)
+        obs = torch.empty((T, len(OBS_FIELDS), B), dtype=torch.int32, device=dev) \
+            if with_obs else None
+        act = torch.empty((T, B, 2), dtype=torch.int8, device=dev) if with_obs else None
+        for _ in range(3):
+            e.rollout(T, 1, 1, obs=obs, act=act)
+        torch.cuda.synchronize()
+        s, f = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(reps):
+            e.rollout(T, 1, 1, obs=obs, act=act)
+        f.record()
+        torch.cuda.synchronize()
+        us = s.elapsed_time(f) * 1e3 / reps
+        out[f"B{B}"] = {"us_per_launch": round(us, 2), "env_steps_per_s": B * T / us * 1e6}
+    print(json.dumps(out), flush=True)
+
+
+def main():
+    if sys.argv[1] == "--child":
+        child(sys.argv[2], "--large" in sys.argv)
+        return
+    large = "--large" in sys.argv
+    for lib in [a for a in sys.argv[1:] if not a.startswith("--")]:
+        for _ in range(2):
+            r = subprocess.run([sys.executable, __file__, "--child", lib] + (["--large"] if large else []),
+                               timeout=300)
+            if r.returncode:
+                sys.exit(r.returncode)
+
+
+if __name__ == "__main__":
+    main()
