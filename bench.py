@@ -55,6 +55,16 @@ def bytes_per_game(kernel: str, K: int, ticks: int = 1) -> int:
     return ticks * (OBS_BYTES + ACT_BYTES) + state_in + state_out
 
 
+def rollout_kernel_name(B: int, K: int) -> str:
+    """The kernel orx_rollout launches for this batch (orx_engine.hip
+    use_pc_rollout: producer/consumer form up to 4 x 65,536 games; the
+    RandomBot + trajectory specialization FAST=1)."""
+    ncap = 0 if K == 0 else 8 if K <= 8 else 16
+    mode = os.environ.get("ORX_ROLLOUT")
+    pc = (B <= 4 * 65536) if mode not in ("pc", "plain") else mode == "pc"
+    return f"{'rollout_pc_kernel' if pc else 'rollout_kernel'}<{ncap}, true>"
+
+
 def cpu_baseline(cfg_dict: dict, seconds: float) -> dict:
     """The C oracle (scalar port of the reference updater), one host core,
     same workload shape; bounded to about `seconds` of CPU work."""
@@ -244,7 +254,7 @@ def main():
     if rank == 0:
         traffic = None
         if os.path.exists(TRAFFIC_FILE):
-            tr = json.load(open(TRAFFIC_FILE)).get("rollout_kernel", {})
+            tr = json.load(open(TRAFFIC_FILE)).get("rollout", {})
             if tr.get("batch") == B and tr.get("ticks") == chunk:
                 traffic = tr.get("hbm_bytes_per_launch")
         extra = None
@@ -278,7 +288,7 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "rollout_kernel<8>",
+                "kernel": rollout_kernel_name(B, cfg.n_npcs),
                 "achieved": achieved_gbs,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

@@ -60,6 +60,14 @@ constexpr uint32_t kWordCap = 4096;  // per stream; exceeding it stops the game
 constexpr int32_t kStartTick = 1;     // GameState.tick of a fresh game (worldgen.py:87,133)
 constexpr uint32_t kDeadSlot = 0xFFFFu;
 
+// Diagnostic builds only (-DORX_DIAG=bits; results are wrong): rollout_kernel
+// 1 no policy RNG, 2 no initiative RNG, 4 no move logic, 8 no reset, 16 no
+// trajectory; rollout_pc_kernel 16 no trajectory, 32 trivial producer, 64 no
+// move logic.  Used by tools/ab_rollout.py to attribute time.
+#ifndef ORX_DIAG
+#define ORX_DIAG 0
+#endif
+
 struct Key {
   uint32_t k0, k1;
 };
@@ -915,9 +923,6 @@ __global__ void __launch_bounds__(256) rollout_kernel(orx_cfg_t hc, orx_state_t 
   Deltas dl = {0, 0, 0, 0, 0, 0};
   bool stairs_dirty = false, npc_dirty = false;
   const bool any_random = pol1 == ORX_POLICY_RANDOM || pol2 == ORX_POLICY_RANDOM;
-#ifndef ORX_DIAG
-#define ORX_DIAG 0  // diagnostic builds only (results wrong): 1 no policy RNG, 2 no
-#endif              // initiative RNG, 4 no move logic, 8 no reset, 16 no trajectory
   for (int32_t t = 0; t < n_ticks; ++t) {
     const uint32_t pk_pol = (ORX_DIAG & 1) ? ((uint32_t)tick * 0x9E3779B9u) ^ (game * 0x85EBCA6Bu)
                             : any_random ? policy_packed(key, game, ep, tick) : 0u;
@@ -1036,7 +1041,6 @@ __global__ void __launch_bounds__(128) rollout_pc_kernel(
   const uint32_t i = blockIdx.x * 64u + lane;
   const bool valid = i < B;                 // no early return: every wave runs every iteration
   const Cfg c = make_cfg(hc);
-  const uint32_t game = off + i;
   const int need = (pol1 == ORX_POLICY_RANDOM) + (pol2 == ORX_POLICY_RANDOM);
   if (wave == 0) {
     rec_t[lane] = -1;
@@ -1044,18 +1048,16 @@ __global__ void __launch_bounds__(128) rollout_pc_kernel(
   }
   __syncthreads();
 
+  // lanes past B shadow game B-1 (uniform control flow; nothing is stored)
+  const uint32_t ic = valid ? i : B - 1u;
+  const uint32_t gc = off + ic;
   if (wave == 0) {
-    KeyPred pk{0, 0, false};
-    if (valid) {
-      pk.ep = (uint32_t)st.episode[i];
-      pk.tick = st.tick[i];
-      pk.ended = st.status[i] != ORX_IN_PROGRESS;
-    }
+    KeyPred pk{(uint32_t)st.episode[ic], st.tick[ic], st.status[ic] != ORX_IN_PROGRESS};
     int32_t seen = -1;
     for (int32_t t = 0; t < n_ticks; ++t) {
       if (t >= kRing)  // slot t % kRing is free once iteration t - kRing was read
         while ((int32_t)lds_acquire(&consumed) <= t - kRing) __builtin_amdgcn_s_sleep(1);
-      if (valid) {
+      {
         const int32_t rt = __hip_atomic_load(&rec_t[lane], __ATOMIC_RELAXED,
                                              __HIP_MEMORY_SCOPE_WORKGROUP);
         if (rt != seen) {  // rare: re-predict from the consumer's posted key
@@ -1065,8 +1067,9 @@ __global__ void __launch_bounds__(128) rollout_pc_kernel(
           pk.ended = rec_ended[lane] != 0;
           for (int32_t k = rt; k < t; ++k) pk.advance(c);
         }
-        ring[(uint32_t)t % kRing][lane] =
-            Slot{pc_word(key, game, pk.ep, pk.tick, need), pk.ep, pk.tick, 0};
+        const uint32_t word = (ORX_DIAG & 32) ? 0x09u ^ ((uint32_t)pk.tick & 64u)
+                                               : pc_word(key, gc, pk.ep, pk.tick, need);
+        ring[(uint32_t)t % kRing][lane] = Slot{word, pk.ep, pk.tick, 0};
         pk.advance(c);
       }
       if (lane == 0) lds_release(&produced, (uint32_t)t + 1);
@@ -1076,30 +1079,32 @@ __global__ void __launch_bounds__(128) rollout_pc_kernel(
 
   // consumer
   Player p1, p2;
-  int32_t tick = 0, status = ORX_IN_PROGRESS;
-  uint32_t ep = 0;
+  load_players(st, B, ic, p1, p2);
+  int32_t tick = st.tick[ic];
+  int32_t status = st.status[ic];
+  uint32_t ep = (uint32_t)st.episode[ic];
   Npcs<NCAP> npc;
+  load_npcs(st, c, B, ic, npc);
   Deltas dl = {0, 0, 0, 0, 0, 0};
   bool stairs_dirty = false, npc_dirty = false;
-  if (valid) {
-    load_players(st, B, i, p1, p2);
-    tick = st.tick[i];
-    status = st.status[i];
-    ep = (uint32_t)st.episode[i];
-    load_npcs(st, c, B, i, npc);
-  }
-  const NpcMem m{st.npc_pos, st.npc_health, B, i};
-  int32_t avail = 0;  // iterations known to be produced by both producers
+  const NpcMem m{st.npc_pos, st.npc_health, B, ic};
+  int32_t avail;  // iterations known to be produced
+  while ((avail = (int32_t)lds_acquire(&produced)) <= 0) __builtin_amdgcn_s_sleep(1);
+  Slot sl = ring[0][lane];
   for (int32_t t = 0; t < n_ticks; ++t) {
-    if (t >= avail)
-      while ((avail = (int32_t)lds_acquire(&produced)) <= t) __builtin_amdgcn_s_sleep(1);
-    const Slot sl = valid ? ring[(uint32_t)t % kRing][lane] : Slot{0, 0, 0, 0};
+    // slot t was read last iteration: hand it back, then prefetch slot t+1 so
+    // its LDS latency hides under this tick
     if (lane == 0) lds_release(&consumed, (uint32_t)t + 1);
-    if (!valid) continue;
+    Slot nx = sl;
+    if (t + 1 < n_ticks) {
+      if (t + 1 >= avail)
+        while ((avail = (int32_t)lds_acquire(&produced)) <= t + 1) __builtin_amdgcn_s_sleep(1);
+      nx = ring[(uint32_t)(t + 1) % kRing][lane];
+    }
     uint32_t w = sl.word;
     if (sl.ep != ep || sl.tick != tick) {
       // rare (after a death): draw here, post the true key
-      w = pc_word(key, game, ep, tick, need);
+      w = pc_word(key, gc, ep, tick, need);
       rec_ep[lane] = ep;
       rec_tick[lane] = tick;
       rec_ended[lane] = status != ORX_IN_PROGRESS;
@@ -1112,16 +1117,25 @@ __global__ void __launch_bounds__(128) rollout_pc_kernel(
       const int32_t descents = dl.descend;
       bool err = (w & 128u) != 0;
       Events<false> ev{nullptr, 0};
-      tick_game(c, key, game, ep, (w & 64u) != 0, true, p1, p2, npc, m, tick, status, err, dl, ev);
+      if (ORX_DIAG & 64) {
+        tick += 1;
+        p1.x ^= (w >> 6) & 1u;
+        status = (c.max_ticks && tick >= c.max_ticks) ? ORX_TIE : ORX_IN_PROGRESS;
+      } else {
+        tick_game(c, key, gc, ep, (w & 64u) != 0, valid, p1, p2, npc, m, tick, status, err, dl,
+                  ev);
+      }
       stairs_dirty |= dl.descend != descents;
     } else if (c.autoreset) {
       ep += 1;
-      setup_game(c, key, game, ep, p1, p2, npc, tick, status);
-      if constexpr (NCAP > 0) store_new_npcs(st, c, B, i, npc);
+      setup_game(c, key, gc, ep, p1, p2, npc, tick, status);
+      if constexpr (NCAP > 0) if (valid) store_new_npcs(st, c, B, i, npc);
       stairs_dirty = true;
       npc_dirty = true;
     }
-    store_traj<FAST>(obs, act, t, B, i, p1, p2, tick, status, a1, a2);
+    if (!(ORX_DIAG & 16) && valid)
+      store_traj<FAST>(obs, act, t, B, i, p1, p2, tick, status, a1, a2);
+    sl = nx;
   }
   if (valid) {
     store_players(st, B, i, p1, p2, stairs_dirty);

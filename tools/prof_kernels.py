@@ -1,6 +1,7 @@
 """Launch sequence for rocprofv3 counter passes (profiles/README.md):
-  rollout_kernel<8>: C3, B=65536, 50 ticks with obs/act  (x3)
-  step_kernel<8> + policy_kernel: C3, B=2^21             (x5)"""
+  rollout at the bench config (C3, B=65536, 50 ticks with obs/act, x4:
+  rollout_pc_kernel<8, true>), then policy_kernel + step_kernel<8> at B=2^21
+  (x6) and the plain rollout_kernel<8, true> at 2^21 x 20 ticks (x2)."""
 import os
 import sys
 
@@ -24,5 +25,10 @@ BL = 1 << 21
 e = BatchedEngine(EnvConfig.c3(), BL, seed=3, device=dev)
 for _ in range(6):
     e.step(e.policy(1, 1))
+T = 20
+obs = torch.empty((T, 14, BL), dtype=torch.int32, device=dev)
+act = torch.empty((T, BL, 2), dtype=torch.int8, device=dev)
+for _ in range(2):
+    e.rollout(T, 1, 1, obs=obs, act=act)
 torch.cuda.synchronize()
 print("done")
