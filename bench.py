@@ -41,8 +41,18 @@ ACT_BYTES = 2
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic.json")
 
 
+def contract_bytes_per_env_step(K: int) -> int:
+    """SURVEY.md §8(d)'s algorithmic bytes per env-step (the roofline contract):
+    read actions 2 + players 32 + tick/status 8 + staircases 16 = 58, write
+    players 32 + tick/status 8 = 40 -> 98 B; +8 B occupancy probe with NPCs
+    (C3) -> 106 B.  A fused rollout keeps the state in registers and skips the
+    re-read (its moved bytes, `traffic` / `materialized_bytes_per_launch`, are
+    lower); the contract figure is what `roofline.achieved` prices."""
+    return 98 + (8 if K else 0)
+
+
 def bytes_per_game(kernel: str, K: int, ticks: int = 1) -> int:
-    """Algorithmic HBM bytes per game per launch of a kernel."""
+    """Bytes each kernel actually reads + writes per game per launch."""
     npc_read = (4 + 2 * K) if K else 0        # alive mask + K packed u16 positions
     if kernel == "step":
         # read: actions 2, players 32, staircases 16, tick/status/episode 12, NPCs
@@ -147,13 +157,14 @@ def extras(torch, cfg, dev, B_cfg, K):
     eng.rollout(T, 1, 1, obs=obs, act=act)
     roll_s = timed_launches(torch, lambda: eng.rollout(T, 1, 1, obs=obs, act=act), 5)
     med = lambda v: sorted(v)[len(v) // 2]
-    sb = bytes_per_game("step", K) * BL
-    rb = bytes_per_game("rollout", K, T) * BL
+    sb = contract_bytes_per_env_step(K) * BL
+    rb = contract_bytes_per_env_step(K) * BL * T
     out["large_batch"] = {
         "games": BL,
         "step_kernel": {"avg_us": med(step_s) * 1e6, "achieved_GBps": sb / med(step_s) / 1e9,
                         "frac": sb / med(step_s) / 1e9 / HBM_PEAK_GBS,
-                        "bytes_per_env_step": bytes_per_game("step", K)},
+                        "bytes_per_env_step": contract_bytes_per_env_step(K),
+                        "moved_bytes_per_env_step": bytes_per_game("step", K)},
         "policy_kernel": {"avg_us": med(pol_s) * 1e6},
         "rollout_kernel": {"avg_us": med(roll_s) * 1e6, "ticks": T,
                            "env_steps_per_s": BL * T / med(roll_s),
@@ -238,8 +249,9 @@ def main():
     durs = [(a.elapsed_time(b) * 1e-3, n) for a, b, n in events]
     full = [d for d, n in durs if n == chunk]
     avg_launch_s = sum(full) / max(1, len(full))
-    bytes_per_launch = bytes_per_game("rollout", cfg.n_npcs, chunk) * B
+    bytes_per_launch = contract_bytes_per_env_step(cfg.n_npcs) * B * chunk
     achieved_gbs = bytes_per_launch / avg_launch_s / 1e9
+    materialized = bytes_per_game("rollout", cfg.n_npcs, chunk) * B
 
     # the only collective: all-gather of per-game episode returns (RCCL / xGMI)
     torch.cuda.synchronize()
@@ -295,7 +307,10 @@ def main():
                 "frac": achieved_gbs / HBM_PEAK_GBS,
                 "traffic": traffic,
                 "bytes_per_launch": bytes_per_launch,
-                "bytes_per_env_step": OBS_BYTES + ACT_BYTES,
+                "bytes_per_env_step": contract_bytes_per_env_step(cfg.n_npcs),
+                "env_steps_per_launch": B * chunk,
+                "materialized_bytes_per_launch": materialized,
+                "materialized_GBps": materialized / avg_launch_s / 1e9,
                 "avg_launch_us": avg_launch_s * 1e6,
                 "launches": len(full),
             },

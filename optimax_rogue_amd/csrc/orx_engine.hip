@@ -980,9 +980,10 @@ __global__ void __launch_bounds__(256) rollout_kernel(orx_cfg_t hc, orx_state_t 
 // max_ticks is reached, then (episode+1, kStartTick) under autoreset -- which
 // is exact except after a player death.  Every slot carries the key it was
 // drawn for; the consumer checks it and on a mismatch draws the words itself
-// and posts its true key, from which the producers re-predict.  Results are
+// and posts its true key, from which the producer re-predicts.  Results are
 // therefore identical to rollout_kernel whatever the timing.
-constexpr int kRing = 8;                 // ticks a producer may run ahead
+constexpr int kRing = 8;        // ticks the producer may run ahead
+constexpr int kBackoff = 8;     // producer poll back-off, units of 64 cycles
 
 // producer word: bits 0-2 first RandomBot move, 3-5 second, 6 p1 first,
 // 7 RNG exhausted
@@ -1055,8 +1056,11 @@ __global__ void __launch_bounds__(128) rollout_pc_kernel(
     KeyPred pk{(uint32_t)st.episode[ic], st.tick[ic], st.status[ic] != ORX_IN_PROGRESS};
     int32_t seen = -1;
     for (int32_t t = 0; t < n_ticks; ++t) {
-      if (t >= kRing)  // slot t % kRing is free once iteration t - kRing was read
-        while ((int32_t)lds_acquire(&consumed) <= t - kRing) __builtin_amdgcn_s_sleep(1);
+      // slot t % kRing is free once iteration t - kRing was read.  A full ring
+      // means the producer is a whole ring ahead: sleep long (each poll takes
+      // issue slots from the consumer on the same SIMD).
+      if (t >= kRing)
+        while ((int32_t)lds_acquire(&consumed) <= t - kRing) __builtin_amdgcn_s_sleep(kBackoff);
       {
         const int32_t rt = __hip_atomic_load(&rec_t[lane], __ATOMIC_RELAXED,
                                              __HIP_MEMORY_SCOPE_WORKGROUP);
