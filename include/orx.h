@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define ORX_ABI_VERSION 1
+#define ORX_ABI_VERSION 2
 
 /* ---- error codes -------------------------------------------------------- */
 #define ORX_OK 0
@@ -138,6 +138,11 @@ typedef struct orx_cfg {
   int32_t player_armor;   /* 1  */
   int32_t autoreset;      /* 1: a finished game is reset by the next step    */
   int32_t flags;          /* extension flags; 0 = reference parity           */
+  int32_t n_layouts;      /* dungeon generator: 0 = EmptyDungeonGenerator
+                             (closed forms, worldgen.py:28-44); L > 0 = a
+                             layout bank: spawn_dungeon(depth) returns layout
+                             randint(L) of orx_state_t.bank_* (an explicit-
+                             grid DungeonGenerator plugin, worldgen.py:9-26) */
 } orx_cfg_t;
 
 /* ---- batch state (SoA, batch axis contiguous; all device pointers) ------- */
@@ -159,6 +164,16 @@ typedef struct orx_state {
   uint16_t* npc_pos;   /* [K][B] x | y << 8  (NULL when K == 0)              */
   int8_t* npc_health;  /* [K][B]                                             */
   uint32_t* npc_alive; /* [B]    bit k = NPC k still in GameState.entities   */
+  /* dungeon bank (cfg->n_layouts = L > 0; all NULL otherwise)               */
+  int16_t* p_layout;            /* [2][B] layout of each player's depth       */
+  const uint8_t* bank_tiles;    /* [L][W][H] Tile codes, Dungeon.tiles layout
+                                   (flat x * H + y)       world.py:19-39     */
+  const uint16_t* bank_ground;  /* [L][W*H] flat indices of the Ground tiles
+                                   in ascending order (get_random_unblocked's
+                                   candidate list, world.py:57-66)           */
+  const int32_t* bank_meta;     /* [L][4] {n_ground, staircase x, staircase y,
+                                   0}: first StaircaseDown in x-major order
+                                   (Dungeon.staircase, world.py:52-55)       */
 } orx_state_t;
 
 /* ---- entry points --------------------------------------------------------- */
@@ -225,6 +240,14 @@ int orx_rollout(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p1,
 int orx_dungeon_stairs(const orx_cfg_t* cfg, const uint32_t* game_ids, const int32_t* episodes,
                        const int32_t* depths, const int32_t* gens, int32_t* sx, int32_t* sy,
                        int64_t n, uint64_t seed, void* stream);
+
+/* orx_dungeon_stairs for any generator: also writes layout[j] (the bank
+ * layout, or -1 for EmptyDungeonGenerator; layout may be NULL).  Only the
+ * bank_* pointers of st are read. */
+int orx_dungeon_spawn(const orx_cfg_t* cfg, const orx_state_t* st, const uint32_t* game_ids,
+                      const int32_t* episodes, const int32_t* depths, const int32_t* gens,
+                      int32_t* sx, int32_t* sy, int32_t* layout, int64_t n, uint64_t seed,
+                      void* stream);
 
 #ifdef __cplusplus
 }

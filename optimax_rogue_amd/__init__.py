@@ -5,10 +5,11 @@ Host side is Python; the tick, reset and bot policies are HIP kernels for
 gfx950 in liborx.so, reached through the C-ABI declared in include/orx.h.
 """
 from .config import EnvConfig
+from .dungeons import DungeonBank
 from .enums import (CombatFlag, DungeonDespawningStrategy, Move, OBS_FIELDS, Policy, StartMode,
                     Tile, UpdateResult)
 
-__all__ = ["EnvConfig", "Move", "UpdateResult", "DungeonDespawningStrategy", "Tile", "CombatFlag",
+__all__ = ["EnvConfig", "DungeonBank", "Move", "UpdateResult", "DungeonDespawningStrategy", "Tile", "CombatFlag",
            "StartMode", "Policy", "OBS_FIELDS", "BatchedEngine", "BatchedUpdater"]
 
 

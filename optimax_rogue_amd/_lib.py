@@ -13,14 +13,15 @@ from .config import OrxCfg
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "liborx.so")
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 
 class OrxState(ctypes.Structure):
     """ctypes mirror of orx_state_t (device pointers)."""
     _fields_ = [(n, ctypes.c_void_p) for n in (
         "p_x", "p_y", "p_depth", "p_health", "st_x", "st_y", "tick", "status", "episode",
-        "ret_sum", "ep_count", "counters", "npc_pos", "npc_health", "npc_alive")]
+        "ret_sum", "ep_count", "counters", "npc_pos", "npc_health", "npc_alive",
+        "p_layout", "bank_tiles", "bank_ground", "bank_meta")]
 
 
 class OrxError(RuntimeError):
@@ -32,7 +33,8 @@ class OrxError(RuntimeError):
 _lib = None
 
 EXPORTS = ("orx_abi_version", "orx_last_error", "orx_validate_cfg", "orx_reset", "orx_step",
-           "orx_step_events", "orx_policy", "orx_rollout", "orx_dungeon_stairs")
+           "orx_step_events", "orx_policy", "orx_rollout", "orx_dungeon_stairs",
+           "orx_dungeon_spawn")
 
 
 def load() -> ctypes.CDLL:
@@ -66,6 +68,9 @@ def load() -> ctypes.CDLL:
     L.orx_rollout.argtypes = [P(OrxCfg), P(OrxState), i32, i32, i32, vp, vp, i64, u64, i64, vp]
     L.orx_dungeon_stairs.restype = ctypes.c_int
     L.orx_dungeon_stairs.argtypes = [P(OrxCfg), vp, vp, vp, vp, vp, vp, i64, u64, vp]
+    L.orx_dungeon_spawn.restype = ctypes.c_int
+    L.orx_dungeon_spawn.argtypes = [P(OrxCfg), P(OrxState), vp, vp, vp, vp, vp, vp, vp, i64, u64,
+                                    vp]
     v = L.orx_abi_version()
     if v != ABI_VERSION:
         raise RuntimeError(f"liborx.so ABI {v} != expected {ABI_VERSION}")

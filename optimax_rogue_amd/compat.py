@@ -98,9 +98,14 @@ class EntityView:
 
 
 class DungeonView:
-    """EmptyDungeonGenerator layout (worldgen.py:33-43) with its staircase."""
+    """A Dungeon (world.py:19-99): the EmptyDungeonGenerator layout
+    (worldgen.py:33-43) with its staircase, or the given tiles (a dungeon-bank
+    layout)."""
 
-    def __init__(self, width: int, height: int, sx: int, sy: int):
+    def __init__(self, width: int, height: int, sx: int, sy: int, tiles=None):
+        if tiles is not None:
+            self.tiles = np.asarray(tiles, np.int32)
+            return
         t = np.full((width, height), Tile.Ground.value, np.int32)
         t[[0, -1], :] = Tile.Wall.value
         t[:, [0, -1]] = Tile.Wall.value
@@ -262,30 +267,37 @@ def world_depths(cfg, d1: int, d2: int) -> List[int]:
     return [d1] if d1 == d2 else [d1, d2]
 
 
-def game_state(snap: dict, i: int, cfg, extra_stairs: Optional[Dict[int, tuple]] = None
-               ) -> GameStateView:
+def game_state(snap: dict, i: int, cfg, extra_stairs: Optional[Dict[int, tuple]] = None,
+               bank=None) -> GameStateView:
     """Game ``i`` of a BatchedEngine.snapshot() in the reference schema.
 
     The world holds the players' current dungeons; with ``extra_stairs``
-    ({depth: (sx, sy)}, from ``BatchedEngine.game_states``) it holds every
-    dungeon of World.dungeons (``world_depths``)."""
+    ({depth: (sx, sy[, layout])}, from ``BatchedEngine.game_states``) it holds
+    every dungeon of World.dungeons (``world_depths``).  With a dungeon bank
+    (``bank``, snapshot with ``p_layout``) the dungeons are its layouts."""
     W, H = int(cfg.width), int(cfg.height)
     ents = []
     dungeons = {}
     cur = {}
+
+    def view(sx, sy, lay=-1):
+        if bank is not None:
+            return DungeonView(W, H, sx, sy, tiles=bank.tiles(int(lay)))
+        return DungeonView(W, H, sx, sy)
+
     for p in range(2):
         d = int(snap["p_depth"][p][i])
         ents.append(EntityView(1 + p, d, snap["p_x"][p][i], snap["p_y"][p][i],
                                snap["p_health"][p][i], cfg.player_health, cfg.player_damage,
                                cfg.player_armor))
-        cur.setdefault(d, (int(snap["st_x"][p][i]), int(snap["st_y"][p][i])))
+        lay = int(snap["p_layout"][p][i]) if bank is not None else -1
+        cur.setdefault(d, (int(snap["st_x"][p][i]), int(snap["st_y"][p][i]), lay))
     if extra_stairs is None:
-        for d, (sx, sy) in cur.items():
-            dungeons[d] = DungeonView(W, H, sx, sy)
+        for d, key in cur.items():
+            dungeons[d] = view(*key)
     else:
         for d in world_depths(cfg, int(snap["p_depth"][0][i]), int(snap["p_depth"][1][i])):
-            sx, sy = cur[d] if d in cur else extra_stairs[d]
-            dungeons[d] = DungeonView(W, H, sx, sy)
+            dungeons[d] = view(*(cur[d] if d in cur else extra_stairs[d]))
     K = int(cfg.n_npcs)
     if K:
         alive = int(snap["npc_alive"][i])

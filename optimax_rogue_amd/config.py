@@ -7,17 +7,22 @@ Reference counterparts:
   TogetherGameStartGenerator(dgen)                  optimax_rogue/logic/worldgen.py:61-87
   SeparatedGameStartGenerator(dgen, p1_depth, p2_depth)  worldgen.py:90-135
   Entity(iden, depth, x, y, 10, 10, 2, 1, [], {})   worldgen.py:85-86
+  an explicit-grid DungeonGenerator plugin          worldgen.py:9-26 (``layouts``,
+                                                    optimax_rogue_amd.dungeons.DungeonBank)
 """
 from __future__ import annotations
 
 import ctypes
 import dataclasses
+from typing import Optional
+
+import numpy as np
 
 from .enums import DungeonDespawningStrategy, StartMode
 
 CFG_FIELDS = ("width", "height", "despawn", "max_ticks", "start_mode", "p1_depth", "p2_depth",
               "n_npcs", "npc_health", "npc_damage", "npc_armor", "player_health",
-              "player_damage", "player_armor", "autoreset", "flags")
+              "player_damage", "player_armor", "autoreset", "flags", "n_layouts")
 
 
 class OrxCfg(ctypes.Structure):
@@ -43,6 +48,13 @@ class EnvConfig:
     player_armor: int = 1
     autoreset: int = 1
     flags: int = 0
+    # explicit-grid dungeon generator: [L, W, H] Tile codes (None =
+    # EmptyDungeonGenerator).  spawn_dungeon(depth) returns layout randint(L).
+    layouts: Optional[np.ndarray] = dataclasses.field(default=None, repr=False, compare=False)
+
+    @property
+    def n_layouts(self) -> int:
+        return 0 if self.layouts is None else int(len(self.layouts))
 
     def to_c(self) -> OrxCfg:
         vals = {f: int(getattr(self, f) or 0) for f in CFG_FIELDS}
@@ -52,8 +64,12 @@ class EnvConfig:
         return {f: int(getattr(self, f) or 0) for f in CFG_FIELDS}
 
     @classmethod
-    def from_dict(cls, d: dict) -> "EnvConfig":
-        return cls(**{k: v for k, v in d.items() if k in CFG_FIELDS})
+    def from_dict(cls, d: dict, layouts=None) -> "EnvConfig":
+        """Fields of CFG_FIELDS (n_layouts is derived from ``layouts``)."""
+        kw = {k: v for k, v in d.items() if k in CFG_FIELDS and k != "n_layouts"}
+        if layouts is None:
+            layouts = d.get("layouts")
+        return cls(**kw, layouts=None if layouts is None else np.asarray(layouts, np.uint8))
 
     # --- the BASELINE.json configurations -------------------------------
     @classmethod

@@ -132,6 +132,7 @@ struct NpBound {
 // ---------------------------------------------------------------------------
 struct Player {
   int32_t x, y, d, hp, sx, sy;
+  int32_t lay;    // bank layout of the player's depth (dungeon bank only)
   int32_t move;   // validated move for this tick
   int32_t tx, ty; // target cell of `move` from the pre-tick position
 };
@@ -146,6 +147,7 @@ __device__ __forceinline__ Player pick(bool c, const Player& a, const Player& b)
   r.hp = c ? a.hp : b.hp;
   r.sx = c ? a.sx : b.sx;
   r.sy = c ? a.sy : b.sy;
+  r.lay = c ? a.lay : b.lay;
   r.move = c ? a.move : b.move;
   r.tx = c ? a.tx : b.tx;
   r.ty = c ? a.ty : b.ty;
@@ -159,6 +161,12 @@ struct Cfg {  // device copy of orx_cfg_t plus derived constants (all wave-unifo
   NpBound ground;    // randint(n_ground), n_ground = (W-2)(H-2) - 1
   NpBound stair_x;   // randint(1, W-2)
   NpBound stair_y;   // randint(1, H-2)
+  // dungeon bank (n_layouts > 0): layouts as Dungeon.tiles, Ground lists, meta
+  int32_t L;
+  NpBound layout;    // randint(L)
+  const uint8_t* tiles;
+  const uint16_t* gground;
+  const int32_t* gmeta;
 };
 
 struct Deltas {  // counter / return increments, flushed once per launch
@@ -265,13 +273,58 @@ __device__ __forceinline__ void calc_pos(int32_t x, int32_t y, int32_t m, int32_
   ny = y + (int32_t)((kDy >> sh) & 3u) - 1;
 }
 
-__device__ __forceinline__ bool blocked(const Cfg& c, int32_t x, int32_t y) {
-  return x <= 0 || x >= c.W - 1 || y <= 0 || y >= c.H - 1;
+// Dungeon.tiles[x, y] of bank layout `lay` (x, y inside the grid).
+__device__ __forceinline__ uint32_t bank_tile(const Cfg& c, int32_t lay, int32_t x, int32_t y) {
+  return c.tiles[(size_t)lay * (uint32_t)(c.W * c.H) + (uint32_t)(x * c.H + y)];
 }
 
-// c-th Ground tile of the dungeon with staircase (sx, sy), x-major order.
-__device__ __forceinline__ void ground_cell(const Cfg& c, uint32_t ch, int32_t sx, int32_t sy,
-                                            int32_t& x, int32_t& y) {
+// Dungeon.is_blocked (world.py:41-46).  GRID = dungeon bank: outside the grid
+// or a Wall tile; else EmptyDungeonGenerator's border.
+template <bool GRID>
+__device__ __forceinline__ bool blocked(const Cfg& c, int32_t lay, int32_t x, int32_t y) {
+  if constexpr (GRID) {
+    if (x < 0 || x >= c.W || y < 0 || y >= c.H) return true;
+    return bank_tile(c, lay, x, y) == ORX_TILE_WALL;
+  } else {
+    return x <= 0 || x >= c.W - 1 || y <= 0 || y >= c.H - 1;
+  }
+}
+
+// dung.tiles[newx, newy] == Tile.StaircaseDown (updater.py:205-206) for an
+// unblocked target: any staircase tile of a bank layout; the one staircase of
+// an EmptyDungeonGenerator dungeon.
+template <bool GRID>
+__device__ __forceinline__ bool stair_tile(const Cfg& c, const Player& p, int32_t x, int32_t y) {
+  if constexpr (GRID)
+    return bank_tile(c, p.lay, x, y) == ORX_TILE_STAIRCASE_DOWN;
+  else
+    return x == p.sx && y == p.sy;
+}
+
+// randint(n_ground) bound of a dungeon (world.py:62).
+template <bool GRID>
+__device__ __forceinline__ NpBound ground_bound(const Cfg& c, int32_t lay) {
+  if constexpr (!GRID) {
+    return c.ground;
+  } else {
+    NpBound b;
+    b.set(c.gmeta[4 * lay]);
+    return b;
+  }
+}
+
+// choice-th Ground tile, x-major order: the bank's Ground list, or the
+// closed form for the dungeon with staircase (sx, sy).
+template <bool GRID>
+__device__ __forceinline__ void ground_cell(const Cfg& c, uint32_t ch, int32_t lay, int32_t sx,
+                                            int32_t sy, int32_t& x, int32_t& y) {
+  if constexpr (GRID) {
+    const uint32_t flat = c.gground[(size_t)lay * (uint32_t)(c.W * c.H) + ch];
+    const uint32_t q = flat / (uint32_t)c.H;
+    x = (int32_t)q;
+    y = (int32_t)(flat - q * (uint32_t)c.H);
+    return;
+  }
   const uint32_t s_idx = (uint32_t)((sx - 1) * c.ih + (sy - 1));
   const uint32_t ci = ch + (ch >= s_idx ? 1u : 0u);
   const uint32_t q = ci / (uint32_t)c.ih;
@@ -280,10 +333,28 @@ __device__ __forceinline__ void ground_cell(const Cfg& c, uint32_t ch, int32_t s
 }
 
 // EmptyDungeonGenerator.spawn_dungeon with words from (episode, depth, gen):
-// randint(1, W-2) then randint(1, H-2).  One loop, one Philox call site.
+// randint(1, W-2) then randint(1, H-2); or, with a dungeon bank, layout
+// randint(L) and its staircase.  One loop, one Philox call site.
+template <bool GRID>
 __device__ __forceinline__ void dungeon_stair(const Cfg& c, Key key, uint32_t game, uint32_t ep,
                                            int32_t depth, uint32_t gen, int32_t& sx, int32_t& sy,
-                                           bool& err) {
+                                           int32_t& lay, bool& err) {
+  if constexpr (GRID) {
+    Stream s;
+    s.init(game, ep, (uint32_t)depth, tag(PUR_DUNGEON, gen));
+    uint32_t v = 0;
+    bool ok = c.layout.rng == 0;
+    for (uint32_t t = 0; t < kWordCap && !ok; ++t) {
+      v = s.next(key) & c.layout.mask;
+      ok = v <= c.layout.rng;
+    }
+    if (!ok) { err = true; v = 0; }
+    lay = (int32_t)v;
+    sx = c.gmeta[4 * lay + 1];
+    sy = c.gmeta[4 * lay + 2];
+    return;
+  }
+  lay = -1;
   Stream s;
   s.init(game, ep, (uint32_t)depth, tag(PUR_DUNGEON, gen));
   int n = 0;
@@ -307,7 +378,7 @@ __device__ __forceinline__ void dungeon_stair(const Cfg& c, Key key, uint32_t ga
 // Game start (setup_game + NPC spawner), all placements in one rejection loop
 // over the INIT stream (one Philox call site, one division site).
 // ---------------------------------------------------------------------------
-template <int NCAP>
+template <int NCAP, bool GRID = false>
 __device__ __forceinline__ void setup_game(const Cfg& c, Key key, uint32_t game, uint32_t ep,
                                         Player& p1, Player& p2, Npcs<NCAP>& npc, int32_t& tick,
                                         int32_t& status) {
@@ -315,11 +386,11 @@ __device__ __forceinline__ void setup_game(const Cfg& c, Key key, uint32_t game,
   const bool sep = c.start_mode == ORX_START_SEPARATED;
   p1.d = sep ? c.d1 : 0;
   p2.d = sep ? c.d2 : 0;
-  dungeon_stair(c, key, game, ep, p1.d, 0, p1.sx, p1.sy, err);
+  dungeon_stair<GRID>(c, key, game, ep, p1.d, 0, p1.sx, p1.sy, p1.lay, err);
   if (sep) {
-    dungeon_stair(c, key, game, ep, p2.d, 0, p2.sx, p2.sy, err);
+    dungeon_stair<GRID>(c, key, game, ep, p2.d, 0, p2.sx, p2.sy, p2.lay, err);
   } else {
-    p2.sx = p1.sx; p2.sy = p1.sy;
+    p2.sx = p1.sx; p2.sy = p1.sy; p2.lay = p1.lay;
   }
   npc.clear();
   Stream s;
@@ -327,17 +398,20 @@ __device__ __forceinline__ void setup_game(const Cfg& c, Key key, uint32_t game,
   const int total = 2 + (NCAP ? c.K : 0);
   int placed = 0;
   p1.x = p1.y = p2.x = p2.y = 0;
+  const NpBound g1 = ground_bound<GRID>(c, p1.lay), g2 = ground_bound<GRID>(c, p2.lay);
   for (uint32_t t = 0; t < kWordCap && placed < total; ++t) {
-    uint32_t v = 0;
-    if (c.ground.rng != 0) {
-      v = s.next(key) & c.ground.mask;
-      if (v > c.ground.rng) continue;
-    }
     // placement 0: player 1, 1: player 2, 2+k: NPC k (all NPCs on p1's depth)
     const bool is_p2 = placed == 1;
+    const NpBound gb = is_p2 ? g2 : g1;
+    uint32_t v = 0;
+    if (gb.rng != 0) {
+      v = s.next(key) & gb.mask;
+      if (v > gb.rng) continue;
+    }
     const int32_t sx = is_p2 ? p2.sx : p1.sx, sy = is_p2 ? p2.sy : p1.sy;
+    const int32_t lay = is_p2 ? p2.lay : p1.lay;
     int32_t x, y;
-    ground_cell(c, v, sx, sy, x, y);
+    ground_cell<GRID>(c, v, lay, sx, sy, x, y);
     bool occ = false;
     if (placed >= 1) occ = x == p1.x && y == p1.y && (placed >= 2 || !sep);
     if (placed >= 2) {
@@ -369,7 +443,7 @@ __device__ __forceinline__ void setup_game(const Cfg& c, Key key, uint32_t game,
 //   Unused:      World == {p1.d, p2.d}, so nd is present iff other.d == nd;
 //                a fresh copy is generation 1 iff the other player already
 //                passed through nd (other.start <= nd < other.d).
-template <int NCAP, bool EV>
+template <int NCAP, bool EV, bool GRID>
 __device__ __forceinline__ void descend(const Cfg& c, Key key, uint32_t game, uint32_t ep,
                                      Player& self, const Player& other, int32_t other_start,
                                      const Npcs<NCAP>& npc, Stream& spawn, Deltas& dl, bool& err,
@@ -383,11 +457,11 @@ __device__ __forceinline__ void descend(const Cfg& c, Key key, uint32_t game, ui
     present = other.d == nd;
     gen = (!present && other_start <= nd && nd < other.d) ? 1u : 0u;
   }
-  int32_t sx, sy;
+  int32_t sx, sy, lay;
   if (present && other.d == nd) {
-    sx = other.sx; sy = other.sy;
+    sx = other.sx; sy = other.sy; lay = other.lay;
   } else {
-    dungeon_stair(c, key, game, ep, nd, gen, sx, sy, err);
+    dungeon_stair<GRID>(c, key, game, ep, nd, gen, sx, sy, lay, err);
   }
   if (!present) {
     dl.dungeon += 1;
@@ -396,19 +470,20 @@ __device__ __forceinline__ void descend(const Cfg& c, Key key, uint32_t game, ui
   const bool npc_depth = NCAP > 0 && nd == c.d1 && npc.alive;
   int32_t x = 0, y = 0;
   bool done = false;
+  const NpBound gb = ground_bound<GRID>(c, lay);
   for (uint32_t t = 0; t < kWordCap && !done; ++t) {
     uint32_t v = 0;
-    if (c.ground.rng != 0) {
-      v = spawn.next(key) & c.ground.mask;
-      if (v > c.ground.rng) continue;
+    if (gb.rng != 0) {
+      v = spawn.next(key) & gb.mask;
+      if (v > gb.rng) continue;
     }
-    ground_cell(c, v, sx, sy, x, y);
+    ground_cell<GRID>(c, v, lay, sx, sy, x, y);
     bool occ = other.d == nd && other.x == x && other.y == y;
     if (npc_depth) occ = occ || npc.find(pack_xy(x, y)) >= 0;
     done = !occ;
   }
   if (!done) err = true;
-  self.d = nd; self.x = x; self.y = y; self.sx = sx; self.sy = sy;
+  self.d = nd; self.x = x; self.y = y; self.sx = sx; self.sy = sy; self.lay = lay;
   dl.descend += 1;
   ev.emit(ORX_EV_POSITION, self_iden, nd, (x & 0xFFFF) | (y << 16));  // updater.py:287-290
 }
@@ -540,7 +615,7 @@ struct NpcMem {  // HBM rows of this game's NPC slots (stride B)
 // handle_move for `self` (updater.py:180-243), branch-free except for the
 // rare descend.  Returns true if the target cell holds an NPC (the slot is
 // resolved in npc_hits); combat against the other player is applied here.
-template <int NCAP, bool EV>
+template <int NCAP, bool EV, bool GRID>
 __device__ __forceinline__ bool handle_move(const Cfg& c, Key key, uint32_t game, uint32_t ep,
                                             Player& self, Player& other, int32_t other_start,
                                             const Npcs<NCAP>& npc, Stream& spawn, Deltas& dl,
@@ -552,7 +627,7 @@ __device__ __forceinline__ bool handle_move(const Cfg& c, Key key, uint32_t game
   const bool hit_npc = NCAP > 0 && moving && !occ_other && self.d == c.d1 &&
                        npc.any(pack_xy(tx, ty));
   const bool free = moving && !occ_other && !hit_npc;
-  const bool stairs = free && tx == self.sx && ty == self.sy;
+  const bool stairs = free && stair_tile<GRID>(c, self, tx, ty);
   const bool step = free && !stairs;
   self.x = step ? tx : self.x;
   self.y = step ? ty : self.y;
@@ -573,7 +648,9 @@ __device__ __forceinline__ bool handle_move(const Cfg& c, Key key, uint32_t game
     if (hit_npc) ev.emit(ORX_EV_COMBAT, self_iden, 3 + npc.find(pack_xy(tx, ty)), ORX_FLAG_BLOCK);
     if (step) ev.emit(ORX_EV_POSITION, self_iden, self.d, (tx & 0xFFFF) | (ty << 16));
   }
-  if (stairs) descend(c, key, game, ep, self, other, other_start, npc, spawn, dl, err, self_iden, ev);
+  if (stairs)
+    descend<NCAP, EV, GRID>(c, key, game, ep, self, other, other_start, npc, spawn, dl, err,
+                            self_iden, ev);
   return hit_npc;
 }
 
@@ -609,16 +686,16 @@ __device__ __forceinline__ void npc_hits(const Cfg& c, Npcs<NCAP>& npc, const Np
 }
 
 // One Updater.update for an in-progress game; p1.move/p2.move = raw moves.
-template <int NCAP, bool EV>
+template <int NCAP, bool EV, bool GRID = false>
 __device__ __forceinline__ void tick_game(const Cfg& c, Key key, uint32_t game, uint32_t ep,
                                           bool p1_first, bool writer, Player& p1, Player& p2,
                                           Npcs<NCAP>& npc, const NpcMem& m, int32_t& tick,
                                           int32_t& status, bool& err, Deltas& dl,
                                           Events<EV>& ev) {
   calc_pos(p1.x, p1.y, p1.move, p1.tx, p1.ty);         // updater.py:89-98
-  if (blocked(c, p1.tx, p1.ty)) p1.move = ORX_MOVE_STAY;
+  if (blocked<GRID>(c, p1.lay, p1.tx, p1.ty)) p1.move = ORX_MOVE_STAY;
   calc_pos(p2.x, p2.y, p2.move, p2.tx, p2.ty);
-  if (blocked(c, p2.tx, p2.ty)) p2.move = ORX_MOVE_STAY;
+  if (blocked<GRID>(c, p2.lay, p2.tx, p2.ty)) p2.move = ORX_MOVE_STAY;
 
   // p1_first: the player shuffle (updater.py:114).  The NPC shuffle (:127)
   // draws later words of the same per-tick stream and only orders Stay-ing
@@ -630,9 +707,9 @@ __device__ __forceinline__ void tick_game(const Cfg& c, Key key, uint32_t game, 
   const int32_t a_start = p1_first ? c.d1 : c.d2;
   const int32_t b_start = p1_first ? c.d2 : c.d1;
   const int32_t a_iden = p1_first ? 1 : 2;
-  const bool hA = handle_move(c, key, game, ep, A, Bp, b_start, npc, spawn, dl, err, a_iden, true,
+  const bool hA = handle_move<NCAP, EV, GRID>(c, key, game, ep, A, Bp, b_start, npc, spawn, dl, err, a_iden, true,
                               ev);
-  const bool hB = handle_move(c, key, game, ep, Bp, A, a_start, npc, spawn, dl, err, 3 - a_iden,
+  const bool hB = handle_move<NCAP, EV, GRID>(c, key, game, ep, Bp, A, a_start, npc, spawn, dl, err, 3 - a_iden,
                               false, ev);
   if (NCAP > 0 && (hA || hB)) {
     // NPCs never move and are swept only after both moves: the slots found at
@@ -663,6 +740,7 @@ __device__ __forceinline__ void tick_game(const Cfg& c, Key key, uint32_t game, 
 // ---------------------------------------------------------------------------
 // SoA load / store helpers (32-bit lane index: B < 2^31)
 // ---------------------------------------------------------------------------
+template <bool GRID = false>
 __device__ __forceinline__ void load_players(const orx_state_t& st, uint32_t B, uint32_t i,
                                              Player& p1, Player& p2) {
   p1.x = st.p_x[i];           p2.x = st.p_x[B + i];
@@ -671,8 +749,11 @@ __device__ __forceinline__ void load_players(const orx_state_t& st, uint32_t B, 
   p1.hp = st.p_health[i];     p2.hp = st.p_health[B + i];
   p1.sx = st.st_x[i];         p2.sx = st.st_x[B + i];
   p1.sy = st.st_y[i];         p2.sy = st.st_y[B + i];
+  p1.lay = GRID ? st.p_layout[i] : -1;
+  p2.lay = GRID ? st.p_layout[B + i] : -1;
 }
 
+template <bool GRID = false>
 __device__ __forceinline__ void store_players(const orx_state_t& st, uint32_t B, uint32_t i,
                                               const Player& p1, const Player& p2, bool stairs) {
   st.p_x[i] = p1.x;           st.p_x[B + i] = p2.x;
@@ -682,6 +763,10 @@ __device__ __forceinline__ void store_players(const orx_state_t& st, uint32_t B,
   if (stairs) {
     st.st_x[i] = p1.sx;       st.st_x[B + i] = p2.sx;
     st.st_y[i] = p1.sy;       st.st_y[B + i] = p2.sy;
+    if constexpr (GRID) {
+      st.p_layout[i] = (int16_t)p1.lay;
+      st.p_layout[B + i] = (int16_t)p2.lay;
+    }
   }
 }
 
@@ -725,7 +810,7 @@ __device__ __forceinline__ void flush_deltas(const orx_state_t& st, uint32_t B, 
   }
 }
 
-__device__ __forceinline__ Cfg make_cfg(const orx_cfg_t& h) {
+__device__ __forceinline__ Cfg make_cfg(const orx_cfg_t& h, const orx_state_t& st) {
   Cfg c;
   c.W = h.width; c.H = h.height; c.despawn = h.despawn; c.max_ticks = h.max_ticks;
   c.start_mode = h.start_mode;
@@ -738,6 +823,11 @@ __device__ __forceinline__ Cfg make_cfg(const orx_cfg_t& h) {
   c.ground.set((h.width - 2) * (h.height - 2) - 1);
   c.stair_x.set(h.width - 3);
   c.stair_y.set(h.height - 3);
+  c.L = h.n_layouts;
+  c.layout.set(h.n_layouts > 0 ? h.n_layouts : 1);
+  c.tiles = st.bank_tiles;
+  c.gground = st.bank_ground;
+  c.gmeta = st.bank_meta;
   return c;
 }
 
@@ -752,19 +842,19 @@ __device__ __forceinline__ uint16_t pack_actions(int32_t a1, int32_t a2) {
 // ---------------------------------------------------------------------------
 // Kernels (NCAP = NPC slot capacity: 0, 8 or 16)
 // ---------------------------------------------------------------------------
-template <int NCAP>
+template <int NCAP, bool GRID>
 __global__ void __launch_bounds__(256) reset_kernel(orx_cfg_t hc, orx_state_t st,
                                                     const uint8_t* __restrict__ mask, uint32_t B,
                                                     Key key, uint32_t off) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= B) return;
   if (mask && !mask[i]) return;
-  const Cfg c = make_cfg(hc);
+  const Cfg c = make_cfg(hc, st);
   Player p1, p2;
   Npcs<NCAP> npc;
   int32_t tick, status;
-  setup_game(c, key, off + i, (uint32_t)st.episode[i], p1, p2, npc, tick, status);
-  store_players(st, B, i, p1, p2, true);
+  setup_game<NCAP, GRID>(c, key, off + i, (uint32_t)st.episode[i], p1, p2, npc, tick, status);
+  store_players<GRID>(st, B, i, p1, p2, true);
   st.tick[i] = tick;
   st.status[i] = status;
   if constexpr (NCAP > 0) {
@@ -773,7 +863,7 @@ __global__ void __launch_bounds__(256) reset_kernel(orx_cfg_t hc, orx_state_t st
   }
 }
 
-template <int NCAP, bool EV>
+template <int NCAP, bool EV, bool GRID>
 __global__ void __launch_bounds__(256) step_kernel(orx_cfg_t hc, orx_state_t st,
                                                    const int8_t* __restrict__ actions, uint32_t B,
                                                    Key key, uint32_t off,
@@ -781,7 +871,7 @@ __global__ void __launch_bounds__(256) step_kernel(orx_cfg_t hc, orx_state_t st,
                                                    int32_t* __restrict__ n_events) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= B) return;
-  const Cfg c = make_cfg(hc);
+  const Cfg c = make_cfg(hc, st);
   const uint32_t game = off + i;
   int32_t status = st.status[i];
   Npcs<NCAP> npc;
@@ -791,8 +881,8 @@ __global__ void __launch_bounds__(256) step_kernel(orx_cfg_t hc, orx_state_t st,
     if (!c.autoreset) return;
     const uint32_t ep = (uint32_t)st.episode[i] + 1u;
     int32_t tick;
-    setup_game(c, key, game, ep, p1, p2, npc, tick, status);
-    store_players(st, B, i, p1, p2, true);
+    setup_game<NCAP, GRID>(c, key, game, ep, p1, p2, npc, tick, status);
+    store_players<GRID>(st, B, i, p1, p2, true);
     st.tick[i] = tick;
     st.status[i] = status;
     st.episode[i] = (int32_t)ep;
@@ -812,15 +902,16 @@ __global__ void __launch_bounds__(256) step_kernel(orx_cfg_t hc, orx_state_t st,
   }
   const uint32_t ep = (uint32_t)st.episode[i];
   int32_t tick = st.tick[i];
-  load_players(st, B, i, p1, p2);
+  load_players<GRID>(st, B, i, p1, p2);
   load_npcs(st, c, B, i, npc);
   const NpcMem m{st.npc_pos, st.npc_health, B, i};
   Deltas dl = {0, 0, 0, 0, 0, 0};
   Events<EV> ev{EV ? events + (size_t)i * ORX_MAX_EVENTS * 4 : nullptr, 0};
   bool err = false;
   const bool p1_first = p1_first_draw(key, game, ep, tick, err);
-  tick_game(c, key, game, ep, p1_first, true, p1, p2, npc, m, tick, status, err, dl, ev);
-  store_players(st, B, i, p1, p2, dl.descend != 0);
+  tick_game<NCAP, EV, GRID>(c, key, game, ep, p1_first, true, p1, p2, npc, m, tick, status, err,
+                            dl, ev);
+  store_players<GRID>(st, B, i, p1, p2, dl.descend != 0);
   st.tick[i] = tick;
   st.status[i] = status;
   if (NCAP > 0 && dl.npc_death) st.npc_alive[i] = npc.alive;
@@ -900,7 +991,7 @@ __device__ __forceinline__ void store_traj(int32_t* obs, int8_t* act, int32_t t,
 
 // FAST: both players are RandomBots and obs/act are both given (compile-time,
 // the common case: no per-tick uniform branches on policy codes or pointers).
-template <int NCAP, bool FAST>
+template <int NCAP, bool FAST, bool GRID>
 __global__ void __launch_bounds__(256) rollout_kernel(orx_cfg_t hc, orx_state_t st, int32_t pol1_,
                                                       int32_t pol2_, int32_t n_ticks,
                                                       int32_t* __restrict__ obs,
@@ -910,10 +1001,10 @@ __global__ void __launch_bounds__(256) rollout_kernel(orx_cfg_t hc, orx_state_t 
   const int32_t pol2 = FAST ? (int32_t)ORX_POLICY_RANDOM : pol2_;
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= B) return;
-  const Cfg c = make_cfg(hc);
+  const Cfg c = make_cfg(hc, st);
   const uint32_t game = off + i;
   Player p1, p2;
-  load_players(st, B, i, p1, p2);
+  load_players<GRID>(st, B, i, p1, p2);
   int32_t tick = st.tick[i];
   int32_t status = st.status[i];
   uint32_t ep = (uint32_t)st.episode[i];
@@ -943,7 +1034,8 @@ __global__ void __launch_bounds__(256) rollout_kernel(orx_cfg_t hc, orx_state_t 
         p1.x ^= p1_first;
         status = (c.max_ticks && tick >= c.max_ticks) ? ORX_TIE : ORX_IN_PROGRESS;
       } else {
-        tick_game(c, key, game, ep, p1_first, true, p1, p2, npc, m, tick, status, err, dl, ev);
+        tick_game<NCAP, false, GRID>(c, key, game, ep, p1_first, true, p1, p2, npc, m, tick,
+                                     status, err, dl, ev);
       }
       stairs_dirty |= dl.descend != descents;
     } else if (c.autoreset) {
@@ -952,7 +1044,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(orx_cfg_t hc, orx_state_t 
         tick = kStartTick;
         status = ORX_IN_PROGRESS;
       } else {
-        setup_game(c, key, game, ep, p1, p2, npc, tick, status);
+        setup_game<NCAP, GRID>(c, key, game, ep, p1, p2, npc, tick, status);
         if constexpr (NCAP > 0) store_new_npcs(st, c, B, i, npc);
       }
       stairs_dirty = true;
@@ -960,7 +1052,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(orx_cfg_t hc, orx_state_t 
     }
     if (!(ORX_DIAG & 16)) store_traj<FAST>(obs, act, t, B, i, p1, p2, tick, status, a1, a2);
   }
-  store_players(st, B, i, p1, p2, stairs_dirty);
+  store_players<GRID>(st, B, i, p1, p2, stairs_dirty);
   st.tick[i] = tick;
   st.status[i] = status;
   st.episode[i] = (int32_t)ep;
@@ -1041,7 +1133,7 @@ __global__ void __launch_bounds__(128) rollout_pc_kernel(
   const uint32_t wave = threadIdx.x >> 6;  // wave-uniform role
   const uint32_t i = blockIdx.x * 64u + lane;
   const bool valid = i < B;                 // no early return: every wave runs every iteration
-  const Cfg c = make_cfg(hc);
+  const Cfg c = make_cfg(hc, st);
   const int need = (pol1 == ORX_POLICY_RANDOM) + (pol2 == ORX_POLICY_RANDOM);
   if (wave == 0) {
     rec_t[lane] = -1;
@@ -1153,21 +1245,27 @@ __global__ void __launch_bounds__(128) rollout_pc_kernel(
 
 // Staircases of arbitrary (game, episode, depth, generation) dungeons, for
 // materializing World.dungeons (compat views, wire codec).
-__global__ void __launch_bounds__(256) stairs_kernel(orx_cfg_t hc, const uint32_t* __restrict__ games,
+template <bool GRID>
+__global__ void __launch_bounds__(256) stairs_kernel(orx_cfg_t hc, orx_state_t st,
+                                                     const uint32_t* __restrict__ games,
                                                      const int32_t* __restrict__ episodes,
                                                      const int32_t* __restrict__ depths,
                                                      const int32_t* __restrict__ gens,
                                                      int32_t* __restrict__ sx,
-                                                     int32_t* __restrict__ sy, uint32_t n,
+                                                     int32_t* __restrict__ sy,
+                                                     int32_t* __restrict__ layout, uint32_t n,
                                                      Key key) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const Cfg c = make_cfg(hc);
+  const Cfg c = make_cfg(hc, st);
   bool err = false;
-  int32_t x, y;
-  dungeon_stair(c, key, games[i], (uint32_t)episodes[i], depths[i], (uint32_t)gens[i], x, y, err);
+  int32_t x, y, lay;
+  dungeon_stair<GRID>(c, key, games[i], (uint32_t)episodes[i], depths[i], (uint32_t)gens[i], x, y,
+                      lay,
+                      err);
   sx[i] = err ? -1 : x;
   sy[i] = err ? -1 : y;
+  if (layout) layout[i] = err ? -1 : lay;
 }
 
 // ---------------------------------------------------------------------------
@@ -1200,8 +1298,12 @@ int check_cfg(const orx_cfg_t* c) {
     return fail(ORX_EINVAL, "NPC positions pack 8+8 bits: W, H <= 256 when n_npcs > 0");
   if (c->n_npcs > 0 && (c->npc_health < 1 || c->npc_health > 127))
     return fail(ORX_EINVAL, "npc_health must be in [1, 127]");
+  if (c->n_layouts < 0 || c->n_layouts > 32767)
+    return fail(ORX_EINVAL, "n_layouts must be in [0, 32767]");
+  if (c->n_layouts > 0 && (int64_t)c->width * c->height > 65536)
+    return fail(ORX_EINVAL, "a dungeon bank needs W * H <= 65536 (u16 Ground lists)");
   const int64_t n_ground = (int64_t)(c->width - 2) * (c->height - 2) - 1;
-  if (n_ground < (int64_t)c->n_npcs + 2)
+  if (c->n_layouts == 0 && n_ground < (int64_t)c->n_npcs + 2)
     return fail(ORX_EINVAL, "board too small for the players and NPCs");
   if (c->player_health < 1) return fail(ORX_EINVAL, "player_health must be >= 1");
   if (c->autoreset != 0 && c->autoreset != 1) return fail(ORX_EINVAL, "autoreset must be 0 or 1");
@@ -1218,6 +1320,8 @@ int check_state(const orx_cfg_t* c, const orx_state_t* s, bool full) {
     return fail(ORX_EINVAL, "ret_sum / ep_count are NULL");
   if (c->n_npcs > 0 && (!s->npc_pos || !s->npc_health || !s->npc_alive))
     return fail(ORX_EINVAL, "n_npcs > 0 needs npc_pos, npc_health and npc_alive");
+  if (c->n_layouts > 0 && (!s->p_layout || !s->bank_tiles || !s->bank_ground || !s->bank_meta))
+    return fail(ORX_EINVAL, "n_layouts > 0 needs p_layout and the bank_* arrays");
   return ORX_OK;
 }
 
@@ -1290,17 +1394,15 @@ int orx_reset(const orx_cfg_t* cfg, const orx_state_t* st, const uint8_t* mask, 
   const uint32_t B = (uint32_t)n_games, off = (uint32_t)game_offset;
   const hipStream_t s = (hipStream_t)stream;
   const Key k = make_key(seed);
-  switch (ncap_for(cfg->n_npcs)) {
-    case 0:
-      hipLaunchKernelGGL(reset_kernel<0>, grid_for(B), dim3(kBlock), 0, s, *cfg, *st, mask, B, k, off);
-      break;
-    case 8:
-      hipLaunchKernelGGL(reset_kernel<8>, grid_for(B), dim3(kBlock), 0, s, *cfg, *st, mask, B, k, off);
-      break;
-    default:
-      hipLaunchKernelGGL(reset_kernel<16>, grid_for(B), dim3(kBlock), 0, s, *cfg, *st, mask, B, k, off);
-      break;
-  }
+  const int nc = ncap_for(cfg->n_npcs);
+  const bool grid = cfg->n_layouts > 0;
+#define ORX_RESET(N, G)                                                                         \
+  if (nc == N && grid == G)                                                                     \
+    hipLaunchKernelGGL((reset_kernel<N, G>), grid_for(B), dim3(kBlock), 0, s, *cfg, *st, mask, B, \
+                       k, off);
+  ORX_RESET(0, false) ORX_RESET(8, false) ORX_RESET(16, false)
+  ORX_RESET(0, true) ORX_RESET(8, true) ORX_RESET(16, true)
+#undef ORX_RESET
   return launch_status("orx_reset");
 }
 
@@ -1317,17 +1419,16 @@ static int launch_step(const orx_cfg_t* cfg, const orx_state_t* st, const int8_t
   const uint32_t B = (uint32_t)n_games, off = (uint32_t)game_offset;
   const hipStream_t s = (hipStream_t)stream;
   const Key k = make_key(seed);
-#define ORX_STEP(NC, E)                                                                       \
-  hipLaunchKernelGGL((step_kernel<NC, E>), grid_for(B), dim3(kBlock), 0, s, *cfg, *st, actions, \
-                     B, k, off, events, n_events)
-  switch (ncap_for(cfg->n_npcs) * 2 + (ev ? 1 : 0)) {
-    case 0: ORX_STEP(0, false); break;
-    case 1: ORX_STEP(0, true); break;
-    case 16: ORX_STEP(8, false); break;
-    case 17: ORX_STEP(8, true); break;
-    case 32: ORX_STEP(16, false); break;
-    default: ORX_STEP(16, true); break;
-  }
+  const int nc = ncap_for(cfg->n_npcs);
+  const bool grid = cfg->n_layouts > 0;
+#define ORX_STEP(NC, E, G)                                                                      \
+  if (nc == NC && ev == E && grid == G)                                                        \
+    hipLaunchKernelGGL((step_kernel<NC, E, G>), grid_for(B), dim3(kBlock), 0, s, *cfg, *st,     \
+                       actions, B, k, off, events, n_events);
+  ORX_STEP(0, false, false) ORX_STEP(0, true, false) ORX_STEP(8, false, false)
+  ORX_STEP(8, true, false) ORX_STEP(16, false, false) ORX_STEP(16, true, false)
+  ORX_STEP(0, false, true) ORX_STEP(0, true, true) ORX_STEP(8, false, true)
+  ORX_STEP(8, true, true) ORX_STEP(16, false, true) ORX_STEP(16, true, true)
 #undef ORX_STEP
   return launch_status(name);
 }
@@ -1378,39 +1479,65 @@ int orx_rollout(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p1, 
   const uint32_t B = (uint32_t)n_games, off = (uint32_t)game_offset;
   const hipStream_t s = (hipStream_t)stream;
   const Key k = make_key(seed);
-  // the buffer-addressed fast path needs one tick's obs rows below 2 GiB
-  const bool rr = policy_p1 == ORX_POLICY_RANDOM && policy_p2 == ORX_POLICY_RANDOM && obs && act &&
-                  (uint64_t)B * ORX_OBS_FIELDS * 4u < (1ull << 31);
-  const bool pc = use_pc_rollout(B);
+  // the buffer-addressed fast path needs one tick's obs rows below 2 GiB; a
+  // dungeon bank runs the generic plain kernel (tile lookups)
+  const bool grid = cfg->n_layouts > 0;
+  const bool rr = !grid && policy_p1 == ORX_POLICY_RANDOM && policy_p2 == ORX_POLICY_RANDOM &&
+                  obs && act && (uint64_t)B * ORX_OBS_FIELDS * 4u < (1ull << 31);
+  const bool pc = !grid && use_pc_rollout(B);
   const int nc = ncap_for(cfg->n_npcs);
-#define ORX_ROLLOUT(N, R)                                                                       \
-  if (nc == N && rr == R) {                                                                     \
+#define ORX_ROLLOUT(N, R, G)                                                                    \
+  if (nc == N && rr == R && grid == G) {                                                        \
     if (pc)                                                                                     \
-      hipLaunchKernelGGL((rollout_pc_kernel<N, R>), dim3((B + 63) / 64),                        \
-                         dim3(128), 0, s, *cfg, *st, policy_p1, policy_p2,                       \
-                         n_ticks, obs, act, B, k, off);                                          \
+      hipLaunchKernelGGL((rollout_pc_kernel<N, R>), dim3((B + 63) / 64), dim3(128), 0, s, *cfg, \
+                         *st, policy_p1, policy_p2, n_ticks, obs, act, B, k, off);              \
     else                                                                                        \
-      hipLaunchKernelGGL((rollout_kernel<N, R>), grid_for(B), dim3(kBlock), 0, s, *cfg, *st,    \
+      hipLaunchKernelGGL((rollout_kernel<N, R, G>), grid_for(B), dim3(kBlock), 0, s, *cfg, *st, \
                          policy_p1, policy_p2, n_ticks, obs, act, B, k, off);                   \
   }
-  ORX_ROLLOUT(0, false) ORX_ROLLOUT(0, true) ORX_ROLLOUT(8, false) ORX_ROLLOUT(8, true)
-  ORX_ROLLOUT(16, false) ORX_ROLLOUT(16, true)
+  ORX_ROLLOUT(0, false, false) ORX_ROLLOUT(0, true, false) ORX_ROLLOUT(8, false, false)
+  ORX_ROLLOUT(8, true, false) ORX_ROLLOUT(16, false, false) ORX_ROLLOUT(16, true, false)
+  ORX_ROLLOUT(0, false, true) ORX_ROLLOUT(8, false, true) ORX_ROLLOUT(16, false, true)
 #undef ORX_ROLLOUT
   return launch_status("orx_rollout");
 }
 
-int orx_dungeon_stairs(const orx_cfg_t* cfg, const uint32_t* game_ids, const int32_t* episodes,
-                       const int32_t* depths, const int32_t* gens, int32_t* sx, int32_t* sy,
-                       int64_t n, uint64_t seed, void* stream) {
+int orx_dungeon_spawn(const orx_cfg_t* cfg, const orx_state_t* st, const uint32_t* game_ids,
+                      const int32_t* episodes, const int32_t* depths, const int32_t* gens,
+                      int32_t* sx, int32_t* sy, int32_t* layout, int64_t n, uint64_t seed,
+                      void* stream) {
   int r;
   if ((r = check_cfg(cfg))) return r;
   if (n < 0 || n > 0x7FFFFFFFLL - kBlock) return fail(ORX_EINVAL, "bad n");
   if (n == 0) return ORX_OK;
   if (!game_ids || !episodes || !depths || !gens || !sx || !sy)
     return fail(ORX_EINVAL, "a pointer is NULL");
-  hipLaunchKernelGGL(stairs_kernel, grid_for(n), dim3(kBlock), 0, (hipStream_t)stream, *cfg,
-                     game_ids, episodes, depths, gens, sx, sy, (uint32_t)n, make_key(seed));
-  return launch_status("orx_dungeon_stairs");
+  orx_state_t bank{};
+  if (cfg->n_layouts > 0) {
+    if (!st || !st->bank_tiles || !st->bank_ground || !st->bank_meta)
+      return fail(ORX_EINVAL, "n_layouts > 0 needs the bank_* arrays");
+    bank.bank_tiles = st->bank_tiles;
+    bank.bank_ground = st->bank_ground;
+    bank.bank_meta = st->bank_meta;
+  }
+  if (cfg->n_layouts > 0)
+    hipLaunchKernelGGL(stairs_kernel<true>, grid_for(n), dim3(kBlock), 0, (hipStream_t)stream,
+                       *cfg, bank, game_ids, episodes, depths, gens, sx, sy, layout, (uint32_t)n,
+                       make_key(seed));
+  else
+    hipLaunchKernelGGL(stairs_kernel<false>, grid_for(n), dim3(kBlock), 0, (hipStream_t)stream,
+                       *cfg, bank, game_ids, episodes, depths, gens, sx, sy, layout, (uint32_t)n,
+                       make_key(seed));
+  return launch_status("orx_dungeon_spawn");
+}
+
+int orx_dungeon_stairs(const orx_cfg_t* cfg, const uint32_t* game_ids, const int32_t* episodes,
+                       const int32_t* depths, const int32_t* gens, int32_t* sx, int32_t* sy,
+                       int64_t n, uint64_t seed, void* stream) {
+  if (cfg && cfg->n_layouts > 0)
+    return fail(ORX_EINVAL, "a dungeon bank needs orx_dungeon_spawn");
+  return orx_dungeon_spawn(cfg, nullptr, game_ids, episodes, depths, gens, sx, sy, nullptr, n, seed,
+                           stream);
 }
 
 }  // extern "C"

@@ -21,6 +21,7 @@ from .enums import MAX_EVENTS, N_COUNTERS, OBS_FIELDS, Policy
 
 STATE_FIELDS = ("p_x", "p_y", "p_depth", "p_health", "st_x", "st_y", "tick", "status", "episode",
                 "ret_sum", "ep_count", "counters", "npc_pos", "npc_health", "npc_alive")
+BANK_FIELDS = ("p_layout", "bank_tiles", "bank_ground", "bank_meta")
 
 
 def _ptr(t: Optional[torch.Tensor]):
@@ -65,7 +66,24 @@ class BatchedEngine:
         self.npc_health = z(max(K, 1), B, dt=torch.int8)
         self.npc_alive = z(B)
         self.actions = torch.full((B, 2), 5, dtype=torch.int8, device=device)
-        self._st = _lib.OrxState(**{f: getattr(self, f).data_ptr() for f in STATE_FIELDS})
+        ptrs = {f: getattr(self, f).data_ptr() for f in STATE_FIELDS}
+        # explicit-grid dungeon generator (cfg.layouts): the bank and each
+        # player's layout index; all NULL for EmptyDungeonGenerator
+        self.bank = None
+        if cfg.layouts is not None:
+            from .dungeons import DungeonBank
+            bank = DungeonBank(cfg.layouts)
+            if (bank.width, bank.height) != (cfg.width, cfg.height):
+                raise ValueError("layouts must be [L, width, height]")
+            if bank.min_ground < K + 2:
+                raise ValueError("every layout needs Ground tiles for both players and the NPCs")
+            self.bank = bank
+            self.p_layout = z(2, B, dt=torch.int16)
+            self.bank_tiles = torch.from_numpy(bank.layouts.reshape(len(bank), -1)).to(device)
+            self.bank_ground = torch.from_numpy(bank.ground.view(np.int16)).to(device)
+            self.bank_meta = torch.from_numpy(bank.meta).to(device)
+            ptrs.update({f: getattr(self, f).data_ptr() for f in BANK_FIELDS})
+        self._st = _lib.OrxState(**ptrs)
         if reset:
             self.reset()
 
@@ -144,8 +162,11 @@ class BatchedEngine:
 
     # -- host views -----------------------------------------------------------
     def snapshot(self) -> dict:
-        """Copies the whole SoA state to numpy (synchronizes)."""
+        """Copies the whole SoA state to numpy (synchronizes); with a dungeon
+        bank also ``p_layout``."""
         out = {}
+        if self.bank is not None:
+            out["p_layout"] = self.p_layout.cpu().numpy()
         for f in STATE_FIELDS:
             a = getattr(self, f).cpu().numpy()
             if f == "npc_pos":
@@ -159,6 +180,8 @@ class BatchedEngine:
 
     def load_snapshot(self, snap: dict) -> None:
         """Writes host arrays (engine layout) into the device state."""
+        if self.bank is not None and "p_layout" in snap:
+            self.p_layout.copy_(torch.from_numpy(np.ascontiguousarray(snap["p_layout"], np.int16)))
         for f in STATE_FIELDS:
             if f not in snap:
                 continue
@@ -181,22 +204,24 @@ class BatchedEngine:
             dst.copy_(torch.from_numpy(a.reshape(dst.shape)))
 
     def dungeon_stairs(self, games, episodes, depths, gens) -> np.ndarray:
-        """Staircases of (local game, episode, depth, generation) dungeons via
-        orx_dungeon_stairs; returns int32 [n, 2]."""
+        """Staircase and layout of (local game, episode, depth, generation)
+        dungeons via orx_dungeon_spawn; returns int32 [n, 3] (sx, sy, layout;
+        layout -1 for EmptyDungeonGenerator)."""
         n = len(games)
         if n == 0:
-            return np.zeros((0, 2), np.int32)
+            return np.zeros((0, 3), np.int32)
         t = lambda a, dt: torch.as_tensor(np.asarray(a), dtype=dt).to(self.device).contiguous()
         g = t(np.asarray(games, np.int64) + self.game_offset, torch.int64).to(torch.int32)
         e, d, gn = t(episodes, torch.int32), t(depths, torch.int32), t(gens, torch.int32)
         sx = torch.empty(n, dtype=torch.int32, device=self.device)
         sy = torch.empty_like(sx)
+        lay = torch.empty_like(sx)
         with torch.cuda.device(self.device):
-            code = self.lib.orx_dungeon_stairs(ctypes.byref(self._ccfg), _ptr(g), _ptr(e), _ptr(d),
-                                               _ptr(gn), _ptr(sx), _ptr(sy), n, self.seed,
-                                               self._stream())
-        _lib.check("orx_dungeon_stairs", code)
-        return torch.stack([sx, sy], 1).cpu().numpy()
+            code = self.lib.orx_dungeon_spawn(ctypes.byref(self._ccfg), ctypes.byref(self._st),
+                                              _ptr(g), _ptr(e), _ptr(d), _ptr(gn), _ptr(sx),
+                                              _ptr(sy), _ptr(lay), n, self.seed, self._stream())
+        _lib.check("orx_dungeon_spawn", code)
+        return torch.stack([sx, sy, lay], 1).cpu().numpy()
 
     def game_states(self, indices=None, full_world: bool = True, snap: Optional[dict] = None):
         """Reference-schema views (compat.GameStateView) of the given games; with
@@ -216,9 +241,10 @@ class BatchedEngine:
             st = self.dungeon_stairs([r[0] for r in req],
                                      [int(snap["episode"][r[0]]) for r in req],
                                      [r[1] for r in req], [0] * len(req))
-            for (i, d), (x, y) in zip(req, st):
-                extra.setdefault(i, {})[d] = (int(x), int(y))
-        return [game_state(snap, i, self.cfg, extra.get(i, {}) if full_world else None)
+            for (i, d), (x, y, lay) in zip(req, st):
+                extra.setdefault(i, {})[d] = (int(x), int(y), int(lay))
+        return [game_state(snap, i, self.cfg, extra.get(i, {}) if full_world else None,
+                           bank=self.bank)
                 for i in idx]
 
     def episode_returns(self) -> torch.Tensor:

@@ -11,7 +11,9 @@ Construction mirrors the reference's plugins:
   dgen           EmptyDungeonGenerator(width, height) (worldgen.py:29-43): any
                  object with ``width``/``height`` whose class is named
                  ``EmptyDungeonGenerator`` (the only generator the reference
-                 has), or a ``(width, height)`` tuple.
+                 has), or a ``(width, height)`` tuple; or an explicit-grid
+                 generator, ``optimax_rogue_amd.dungeons.DungeonBank(layouts)``
+                 (the plugin API of worldgen.py:9-26 as a layout bank).
   despawn_strat  DungeonDespawningStrategy (updater.py:47-50); ValueError for
                  anything else (updater.py:257).
   max_ticks      None / 0 = no limit (updater.py:158).
@@ -30,13 +32,17 @@ from .enums import DungeonDespawningStrategy, Move, Policy, StartMode
 
 
 def _dims(dgen):
+    """(width, height, layouts or None) of a generator argument."""
+    from .dungeons import DungeonBank
     if isinstance(dgen, tuple):
-        return int(dgen[0]), int(dgen[1])
+        return int(dgen[0]), int(dgen[1]), None
+    if isinstance(dgen, DungeonBank):
+        return dgen.width, dgen.height, dgen.layouts
     name = type(dgen).__name__
     if name not in ("EmptyDungeonGenerator",):
         raise ValueError(f"unsupported DungeonGenerator {name}: the engine implements "
-                         "EmptyDungeonGenerator (worldgen.py:29-43)")
-    return int(dgen.width), int(dgen.height)
+                         "EmptyDungeonGenerator (worldgen.py:29-43) and DungeonBank layouts")
+    return int(dgen.width), int(dgen.height), None
 
 
 class BatchedUpdater:
@@ -46,9 +52,9 @@ class BatchedUpdater:
                  device: Optional[torch.device] = None, autoreset: bool = False):
         if int(despawn_strat) not in (1, 2):
             raise ValueError(f"Unknown despawn strat {despawn_strat}")
-        w, h = _dims(dgen)
+        w, h, layouts = _dims(dgen)
         cfg = EnvConfig(width=w, height=h, despawn=int(despawn_strat), max_ticks=max_ticks or 0,
-                        n_npcs=n_npcs, autoreset=int(autoreset))
+                        n_npcs=n_npcs, autoreset=int(autoreset), layouts=layouts)
         if game_start != "together":
             kind, d1, d2 = game_start
             if kind != "separated":
@@ -83,7 +89,7 @@ class BatchedUpdater:
     def game_state(self, i: int):
         """Game i in the reference GameState schema (compat.GameStateView)."""
         from .compat import game_state
-        return game_state(self.engine.snapshot(), i, self.engine.cfg)
+        return game_state(self.engine.snapshot(), i, self.engine.cfg, bank=self.engine.bank)
 
 
 class GameUpdater:
@@ -128,8 +134,10 @@ class GameUpdater:
         def dungeon_for(depth):
             for p in range(2):
                 if int(snap["p_depth"][p][0]) == depth:
+                    tiles = (eng.bank.tiles(int(snap["p_layout"][p][0]))
+                             if eng.bank is not None else None)
                     return DungeonView(cfg.width, cfg.height, int(snap["st_x"][p][0]),
-                                       int(snap["st_y"][p][0]))
+                                       int(snap["st_y"][p][0]), tiles=tiles)
             raise KeyError(depth)
 
         ups = from_events(rows, self.current_update_order,

@@ -19,7 +19,7 @@ LIB_PATH = os.path.join(HERE, "liborx_oracle.so")
 # Field order of orx_cfg_t (include/orx.h); tests check it against the header.
 CFG_FIELDS = ["width", "height", "despawn", "max_ticks", "start_mode", "p1_depth", "p2_depth",
               "n_npcs", "npc_health", "npc_damage", "npc_armor", "player_health",
-              "player_damage", "player_armor", "autoreset", "flags"]
+              "player_damage", "player_armor", "autoreset", "flags", "n_layouts"]
 
 
 class _Cfg(ctypes.Structure):
@@ -28,7 +28,8 @@ class _Cfg(ctypes.Structure):
 
 DEFAULT_CFG = dict(width=32, height=32, despawn=1, max_ticks=1000, start_mode=1, p1_depth=0,
                    p2_depth=0, n_npcs=0, npc_health=3, npc_damage=1, npc_armor=0,
-                   player_health=10, player_damage=2, player_armor=1, autoreset=1, flags=0)
+                   player_health=10, player_damage=2, player_armor=1, autoreset=1, flags=0,
+                   n_layouts=0)
 
 _lib = None
 
@@ -63,6 +64,8 @@ def lib():
         L.oracle_philox.argtypes = [vp, vp, vp]
         L.oracle_rollout.argtypes = [vp, i32, i32, i32, vp]
         L.oracle_set_rng.argtypes = [vp, u64, i64]
+        L.oracle_set_bank.argtypes = [vp, vp, i32]
+        L.oracle_export_layout.argtypes = [vp, vp]
         _lib = L
     return _lib
 
@@ -83,15 +86,23 @@ class Oracle:
     """B reference games on the CPU (same stream keys as the engine)."""
 
     def __init__(self, cfg: dict, n_games: int, seed: int, game_offset: int = 0,
-                 record_events: bool = False):
+                 record_events: bool = False, layouts=None):
+        """layouts: optional [L, W, H] Tile codes -- an explicit-grid dungeon
+        generator (spawn_dungeon picks randint(L)); None = EmptyDungeonGenerator."""
         full = dict(DEFAULT_CFG)
         full.update({k: v for k, v in cfg.items() if k in CFG_FIELDS})
+        full["n_layouts"] = 0 if layouts is None else len(layouts)
         self.cfg = full
         self.B = int(n_games)
         self.K = int(full["n_npcs"])
         self._c = _Cfg(**full)
         self._h = lib().oracle_new(ctypes.byref(self._c), self.B, int(seed), int(game_offset),
                                    int(record_events))
+        self.layouts = None
+        if layouts is not None:
+            self.layouts = np.ascontiguousarray(layouts, np.uint8)
+            assert self.layouts.shape[1:] == (full["width"], full["height"])
+            lib().oracle_set_bank(self._h, _ptr(self.layouts), len(self.layouts))
 
     def __del__(self):
         if getattr(self, "_h", None):
@@ -131,12 +142,17 @@ class Oracle:
                  "episode", "ret_sum", "ep_count", "counters", "npc_pos", "npc_health",
                  "npc_alive"]
         lib().oracle_export(self._h, *[_ptr(out[k]) for k in order])
+        if self.layouts is not None:
+            out["p_layout"] = np.zeros((2, B), np.int16)
+            lib().oracle_export_layout(self._h, _ptr(out["p_layout"]))
         return out
 
     def world(self, g: int):
-        buf = np.zeros((4096, 3), np.int32)
+        """World.dungeons as (depth, sx, sy) -- plus the layout index with a bank."""
+        buf = np.zeros((4096, 4), np.int32)
         n = lib().oracle_world(self._h, g, _ptr(buf), 4096)
-        return [tuple(int(v) for v in r) for r in buf[:n]]
+        w = 4 if self.layouts is not None else 3
+        return [tuple(int(v) for v in r[:w]) for r in buf[:n]]
 
     def events(self, g: int):
         buf = np.zeros((256, 4), np.int32)

@@ -19,6 +19,9 @@ int main(void) {
   if (orx_validate_cfg(&c) != ORX_EINVAL) { printf("bad cfg accepted\n"); return 3; }
   if (strlen(orx_last_error()) == 0) { printf("no error message\n"); return 4; }
   c.width = 64;
+  c.n_layouts = 40000; /* dungeon bank: at most 32767 layouts */
+  if (orx_validate_cfg(&c) != ORX_EINVAL) { printf("bad bank accepted\n"); return 8; }
+  c.n_layouts = 0;
   /* zero games: no device work, no pointers needed */
   if (orx_step(&c, NULL, NULL, 0, 1, 0, NULL) != ORX_OK) { printf("empty step failed\n"); return 5; }
   if (orx_rollout(&c, NULL, ORX_POLICY_RANDOM, ORX_POLICY_RANDOM, 5, NULL, NULL, 0, 1, 0, NULL) != ORX_OK) return 6;

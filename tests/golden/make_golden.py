@@ -28,6 +28,13 @@ output:
   ``EmptyDungeonGenerator`` (its plugin API, worldgen.py:9-43) that only selects
   the word stream (episode, depth, generation) before calling the reference's
   ``spawn_dungeon``.
+* Explicit-grid cases (``layouts``): ``KeyedBankGenerator``, a subclass of the
+  reference's ``DungeonGenerator`` (worldgen.py:9-26), returns the reference's
+  ``Dungeon(tiles)`` for layout ``np.random.randint(L)`` of a fixed bank --
+  the engine's dungeon-bank plugin; the reference's own ``is_blocked``,
+  ``get_random_unblocked``, ``staircase`` and ``handle_move`` then run on
+  walls, open borders and several staircases.  The bank is saved with the
+  fixture.
 * NPCs ("enemies") come from ``NpcGameStart``, a ``GameStartGenerator``
   (worldgen.py:47-58) that calls the reference's Together/Separated
   ``setup_game`` and then places K NPCs with the reference's
@@ -216,7 +223,28 @@ class Harness:
                                                      self.dmg, self.arm, [], dict()))
                 return gs
 
-        self.dgen = KeyedDungeonGenerator(cfg["width"], cfg["height"])
+        class KeyedBankGenerator(R_.worldgen.DungeonGenerator):
+            def __init__(self, width, height, layouts):
+                super().__init__(width, height)
+                self.layouts = layouts
+
+            def spawn_dungeon(self, depth):
+                gen = harness.gens.get(depth, 0)
+                harness.gens[depth] = gen + 1
+                saved = R_.nprand.stream
+                R_.nprand.stream = Stream(harness.seed, harness.gid, harness.episode, depth,
+                                          PUR_DUNGEON, gen)
+                try:
+                    idx = R_.worldgen.np.random.randint(len(self.layouts))
+                finally:
+                    R_.nprand.stream = saved
+                return R_.world.Dungeon(self.layouts[idx].astype(np.int32))
+
+        self.layouts = cfg.get("layouts")
+        if self.layouts is not None:
+            self.dgen = KeyedBankGenerator(cfg["width"], cfg["height"], self.layouts)
+        else:
+            self.dgen = KeyedDungeonGenerator(cfg["width"], cfg["height"])
         if cfg["start_mode"] == 2:
             inner = R.worldgen.SeparatedGameStartGenerator(self.dgen, cfg["p1_depth"],
                                                            cfg["p2_depth"])
@@ -329,9 +357,40 @@ class Harness:
         rec["npc_pos"] = pos
         rec["npc_health"] = hp
         rec["npc_alive"] = alive
-        rec["world"] = [(d, *gs.world.dungeons[d].staircase()) for d in gs.world.dungeons]
+        if self.layouts is None:
+            rec["world"] = [(d, *gs.world.dungeons[d].staircase()) for d in gs.world.dungeons]
+        else:
+            lay = lambda dung: next(i for i, t in enumerate(self.layouts)
+                                    if np.array_equal(dung.tiles, t))
+            rec["world"] = [(d, *gs.world.dungeons[d].staircase(), lay(gs.world.dungeons[d]))
+                            for d in gs.world.dungeons]
+            rec["p_layout"] = [lay(gs.world.get_at_depth(e.depth)) for e in p]
         rec["entities"] = [(e.iden, e.depth, e.x, e.y, e.health) for e in gs.entities]
         return rec
+
+
+def make_layouts(W, H, L, seed, n_stairs=(1,), open_border=False, wall_p=0.18):
+    """A deterministic bank of L layouts (Tile codes, [L, W, H]): border walls
+    (with gaps when open_border), random interior walls, n_stairs[l] staircases."""
+    rs = np.random.RandomState(seed)
+    out = []
+    for li in range(L):
+        t = np.ones((W, H), np.uint8)
+        t[[0, -1], :] = 2
+        t[:, [0, -1]] = 2
+        if open_border and li % 2 == 0:  # Ground on the edge: moving off it is out of bounds
+            t[0, 1:H - 1] = 1
+            t[1:W - 1, H - 1] = 1
+        inner = rs.rand(W, H) < wall_p
+        inner[[0, -1], :] = False
+        inner[:, [0, -1]] = False
+        t[inner] = 2
+        ground = np.argwhere(t == 1)
+        pick = rs.choice(len(ground), n_stairs[li % len(n_stairs)], replace=False)
+        for j in pick:
+            t[tuple(ground[j])] = 3
+        out.append(t)
+    return np.stack(out)
 
 
 DEFAULT_CFG = dict(width=32, height=32, despawn=1, max_ticks=1000, start_mode=1, p1_depth=0,
@@ -370,6 +429,20 @@ CASES = {
     # non-square, game_offset != 0, seed > 2^32
     "offset_seed": dict(cfg=dict(width=9, height=5, max_ticks=80, n_npcs=2), seed=(7 << 32) | 11,
                         games=8, ticks=200, offset=1000),
+    # explicit-grid dungeon bank: interior walls, open borders, NPCs, random play
+    "bank_random_npc": dict(cfg=dict(width=9, height=8, max_ticks=90, n_npcs=3,
+                                     layouts=make_layouts(9, 8, 4, 101, open_border=True)),
+                            seed=12, games=16, ticks=300),
+    # bank + StaircaseBot deep play under Unused (regenerated layouts), 2-3 staircases
+    "bank_stairs_unused": dict(cfg=dict(width=8, height=9, max_ticks=150, despawn=2,
+                                        policy=(2, 1), n_npcs=2,
+                                        layouts=make_layouts(8, 9, 3, 102, n_stairs=(1, 3, 2))),
+                               seed=13, games=16, ticks=320),
+    # a one-layout bank (no dungeon draw), Separated start, both StaircaseBots
+    "bank_single_separated": dict(cfg=dict(width=7, height=7, max_ticks=100, start_mode=2,
+                                           p1_depth=1, p2_depth=0, policy=(2, 2),
+                                           layouts=make_layouts(7, 7, 1, 103, n_stairs=(2,))),
+                                  seed=14, games=12, ticks=260),
 }
 
 SNAP_KEYS_I32 = ["p_x", "p_y", "p_depth", "p_health", "st_x", "st_y", "tick", "status",
@@ -383,7 +456,9 @@ def run_case(R, name, spec):
     seed, G, T = spec["seed"], spec["games"], spec["ticks"]
     off = spec.get("offset", 0)
     hs = [Harness(R, cfg, seed, off + g) for g in range(G)]
-    snaps = {k: [] for k in SNAP_KEYS_I32}
+    bank = cfg.get("layouts")
+    keys = SNAP_KEYS_I32 + (["p_layout"] if bank is not None else [])
+    snaps = {k: [] for k in keys}
     actions = np.zeros((T, G, 2), np.int8)
     world_len = np.zeros((T + 1, G), np.int32)
     world = []
@@ -394,7 +469,7 @@ def run_case(R, name, spec):
 
     def record(t):
         recs = [h.snapshot() for h in hs]
-        for k in SNAP_KEYS_I32:
+        for k in keys:
             snaps[k].append([r[k] for r in recs])
         for g, r in enumerate(recs):
             world_len[t, g] = len(r["world"])
@@ -426,19 +501,24 @@ def run_case(R, name, spec):
         record(t + 1)
         record_ser(t + 1)
 
-    out = {"cfg_json": np.frombuffer(json.dumps(cfg).encode(), np.uint8),
+    cfg_js = {k: v for k, v in cfg.items() if k != "layouts"}
+    cfg_js["n_layouts"] = 0 if bank is None else int(len(bank))
+    out = {"cfg_json": np.frombuffer(json.dumps(cfg_js).encode(), np.uint8),
            "seed": np.array([seed], np.uint64), "game_offset": np.array([off], np.int64),
            "actions": actions, "world_len": world_len,
-           "world": np.array(world, np.int32).reshape(-1, 3),
+           "world": np.array(world, np.int32).reshape(-1, 3 if bank is None else 4),
            "event_len": ev_len, "events": np.array(events, np.int32).reshape(-1, 4),
            "entity_len": ent_len, "entities": np.array(ents, np.int32).reshape(-1, 5),
            "ser_ticks": np.array(ser_ticks, np.int32), "ser_len": ser_len,
            "ser_bytes": np.frombuffer(b"".join(ser_blobs), np.uint8)}
-    for k in SNAP_KEYS_I32:
+    if bank is not None:
+        out["layouts"] = np.ascontiguousarray(bank, np.uint8)
+    for k in keys:
         a = np.array(snaps[k])
         if a.ndim == 3:  # [T+1, G, F] -> [T+1, F, G] (engine SoA layout)
             a = a.transpose(0, 2, 1)
-        dt = {"npc_pos": np.uint16, "npc_health": np.int8, "npc_alive": np.uint32}.get(k, np.int32)
+        dt = {"npc_pos": np.uint16, "npc_health": np.int8, "npc_alive": np.uint32,
+              "p_layout": np.int16}.get(k, np.int32)
         out[k] = np.ascontiguousarray(a.astype(dt))
     path = os.path.join(HERE, f"{name}.npz")
     np.savez_compressed(path, **out)

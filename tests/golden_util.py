@@ -34,6 +34,8 @@ class Fixture:
         self.T, self.G = self.actions.shape[:2]
         self.K = int(self.cfg["n_npcs"])
         self.policy = tuple(self.cfg["policy"])
+        # explicit-grid cases: the dungeon bank ([L, W, H] Tile codes), else None
+        self.layouts = self.z.get("layouts")
         wl = self.z["world_len"]
         self._world_off = np.concatenate([[0], np.cumsum(wl.ravel())])
         el = self.z["event_len"]
@@ -51,7 +53,10 @@ class Fixture:
 
     def state(self, t: int) -> dict:
         """Engine-layout state after t steps (t = 0: after the initial reset)."""
-        return {k: self.z[k][t] for k in STATE_KEYS}
+        out = {k: self.z[k][t] for k in STATE_KEYS}
+        if "p_layout" in self.z:
+            out["p_layout"] = self.z["p_layout"][t]
+        return out
 
     def world(self, t: int, g: int):
         i = t * self.G + g
@@ -71,8 +76,10 @@ class Fixture:
 
 
 def compare_state(got: dict, want: dict, K: int, where: str = ""):
-    """Asserts bit-exact equality of every state field (NPC slots only if K)."""
-    for k in STATE_KEYS:
+    """Asserts bit-exact equality of every state field (NPC slots only if K;
+    the bank layout of each player's depth when both sides carry it)."""
+    keys = STATE_KEYS + (["p_layout"] if "p_layout" in got and "p_layout" in want else [])
+    for k in keys:
         if k.startswith("npc") and K == 0:
             continue
         g = np.asarray(got[k])

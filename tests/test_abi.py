@@ -38,7 +38,7 @@ def test_library_exports_every_declared_symbol(lib):
     decl = declared_functions()
     assert decl == sorted(["orx_abi_version", "orx_last_error", "orx_validate_cfg", "orx_reset",
                            "orx_step", "orx_step_events", "orx_policy", "orx_rollout",
-                           "orx_dungeon_stairs"])
+                           "orx_dungeon_stairs", "orx_dungeon_spawn"])
     from optimax_rogue_amd import _lib
     assert sorted(_lib.EXPORTS) == decl
     for name in decl:
@@ -86,6 +86,12 @@ def test_validate_cfg(lib):
            EnvConfig(n_npcs=17), EnvConfig(n_npcs=2, width=300), EnvConfig(max_ticks=-1),
            EnvConfig(width=4, height=4, n_npcs=2), EnvConfig(flags=1),
            EnvConfig(n_npcs=1, npc_health=0)]
+    # dungeon bank: n_layouts rides in the struct (the layouts themselves are
+    # validated by DungeonBank on the host)
+    import numpy as np
+    lay = np.ones((2, 300, 300), np.uint8)
+    bad.append(EnvConfig(width=300, height=300, layouts=lay))          # W*H > 65536
+    ok.append(EnvConfig(width=6, height=5, layouts=np.ones((3, 6, 5), np.uint8)))
     for c in ok:
         assert lib.orx_validate_cfg(ctypes.byref(c.to_c())) == 0, c
     for c in bad:
@@ -101,7 +107,7 @@ def test_plain_c_consumer(lib, tmp_path):
                     "-Wl,-rpath," + os.path.join(ROOT, "optimax_rogue_amd")], check=True)
     r = subprocess.run([str(exe)], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert "sizeof(orx_cfg_t)=64" in r.stdout
+    assert "sizeof(orx_cfg_t)=68" in r.stdout
 
 
 def test_engine_refuses_cpu():

@@ -86,7 +86,10 @@ def oracle_view(o, g, cfg):
     """GameStateView from the oracle's own world dict (exact insertion order)
     and entity list."""
     from optimax_rogue_amd.compat import DungeonView, EntityView, GameStateView, WorldView
-    dungeons = {d: DungeonView(cfg.width, cfg.height, sx, sy) for d, sx, sy in o.world(g)}
+    dungeons = {}
+    for w in o.world(g):   # (depth, sx, sy[, bank layout])
+        tiles = o.layouts[w[3]] if len(w) > 3 else None
+        dungeons[w[0]] = DungeonView(cfg.width, cfg.height, w[1], w[2], tiles=tiles)
     ents = []
     for iden, depth, x, y, hp, dmg, arm in o.entities(g):
         base = cfg.player_health if iden <= 2 else cfg.npc_health
@@ -100,8 +103,8 @@ def test_wire_codec_matches_reference_bytes(oracle_lib, name):
     and entity encodings) equal the reference's bytes at the sampled ticks."""
     from golden_util import Fixture
     fx = Fixture(name)
-    cfg = EnvConfig.from_dict(fx.cfg)
-    o = oracle_lib.Oracle(fx.cfg, fx.G, fx.seed, fx.game_offset)
+    cfg = EnvConfig.from_dict(fx.cfg, layouts=fx.layouts)
+    o = oracle_lib.Oracle(fx.cfg, fx.G, fx.seed, fx.game_offset, layouts=fx.layouts)
     o.reset(episode=np.zeros(fx.G, np.int32))
     ticks = set(int(t) for t in fx.z["ser_ticks"])
     for t in range(fx.T + 1):
@@ -129,3 +132,50 @@ def test_world_depths_rule(oracle_lib):
                     assert got == want, (name, t, g)
                 else:
                     assert sorted(got) == sorted(want), (name, t, g)
+
+
+def test_dungeon_bank_tables():
+    """DungeonBank's precomputed tables equal the reference Dungeon methods'
+    results: Ground list = get_random_unblocked's candidates (x-major flat
+    order, world.py:57-66), staircase = first StaircaseDown (world.py:52-55)."""
+    from golden_util import Fixture
+    from optimax_rogue_amd import DungeonBank
+    fx = Fixture("bank_stairs_unused")
+    bank = DungeonBank(fx.layouts)
+    L, W, H = fx.layouts.shape
+    for li in range(L):
+        t = fx.layouts[li].astype(np.int32)
+        avail = t == 1
+        want = np.arange(W * H).reshape(W, H)[avail]
+        n = int(bank.meta[li, 0])
+        assert n == len(want) and np.array_equal(bank.ground[li, :n], want)
+        assert bank.staircase(li) == tuple(int(v) for v in np.argwhere(t == 3)[0])
+    with pytest.raises(ValueError):
+        DungeonBank(np.ones((1, 5, 5), np.uint8))          # no staircase
+    with pytest.raises(ValueError):
+        DungeonBank(np.full((1, 5, 5), 7, np.uint8))       # not a Tile code
+
+
+def test_reference_staircasebot_on_bank_views(oracle_lib):
+    """The reference's StaircaseBot on views of an explicit-grid game walks
+    to the bank layout's first staircase, as the oracle's policy does."""
+    R = _ref_bots()
+    from golden_util import Fixture
+    fx = Fixture("bank_single_separated")
+    from optimax_rogue_amd import DungeonBank
+    bank = DungeonBank(fx.layouts)
+    cfg = EnvConfig.from_dict(fx.cfg, layouts=fx.layouts)
+    B = fx.G
+    o = oracle_lib.Oracle(fx.cfg, B, fx.seed, 0, layouts=fx.layouts)
+    o.reset()
+    bots = [[R.staircasebot.StaircaseBot(1 + p) for _ in range(B)] for p in range(2)]
+    for t in range(40):
+        snap = o.export()
+        want = o.policy(2, 2)
+        got = np.zeros_like(want)
+        for i in range(B):
+            gs = game_state(snap, i, cfg, bank=bank)
+            for p in range(2):
+                got[i, p] = int(bots[p][i].move(gs.view_for(gs.iden_lookup[1 + p])))
+        assert np.array_equal(got, want), t
+        o.step(want)

@@ -83,10 +83,10 @@ def test_engine_game_states_codec(name, oracle_lib):
     from optimax_rogue_amd.engine import BatchedEngine
     from test_compat import oracle_view
     fx = Fixture(name)
-    cfg = EnvConfig.from_dict(fx.cfg)
+    cfg = EnvConfig.from_dict(fx.cfg, layouts=fx.layouts)
     eng = BatchedEngine(cfg, fx.G, seed=fx.seed, game_offset=fx.game_offset,
                         device=torch.device("cuda", 0))
-    o = oracle_lib.Oracle(fx.cfg, fx.G, fx.seed, fx.game_offset)
+    o = oracle_lib.Oracle(fx.cfg, fx.G, fx.seed, fx.game_offset, layouts=fx.layouts)
     o.reset(episode=np.zeros(fx.G, np.int32))
     exact = cfg.start_mode == 1 and cfg.despawn == 1
     ticks = set(int(t) for t in fx.z["ser_ticks"])
@@ -118,7 +118,8 @@ def _as_record(u):
 
 @pytest.mark.parametrize("name,g", [("small_npc_random", 0), ("small_npc_random", 5),
                                     ("stairs_unreachable", 2), ("duel_5", 1),
-                                    ("separated_unused", 3)])
+                                    ("separated_unused", 3), ("bank_random_npc", 4),
+                                    ("bank_stairs_unused", 1)])
 def test_game_updater_drop_in(name, g):
     """GameUpdater.update(gs, m1, m2) -> (UpdateResult, updates) over one
     fixture game: the returned updates equal the reference's, applying them
@@ -127,10 +128,12 @@ def test_game_updater_drop_in(name, g):
     from golden_util import Fixture
     from optimax_rogue_amd import DungeonDespawningStrategy, UpdateResult
     from optimax_rogue_amd.updater import GameUpdater
+    from optimax_rogue_amd import DungeonBank
     fx = Fixture(name)
     c = fx.cfg
     start = "together" if c["start_mode"] == 1 else ("separated", c["p1_depth"], c["p2_depth"])
-    upd = GameUpdater((c["width"], c["height"]), DungeonDespawningStrategy(c["despawn"]),
+    dgen = (c["width"], c["height"]) if fx.layouts is None else DungeonBank(fx.layouts)
+    upd = GameUpdater(dgen, DungeonDespawningStrategy(c["despawn"]),
                       c["max_ticks"] or None, seed=fx.seed, game_id=fx.game_offset + g,
                       game_start=start, n_npcs=c["n_npcs"], device=torch.device("cuda", 0))
     gs = upd.setup_game()

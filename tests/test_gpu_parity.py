@@ -8,12 +8,12 @@ from golden_util import STATE_KEYS, Fixture, case_names, compare_state
 pytestmark = pytest.mark.gpu
 
 
-def _engine(cfg, n_games, seed, offset=0, reset=True):
+def _engine(cfg, n_games, seed, offset=0, reset=True, layouts=None):
     import torch
     from optimax_rogue_amd import EnvConfig
     from optimax_rogue_amd.engine import BatchedEngine
-    return BatchedEngine(EnvConfig.from_dict(cfg), n_games, seed=seed, game_offset=offset,
-                         device=torch.device("cuda", 0), reset=reset)
+    return BatchedEngine(EnvConfig.from_dict(cfg, layouts=layouts), n_games, seed=seed,
+                         game_offset=offset, device=torch.device("cuda", 0), reset=reset)
 
 
 @pytest.mark.parametrize("name", case_names())
@@ -21,7 +21,7 @@ def test_golden_step_by_step(name):
     """policy kernel + step kernel, tick by tick, vs the reference fixtures."""
     import torch
     fx = Fixture(name)
-    eng = _engine(fx.cfg, fx.G, fx.seed, fx.game_offset)
+    eng = _engine(fx.cfg, fx.G, fx.seed, fx.game_offset, layouts=fx.layouts)
     compare_state(eng.snapshot(), fx.state(0), fx.K, f"{name} reset")
     for t in range(fx.T):
         a = eng.policy(*fx.policy)
@@ -38,7 +38,7 @@ def test_golden_update_events(name):
     equal the GameStateUpdate list the reference returned."""
     import torch
     fx = Fixture(name)
-    eng = _engine(fx.cfg, fx.G, fx.seed, fx.game_offset)
+    eng = _engine(fx.cfg, fx.G, fx.seed, fx.game_offset, layouts=fx.layouts)
     acts = torch.from_numpy(fx.actions).to(eng.device)
     for t in range(fx.T):
         _, ev, n = eng.step(acts[t].contiguous(), events=True)
@@ -54,7 +54,7 @@ def test_golden_step_given_actions(name):
     """step kernel driven by the fixture's recorded actions (uploaded once)."""
     import torch
     fx = Fixture(name)
-    eng = _engine(fx.cfg, fx.G, fx.seed, fx.game_offset)
+    eng = _engine(fx.cfg, fx.G, fx.seed, fx.game_offset, layouts=fx.layouts)
     acts = torch.from_numpy(fx.actions).to(eng.device)
     for t in range(fx.T):
         eng.step(acts[t].contiguous())
@@ -67,7 +67,7 @@ def test_golden_rollout(name):
     import torch
     from optimax_rogue_amd.enums import OBS_FIELDS
     fx = Fixture(name)
-    eng = _engine(fx.cfg, fx.G, fx.seed, fx.game_offset)
+    eng = _engine(fx.cfg, fx.G, fx.seed, fx.game_offset, layouts=fx.layouts)
     # split in two launches to exercise state hand-over between launches
     t1 = fx.T // 3
     obs = torch.zeros((fx.T, len(OBS_FIELDS), fx.G), dtype=torch.int32, device=eng.device)
@@ -86,6 +86,28 @@ def test_golden_rollout(name):
     compare_state(eng.snapshot(), fx.state(fx.T), fx.K, f"{name} final")
 
 
+def _bank(W, H, L, seed, stairs=(1,)):
+    """Explicit-grid layouts for the large oracle cases (walls ~20%, open edges
+    on even layouts, n staircases)."""
+    rs = np.random.RandomState(seed)
+    out = []
+    for li in range(L):
+        t = np.ones((W, H), np.uint8)
+        t[[0, -1], :] = 2
+        t[:, [0, -1]] = 2
+        if li % 2 == 0:
+            t[0, 1:H - 1] = 1
+        inner = rs.rand(W, H) < 0.2
+        inner[[0, -1], :] = False
+        inner[:, [0, -1]] = False
+        t[inner] = 2
+        g = np.argwhere(t == 1)
+        for j in rs.choice(len(g), stairs[li % len(stairs)], replace=False):
+            t[tuple(g[j])] = 3
+        out.append(t)
+    return np.stack(out)
+
+
 ORACLE_CASES = {
     "c2_random_32": (dict(width=32, height=32), (1, 1), 4096, 400, 2),
     "npc_small_unused": (dict(width=7, height=6, n_npcs=5, despawn=2, max_ticks=90), (1, 2),
@@ -96,7 +118,12 @@ ORACLE_CASES = {
     "c5_stairs_128": (dict(width=128, height=128), (2, 2), 1024, 600, 5),
     "npc16_8x8": (dict(width=8, height=8, n_npcs=16, npc_health=2, max_ticks=50), (1, 1), 2048,
                   200, 14),
+    # explicit-grid dungeon bank (16 layouts), NPCs, both bots, both despawn rules
+    "bank_64_npc": (dict(width=64, height=64, n_npcs=8, max_ticks=300), (1, 1), 2048, 400, 15),
+    "bank_stairs_unused": (dict(width=12, height=10, n_npcs=2, max_ticks=200, despawn=2), (2, 1),
+                           2048, 400, 16),
 }
+ORACLE_BANKS = {"bank_64_npc": (64, 64, 16, 21, (1,)), "bank_stairs_unused": (12, 10, 5, 22, (1, 3))}
 
 
 @pytest.mark.parametrize("name", sorted(ORACLE_CASES))
@@ -104,10 +131,11 @@ def test_vs_oracle_large(name, oracle_lib):
     """thousands of games: engine (policy+step and rollout) vs the C oracle."""
     import torch
     cfg, pol, B, T, seed = ORACLE_CASES[name]
-    ora = oracle_lib.Oracle(cfg, B, seed, 0)
+    lay = _bank(*ORACLE_BANKS[name]) if name in ORACLE_BANKS else None
+    ora = oracle_lib.Oracle(cfg, B, seed, 0, layouts=lay)
     ora.reset(episode=np.zeros(B, np.int32))
-    eng = _engine(cfg, B, seed)
-    eng2 = _engine(cfg, B, seed)
+    eng = _engine(cfg, B, seed, layouts=lay)
+    eng2 = _engine(cfg, B, seed, layouts=lay)
     compare_state(eng.snapshot(), ora.export(), ora.K, f"{name} reset")
     chunk = T // 4
     for c in range(4):

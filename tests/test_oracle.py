@@ -23,9 +23,12 @@ def test_oracle_vs_reference_fixture(oracle_lib, name):
     """Every tick: SoA state, World.dungeons dict, update events (type and
     order) and GameState.entities order match the reference."""
     fx = Fixture(name)
-    o = oracle_lib.Oracle(fx.cfg, fx.G, fx.seed, fx.game_offset, record_events=True)
+    o = oracle_lib.Oracle(fx.cfg, fx.G, fx.seed, fx.game_offset, record_events=True,
+                          layouts=fx.layouts)
     o.reset(episode=np.zeros(fx.G, np.int32))
     compare_state(o.export(), fx.state(0), fx.K, f"{name} t=0")
+    if fx.layouts is not None:
+        assert "p_layout" in o.export()
     for t in range(fx.T):
         a = o.policy(*fx.policy)
         assert np.array_equal(a, fx.actions[t]), f"{name} policy t={t}"

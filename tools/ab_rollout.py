@@ -19,16 +19,21 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def child(arg, large):
     lib, *envs = arg.split("@")
     with_obs = True
+    abi = None
     for env in envs:
         k, _, v = env.partition("=")
         if k == "OBS":          # OBS=0: no trajectory output
             with_obs = v != "0"
+        elif k == "ABI":        # ABI=n: accept an older library build (same call shapes)
+            abi = int(v)
         else:
             os.environ[k] = v
     sys.path.insert(0, ROOT)
     import torch
     from optimax_rogue_amd import _lib, EnvConfig
     _lib.LIB_PATH = os.path.abspath(lib)
+    if abi is not None:
+        _lib.ABI_VERSION = abi
     from optimax_rogue_amd.engine import BatchedEngine
     from optimax_rogue_amd.enums import OBS_FIELDS
     dev = torch.device("cuda", 0)
