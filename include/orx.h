@@ -76,6 +76,17 @@ extern "C" {
 #define ORX_POLICY_STAIRCASE 2 /* StaircaseBot.move staircasebot.py:9-21       */
 #define ORX_POLICY_STAY 3      /* always Move.Stay                            */
 
+/* build extensions (orx_cfg_t.flags): mechanics the reference's readme
+ * describes but its code does not implement (readme.md:44-48); off = parity.
+ * No reference output pins them ("parity unpinned").        */
+#define ORX_EXT_SEPARATION_DAMAGE 1 /* "if the agents are on separate levels
+   the agent further behind begins taking damage that scales linearly with
+   time since separation": at the end of the k-th consecutive separated
+   tick the shallower player loses ceil(k / sep_period) health            */
+#define ORX_EXT_RANDOM_DOUBLE_DEATH 2 /* "If both agents die during the same
+   tick then one wins at random": one word of stream purpose 6 (c2 = tick)
+   instead of Tie; top bit 0 = Player1Win                                  */
+
 /* per-game event counters (rows of orx_state_t.counters)                    */
 #define ORX_CNT_COMBAT 0        /* handle_combat calls       updater.py:298  */
 #define ORX_CNT_DESCEND 1       /* player descents           updater.py:259  */
@@ -93,6 +104,8 @@ extern "C" {
 #define ORX_EV_DEATH 2
 #define ORX_EV_POSITION 3
 #define ORX_EV_DUNGEON 4
+#define ORX_EV_HEALTH 5  /* {5, iden, amount, 0}  EntityHealthUpdate updates.py:222-253
+                            (separation damage, ORX_EXT_SEPARATION_DAMAGE)   */
 #define ORX_MAX_EVENTS 8 /* per game per tick (at most 6 occur)            */
 
 #define ORX_MAX_NPCS 16 /* NPCs per game (alive mask is 32-bit; registers)  */
@@ -137,12 +150,13 @@ typedef struct orx_cfg {
   int32_t player_damage;  /* 2  */
   int32_t player_armor;   /* 1  */
   int32_t autoreset;      /* 1: a finished game is reset by the next step    */
-  int32_t flags;          /* extension flags; 0 = reference parity           */
+  int32_t flags;          /* ORX_EXT_* build extensions; 0 = reference parity */
   int32_t n_layouts;      /* dungeon generator: 0 = EmptyDungeonGenerator
                              (closed forms, worldgen.py:28-44); L > 0 = a
                              layout bank: spawn_dungeon(depth) returns layout
                              randint(L) of orx_state_t.bank_* (an explicit-
                              grid DungeonGenerator plugin, worldgen.py:9-26) */
+  int32_t sep_period;     /* ORX_EXT_SEPARATION_DAMAGE: ticks per +1 damage   */
 } orx_cfg_t;
 
 /* ---- batch state (SoA, batch axis contiguous; all device pointers) ------- */
@@ -174,6 +188,9 @@ typedef struct orx_state {
   const int32_t* bank_meta;     /* [L][4] {n_ground, staircase x, staircase y,
                                    0}: first StaircaseDown in x-major order
                                    (Dungeon.staircase, world.py:52-55)       */
+  int32_t* sep_start;           /* [B] ORX_EXT_SEPARATION_DAMAGE: tick the
+                                   current separation began, -1 = together
+                                   (NULL when the extension is off)          */
 } orx_state_t;
 
 /* ---- entry points --------------------------------------------------------- */

@@ -21,7 +21,7 @@ class OrxState(ctypes.Structure):
     _fields_ = [(n, ctypes.c_void_p) for n in (
         "p_x", "p_y", "p_depth", "p_health", "st_x", "st_y", "tick", "status", "episode",
         "ret_sum", "ep_count", "counters", "npc_pos", "npc_health", "npc_alive",
-        "p_layout", "bank_tiles", "bank_ground", "bank_meta")]
+        "p_layout", "bank_tiles", "bank_ground", "bank_meta", "sep_start")]
 
 
 class OrxError(RuntimeError):

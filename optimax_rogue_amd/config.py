@@ -22,7 +22,7 @@ from .enums import DungeonDespawningStrategy, StartMode
 
 CFG_FIELDS = ("width", "height", "despawn", "max_ticks", "start_mode", "p1_depth", "p2_depth",
               "n_npcs", "npc_health", "npc_damage", "npc_armor", "player_health",
-              "player_damage", "player_armor", "autoreset", "flags", "n_layouts")
+              "player_damage", "player_armor", "autoreset", "flags", "n_layouts", "sep_period")
 
 
 class OrxCfg(ctypes.Structure):
@@ -47,7 +47,8 @@ class EnvConfig:
     player_damage: int = 2
     player_armor: int = 1
     autoreset: int = 1
-    flags: int = 0
+    flags: int = 0                  # enums.EXT_* build extensions (readme-only mechanics)
+    sep_period: int = 0             # EXT_SEPARATION_DAMAGE: ticks per +1 damage
     # explicit-grid dungeon generator: [L, W, H] Tile codes (None =
     # EmptyDungeonGenerator).  spawn_dungeon(depth) returns layout randint(L).
     layouts: Optional[np.ndarray] = dataclasses.field(default=None, repr=False, compare=False)

@@ -55,7 +55,10 @@ namespace {
 // ---------------------------------------------------------------------------
 // Philox4x32-10 and the reference's bounded-integer transforms
 // ---------------------------------------------------------------------------
-enum : uint32_t { PUR_INIT = 1, PUR_DUNGEON = 2, PUR_SHUFFLE = 3, PUR_SPAWN = 4, PUR_POLICY = 5 };
+enum : uint32_t {
+  PUR_INIT = 1, PUR_DUNGEON = 2, PUR_SHUFFLE = 3, PUR_SPAWN = 4, PUR_POLICY = 5,
+  PUR_RESOLVE = 6  // ORX_EXT_RANDOM_DOUBLE_DEATH
+};
 constexpr uint32_t kWordCap = 4096;  // per stream; exceeding it stops the game
 constexpr int32_t kStartTick = 1;     // GameState.tick of a fresh game (worldgen.py:87,133)
 constexpr uint32_t kDeadSlot = 0xFFFFu;
@@ -157,6 +160,7 @@ __device__ __forceinline__ Player pick(bool c, const Player& a, const Player& b)
 struct Cfg {  // device copy of orx_cfg_t plus derived constants (all wave-uniform)
   int32_t W, H, despawn, max_ticks, start_mode, d1, d2, K;
   int32_t npc_hp, player_hp, player_dmg_net, autoreset;
+  int32_t ext, sep_period;  // ORX_EXT_* build extensions (0 in FAST kernels)
   int32_t ih;        // H - 2 (interior column height)
   NpBound ground;    // randint(n_ground), n_ground = (W-2)(H-2) - 1
   NpBound stair_x;   // randint(1, W-2)
@@ -691,7 +695,7 @@ __device__ __forceinline__ void tick_game(const Cfg& c, Key key, uint32_t game, 
                                           bool p1_first, bool writer, Player& p1, Player& p2,
                                           Npcs<NCAP>& npc, const NpcMem& m, int32_t& tick,
                                           int32_t& status, bool& err, Deltas& dl,
-                                          Events<EV>& ev) {
+                                          Events<EV>& ev, int32_t& sep_start) {
   calc_pos(p1.x, p1.y, p1.move, p1.tx, p1.ty);         // updater.py:89-98
   if (blocked<GRID>(c, p1.lay, p1.tx, p1.ty)) p1.move = ORX_MOVE_STAY;
   calc_pos(p2.x, p2.y, p2.move, p2.tx, p2.ty);
@@ -721,9 +725,30 @@ __device__ __forceinline__ void tick_game(const Cfg& c, Key key, uint32_t game, 
   p1 = pick(p1_first, A, Bp);
   p2 = pick(p1_first, Bp, A);
 
+  if (c.ext & ORX_EXT_SEPARATION_DAMAGE) {  // build extension (readme.md:46-47)
+    if (p1.d != p2.d) {
+      if (sep_start < 0) sep_start = tick;
+      const int32_t k = tick - sep_start + 1;
+      const int32_t dmg = (k + c.sep_period - 1) / c.sep_period;
+      const bool p1_behind = p1.d < p2.d;
+      if (p1_behind) p1.hp -= dmg; else p2.hp -= dmg;
+      ev.emit(ORX_EV_HEALTH, p1_behind ? 1 : 2, -dmg, 0);
+    } else {
+      sep_start = -1;
+    }
+  }
+  bool p2_wins_draw = false;
+  if ((c.ext & ORX_EXT_RANDOM_DOUBLE_DEATH) && p1.hp <= 0 && p2.hp <= 0) {  // readme.md:47-48
+    Stream r;
+    r.init(game, ep, (uint32_t)tick, tag(PUR_RESOLVE, 0));
+    p2_wins_draw = (r.next(key) >> 31) != 0;
+  }
+
   tick += 1;                                           // updater.py:148-162
   if (p1.hp <= 0)
-    status = p2.hp <= 0 ? ORX_TIE : ORX_PLAYER2_WIN;
+    status = p2.hp > 0 ? ORX_PLAYER2_WIN
+             : !(c.ext & ORX_EXT_RANDOM_DOUBLE_DEATH) ? ORX_TIE
+             : p2_wins_draw ? ORX_PLAYER2_WIN : ORX_PLAYER1_WIN;
   else if (p2.hp <= 0)
     status = ORX_PLAYER1_WIN;
   else if (c.max_ticks && tick >= c.max_ticks)
@@ -819,6 +844,8 @@ __device__ __forceinline__ Cfg make_cfg(const orx_cfg_t& h, const orx_state_t& s
   c.K = h.n_npcs; c.npc_hp = h.npc_health; c.player_hp = h.player_health;
   c.player_dmg_net = h.player_damage - h.player_armor;
   c.autoreset = h.autoreset;
+  c.ext = h.flags;
+  c.sep_period = h.sep_period > 0 ? h.sep_period : 1;
   c.ih = h.height - 2;
   c.ground.set((h.width - 2) * (h.height - 2) - 1);
   c.stair_x.set(h.width - 3);
@@ -857,6 +884,7 @@ __global__ void __launch_bounds__(256) reset_kernel(orx_cfg_t hc, orx_state_t st
   store_players<GRID>(st, B, i, p1, p2, true);
   st.tick[i] = tick;
   st.status[i] = status;
+  if (c.ext & ORX_EXT_SEPARATION_DAMAGE) st.sep_start[i] = -1;
   if constexpr (NCAP > 0) {
     st.npc_alive[i] = npc.alive;
     store_new_npcs(st, c, B, i, npc);
@@ -886,6 +914,7 @@ __global__ void __launch_bounds__(256) step_kernel(orx_cfg_t hc, orx_state_t st,
     st.tick[i] = tick;
     st.status[i] = status;
     st.episode[i] = (int32_t)ep;
+    if (c.ext & ORX_EXT_SEPARATION_DAMAGE) st.sep_start[i] = -1;
     if constexpr (NCAP > 0) {
       st.npc_alive[i] = npc.alive;
       store_new_npcs(st, c, B, i, npc);
@@ -909,8 +938,10 @@ __global__ void __launch_bounds__(256) step_kernel(orx_cfg_t hc, orx_state_t st,
   Events<EV> ev{EV ? events + (size_t)i * ORX_MAX_EVENTS * 4 : nullptr, 0};
   bool err = false;
   const bool p1_first = p1_first_draw(key, game, ep, tick, err);
+  int32_t sep = (c.ext & ORX_EXT_SEPARATION_DAMAGE) ? st.sep_start[i] : -1;
   tick_game<NCAP, EV, GRID>(c, key, game, ep, p1_first, true, p1, p2, npc, m, tick, status, err,
-                            dl, ev);
+                            dl, ev, sep);
+  if (c.ext & ORX_EXT_SEPARATION_DAMAGE) st.sep_start[i] = sep;
   store_players<GRID>(st, B, i, p1, p2, dl.descend != 0);
   st.tick[i] = tick;
   st.status[i] = status;
@@ -1001,7 +1032,8 @@ __global__ void __launch_bounds__(256) rollout_kernel(orx_cfg_t hc, orx_state_t 
   const int32_t pol2 = FAST ? (int32_t)ORX_POLICY_RANDOM : pol2_;
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= B) return;
-  const Cfg c = make_cfg(hc, st);
+  Cfg c = make_cfg(hc, st);
+  if (FAST) c.ext = 0;  // FAST launches require flags == 0
   const uint32_t game = off + i;
   Player p1, p2;
   load_players<GRID>(st, B, i, p1, p2);
@@ -1012,6 +1044,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(orx_cfg_t hc, orx_state_t 
   load_npcs(st, c, B, i, npc);
   const NpcMem m{st.npc_pos, st.npc_health, B, i};
   Deltas dl = {0, 0, 0, 0, 0, 0};
+  int32_t sep = (c.ext & ORX_EXT_SEPARATION_DAMAGE) ? st.sep_start[i] : -1;
   bool stairs_dirty = false, npc_dirty = false;
   const bool any_random = pol1 == ORX_POLICY_RANDOM || pol2 == ORX_POLICY_RANDOM;
   for (int32_t t = 0; t < n_ticks; ++t) {
@@ -1035,7 +1068,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(orx_cfg_t hc, orx_state_t 
         status = (c.max_ticks && tick >= c.max_ticks) ? ORX_TIE : ORX_IN_PROGRESS;
       } else {
         tick_game<NCAP, false, GRID>(c, key, game, ep, p1_first, true, p1, p2, npc, m, tick,
-                                     status, err, dl, ev);
+                                     status, err, dl, ev, sep);
       }
       stairs_dirty |= dl.descend != descents;
     } else if (c.autoreset) {
@@ -1049,6 +1082,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(orx_cfg_t hc, orx_state_t 
       }
       stairs_dirty = true;
       npc_dirty = true;
+      sep = -1;
     }
     if (!(ORX_DIAG & 16)) store_traj<FAST>(obs, act, t, B, i, p1, p2, tick, status, a1, a2);
   }
@@ -1056,6 +1090,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(orx_cfg_t hc, orx_state_t 
   st.tick[i] = tick;
   st.status[i] = status;
   st.episode[i] = (int32_t)ep;
+  if (c.ext & ORX_EXT_SEPARATION_DAMAGE) st.sep_start[i] = sep;
   if (NCAP > 0 && (npc_dirty || dl.npc_death)) st.npc_alive[i] = npc.alive;
   flush_deltas(st, B, i, dl);
 }
@@ -1133,7 +1168,8 @@ __global__ void __launch_bounds__(128) rollout_pc_kernel(
   const uint32_t wave = threadIdx.x >> 6;  // wave-uniform role
   const uint32_t i = blockIdx.x * 64u + lane;
   const bool valid = i < B;                 // no early return: every wave runs every iteration
-  const Cfg c = make_cfg(hc, st);
+  Cfg c = make_cfg(hc, st);
+  if (FAST) c.ext = 0;  // FAST launches require flags == 0
   const int need = (pol1 == ORX_POLICY_RANDOM) + (pol2 == ORX_POLICY_RANDOM);
   if (wave == 0) {
     rec_t[lane] = -1;
@@ -1182,6 +1218,7 @@ __global__ void __launch_bounds__(128) rollout_pc_kernel(
   Npcs<NCAP> npc;
   load_npcs(st, c, B, ic, npc);
   Deltas dl = {0, 0, 0, 0, 0, 0};
+  int32_t sep = (c.ext & ORX_EXT_SEPARATION_DAMAGE) ? st.sep_start[ic] : -1;
   bool stairs_dirty = false, npc_dirty = false;
   const NpcMem m{st.npc_pos, st.npc_health, B, ic};
   int32_t avail;  // iterations known to be produced
@@ -1219,7 +1256,7 @@ __global__ void __launch_bounds__(128) rollout_pc_kernel(
         status = (c.max_ticks && tick >= c.max_ticks) ? ORX_TIE : ORX_IN_PROGRESS;
       } else {
         tick_game(c, key, gc, ep, (w & 64u) != 0, valid, p1, p2, npc, m, tick, status, err, dl,
-                  ev);
+                  ev, sep);
       }
       stairs_dirty |= dl.descend != descents;
     } else if (c.autoreset) {
@@ -1228,6 +1265,7 @@ __global__ void __launch_bounds__(128) rollout_pc_kernel(
       if constexpr (NCAP > 0) if (valid) store_new_npcs(st, c, B, i, npc);
       stairs_dirty = true;
       npc_dirty = true;
+      sep = -1;
     }
     if (!(ORX_DIAG & 16) && valid)
       store_traj<FAST>(obs, act, t, B, i, p1, p2, tick, status, a1, a2);
@@ -1238,6 +1276,7 @@ __global__ void __launch_bounds__(128) rollout_pc_kernel(
     st.tick[i] = tick;
     st.status[i] = status;
     st.episode[i] = (int32_t)ep;
+    if (c.ext & ORX_EXT_SEPARATION_DAMAGE) st.sep_start[i] = sep;
     if (NCAP > 0 && (npc_dirty || dl.npc_death)) st.npc_alive[i] = npc.alive;
     flush_deltas(st, B, i, dl);
   }
@@ -1307,7 +1346,10 @@ int check_cfg(const orx_cfg_t* c) {
     return fail(ORX_EINVAL, "board too small for the players and NPCs");
   if (c->player_health < 1) return fail(ORX_EINVAL, "player_health must be >= 1");
   if (c->autoreset != 0 && c->autoreset != 1) return fail(ORX_EINVAL, "autoreset must be 0 or 1");
-  if (c->flags != 0) return fail(ORX_EINVAL, "no extension flags are implemented");
+  if (c->flags & ~(ORX_EXT_SEPARATION_DAMAGE | ORX_EXT_RANDOM_DOUBLE_DEATH))
+    return fail(ORX_EINVAL, "unknown extension flag");
+  if ((c->flags & ORX_EXT_SEPARATION_DAMAGE) && c->sep_period < 1)
+    return fail(ORX_EINVAL, "separation damage needs sep_period >= 1");
   return ORX_OK;
 }
 
@@ -1322,6 +1364,8 @@ int check_state(const orx_cfg_t* c, const orx_state_t* s, bool full) {
     return fail(ORX_EINVAL, "n_npcs > 0 needs npc_pos, npc_health and npc_alive");
   if (c->n_layouts > 0 && (!s->p_layout || !s->bank_tiles || !s->bank_ground || !s->bank_meta))
     return fail(ORX_EINVAL, "n_layouts > 0 needs p_layout and the bank_* arrays");
+  if ((c->flags & ORX_EXT_SEPARATION_DAMAGE) && !s->sep_start)
+    return fail(ORX_EINVAL, "separation damage needs sep_start");
   return ORX_OK;
 }
 
@@ -1482,8 +1526,9 @@ int orx_rollout(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p1, 
   // the buffer-addressed fast path needs one tick's obs rows below 2 GiB; a
   // dungeon bank runs the generic plain kernel (tile lookups)
   const bool grid = cfg->n_layouts > 0;
-  const bool rr = !grid && policy_p1 == ORX_POLICY_RANDOM && policy_p2 == ORX_POLICY_RANDOM &&
-                  obs && act && (uint64_t)B * ORX_OBS_FIELDS * 4u < (1ull << 31);
+  const bool rr = !grid && cfg->flags == 0 && policy_p1 == ORX_POLICY_RANDOM &&
+                  policy_p2 == ORX_POLICY_RANDOM && obs && act &&
+                  (uint64_t)B * ORX_OBS_FIELDS * 4u < (1ull << 31);
   const bool pc = !grid && use_pc_rollout(B);
   const int nc = ncap_for(cfg->n_npcs);
 #define ORX_ROLLOUT(N, R, G)                                                                    \

@@ -17,7 +17,7 @@ import torch
 
 from . import _lib
 from .config import EnvConfig
-from .enums import MAX_EVENTS, N_COUNTERS, OBS_FIELDS, Policy
+from .enums import EXT_SEPARATION_DAMAGE, MAX_EVENTS, N_COUNTERS, OBS_FIELDS, Policy
 
 STATE_FIELDS = ("p_x", "p_y", "p_depth", "p_health", "st_x", "st_y", "tick", "status", "episode",
                 "ret_sum", "ep_count", "counters", "npc_pos", "npc_health", "npc_alive")
@@ -83,6 +83,11 @@ class BatchedEngine:
             self.bank_ground = torch.from_numpy(bank.ground.view(np.int16)).to(device)
             self.bank_meta = torch.from_numpy(bank.meta).to(device)
             ptrs.update({f: getattr(self, f).data_ptr() for f in BANK_FIELDS})
+        # EXT_SEPARATION_DAMAGE state (first separated tick, -1 = together)
+        self.sep_start = None
+        if int(cfg.flags) & EXT_SEPARATION_DAMAGE:
+            self.sep_start = torch.full((B,), -1, dtype=torch.int32, device=device)
+            ptrs["sep_start"] = self.sep_start.data_ptr()
         self._st = _lib.OrxState(**ptrs)
         if reset:
             self.reset()
@@ -167,6 +172,8 @@ class BatchedEngine:
         out = {}
         if self.bank is not None:
             out["p_layout"] = self.p_layout.cpu().numpy()
+        if self.sep_start is not None:
+            out["sep_start"] = self.sep_start.cpu().numpy()
         for f in STATE_FIELDS:
             a = getattr(self, f).cpu().numpy()
             if f == "npc_pos":
@@ -182,6 +189,8 @@ class BatchedEngine:
         """Writes host arrays (engine layout) into the device state."""
         if self.bank is not None and "p_layout" in snap:
             self.p_layout.copy_(torch.from_numpy(np.ascontiguousarray(snap["p_layout"], np.int16)))
+        if self.sep_start is not None and "sep_start" in snap:
+            self.sep_start.copy_(torch.from_numpy(np.ascontiguousarray(snap["sep_start"], np.int32)))
         for f in STATE_FIELDS:
             if f not in snap:
                 continue

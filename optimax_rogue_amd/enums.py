@@ -60,6 +60,11 @@ class Policy(enum.IntEnum):
 STATUS_BAD_ACTION = 16
 STATUS_RNG_EXHAUSTED = 17
 
+# build extensions (orx_cfg_t.flags, include/orx.h ORX_EXT_*): readme-only
+# mechanics, off by default, parity unpinned
+EXT_SEPARATION_DAMAGE = 1
+EXT_RANDOM_DOUBLE_DEATH = 2
+
 # per-game event counter rows (include/orx.h ORX_CNT_*)
 CNT_COMBAT, CNT_DESCEND, CNT_DUNGEON, CNT_NPC_DEATH = range(4)
 N_COUNTERS = 4
@@ -70,5 +75,5 @@ OBS_FIELDS = ("p1_x", "p1_y", "p1_depth", "p1_health", "p2_x", "p2_y", "p2_depth
               "p2_stair_y")
 
 # update-event records of orx_step_events (include/orx.h ORX_EV_*)
-EV_COMBAT, EV_DEATH, EV_POSITION, EV_DUNGEON = 1, 2, 3, 4
+EV_COMBAT, EV_DEATH, EV_POSITION, EV_DUNGEON, EV_HEALTH = 1, 2, 3, 4, 5
 MAX_EVENTS = 8

@@ -18,7 +18,7 @@ from __future__ import annotations
 
 from typing import List
 
-from .enums import EV_COMBAT, EV_DEATH, EV_DUNGEON, EV_POSITION, CombatFlag
+from .enums import EV_COMBAT, EV_DEATH, EV_DUNGEON, EV_HEALTH, EV_POSITION, CombatFlag
 
 
 class GameStateUpdate:
@@ -100,6 +100,28 @@ class DungeonCreatedUpdate(GameStateUpdate):
         return depth == self.depth
 
 
+class EntityHealthUpdate(GameStateUpdate):
+    """Health change outside combat (updates.py:222-253); emitted only by the
+    EXT_SEPARATION_DAMAGE build extension (source = the entity itself)."""
+
+    def __init__(self, order, entity_iden, source_iden, amount, tags):
+        super().__init__(order)
+        self.entity_iden, self.source_iden, self.amount = entity_iden, source_iden, amount
+        self.tags = frozenset(tags)
+
+    def to_prims(self):
+        return {'order': self.order, 'entity_iden': self.entity_iden,
+                'source_iden': self.source_iden, 'amount': self.amount,
+                'tags': tuple(self.tags)}
+
+    def apply(self, game_state) -> None:
+        game_state.iden_lookup[self.entity_iden].health += self.amount
+
+    def relevant_for(self, game_state, depth: int) -> bool:
+        return depth in (game_state.iden_lookup[self.entity_iden].depth,
+                         game_state.iden_lookup[self.source_iden].depth)
+
+
 def from_events(rows, order_start: int, og_damage: int, pre_depth: dict,
                 dungeon_for=None) -> List[GameStateUpdate]:
     """Update objects for one game's event records [(type, iden, a, b), ...].
@@ -120,6 +142,8 @@ def from_events(rows, order_start: int, og_damage: int, pre_depth: dict,
             out.append(EntityPositionUpdate(order, iden, a, pre_depth[iden], b & 0xFFFF, b >> 16))
         elif typ == EV_DUNGEON:
             out.append(DungeonCreatedUpdate(order, a, dungeon_for(a) if dungeon_for else None))
+        elif typ == EV_HEALTH:
+            out.append(EntityHealthUpdate(order, iden, iden, a, {"separation"}))
         else:
             raise ValueError(f"unknown event type {typ}")
         order += 1

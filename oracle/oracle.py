@@ -19,7 +19,7 @@ LIB_PATH = os.path.join(HERE, "liborx_oracle.so")
 # Field order of orx_cfg_t (include/orx.h); tests check it against the header.
 CFG_FIELDS = ["width", "height", "despawn", "max_ticks", "start_mode", "p1_depth", "p2_depth",
               "n_npcs", "npc_health", "npc_damage", "npc_armor", "player_health",
-              "player_damage", "player_armor", "autoreset", "flags", "n_layouts"]
+              "player_damage", "player_armor", "autoreset", "flags", "n_layouts", "sep_period"]
 
 
 class _Cfg(ctypes.Structure):
@@ -29,7 +29,7 @@ class _Cfg(ctypes.Structure):
 DEFAULT_CFG = dict(width=32, height=32, despawn=1, max_ticks=1000, start_mode=1, p1_depth=0,
                    p2_depth=0, n_npcs=0, npc_health=3, npc_damage=1, npc_armor=0,
                    player_health=10, player_damage=2, player_armor=1, autoreset=1, flags=0,
-                   n_layouts=0)
+                   n_layouts=0, sep_period=0)
 
 _lib = None
 
@@ -66,6 +66,7 @@ def lib():
         L.oracle_set_rng.argtypes = [vp, u64, i64]
         L.oracle_set_bank.argtypes = [vp, vp, i32]
         L.oracle_export_layout.argtypes = [vp, vp]
+        L.oracle_export_sep.argtypes = [vp, vp]
         _lib = L
     return _lib
 
@@ -142,6 +143,9 @@ class Oracle:
                  "episode", "ret_sum", "ep_count", "counters", "npc_pos", "npc_health",
                  "npc_alive"]
         lib().oracle_export(self._h, *[_ptr(out[k]) for k in order])
+        if self.cfg["flags"] & 1:   # ORX_EXT_SEPARATION_DAMAGE
+            out["sep_start"] = np.zeros(B, np.int32)
+            lib().oracle_export_sep(self._h, _ptr(out["sep_start"]))
         if self.layouts is not None:
             out["p_layout"] = np.zeros((2, B), np.int16)
             lib().oracle_export_layout(self._h, _ptr(out["p_layout"]))

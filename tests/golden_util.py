@@ -78,7 +78,7 @@ class Fixture:
 def compare_state(got: dict, want: dict, K: int, where: str = ""):
     """Asserts bit-exact equality of every state field (NPC slots only if K;
     the bank layout of each player's depth when both sides carry it)."""
-    keys = STATE_KEYS + (["p_layout"] if "p_layout" in got and "p_layout" in want else [])
+    keys = STATE_KEYS + [k for k in ("p_layout", "sep_start") if k in got and k in want]
     for k in keys:
         if k.startswith("npc") and K == 0:
             continue

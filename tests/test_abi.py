@@ -92,6 +92,9 @@ def test_validate_cfg(lib):
     lay = np.ones((2, 300, 300), np.uint8)
     bad.append(EnvConfig(width=300, height=300, layouts=lay))          # W*H > 65536
     ok.append(EnvConfig(width=6, height=5, layouts=np.ones((3, 6, 5), np.uint8)))
+    # build extensions: known bits only; separation damage needs a period
+    ok.append(EnvConfig(flags=3, sep_period=5))
+    bad += [EnvConfig(flags=4), EnvConfig(flags=1, sep_period=0)]
     for c in ok:
         assert lib.orx_validate_cfg(ctypes.byref(c.to_c())) == 0, c
     for c in bad:
@@ -107,7 +110,7 @@ def test_plain_c_consumer(lib, tmp_path):
                     "-Wl,-rpath," + os.path.join(ROOT, "optimax_rogue_amd")], check=True)
     r = subprocess.run([str(exe)], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert "sizeof(orx_cfg_t)=68" in r.stdout
+    assert "sizeof(orx_cfg_t)=72" in r.stdout
 
 
 def test_engine_refuses_cpu():

@@ -122,6 +122,11 @@ ORACLE_CASES = {
     "bank_64_npc": (dict(width=64, height=64, n_npcs=8, max_ticks=300), (1, 1), 2048, 400, 15),
     "bank_stairs_unused": (dict(width=12, height=10, n_npcs=2, max_ticks=200, despawn=2), (2, 1),
                            2048, 400, 16),
+    # build extensions (readme-only mechanics, parity unpinned: engine vs oracle)
+    "ext_separation": (dict(width=9, height=9, start_mode=2, p1_depth=0, p2_depth=2, n_npcs=2,
+                            max_ticks=300, flags=1, sep_period=4), (2, 1), 2048, 400, 17),
+    "ext_double_death": (dict(width=4, height=5, max_ticks=0, player_health=1, flags=3,
+                              sep_period=2), (1, 1), 2048, 200, 18),
 }
 ORACLE_BANKS = {"bank_64_npc": (64, 64, 16, 21, (1,)), "bank_stairs_unused": (12, 10, 5, 22, (1, 3))}
 
@@ -148,6 +153,30 @@ def test_vs_oracle_large(name, oracle_lib):
         compare_state(eng.snapshot(), want, ora.K, f"{name} step chunk {c}")
         compare_state(eng2.snapshot(), want, ora.K, f"{name} rollout chunk {c}")
     torch.cuda.synchronize()
+
+
+def test_ext_events_vs_oracle(oracle_lib):
+    """Separation-damage EntityHealthUpdate records and random double-death
+    outcomes: orx_step_events against the oracle, tick by tick."""
+    import torch
+    cfg = dict(width=6, height=6, start_mode=2, p1_depth=1, p2_depth=0, max_ticks=120,
+               flags=3, sep_period=2, n_npcs=1)
+    B = 512
+    ora = oracle_lib.Oracle(cfg, B, 19, 0, record_events=True)
+    ora.reset(episode=np.zeros(B, np.int32))
+    eng = _engine(cfg, B, 19)
+    seen_health = 0
+    for t in range(150):
+        a = ora.policy(2, 1)
+        ora.step(a)
+        _, ev, n = eng.step(torch.from_numpy(a).to(eng.device).contiguous(), events=True)
+        ev, n = ev.cpu().numpy(), n.cpu().numpy()
+        for g in range(B):
+            got = [tuple(int(v) for v in r) for r in ev[g, : n[g]]]
+            assert got == ora.events(g), (t, g)
+            seen_health += sum(1 for r in got if r[0] == 5)
+    compare_state(eng.snapshot(), ora.export(), 1, "ext final")
+    assert seen_health > 100
 
 
 def test_sharding_invariance():

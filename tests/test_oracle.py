@@ -88,3 +88,55 @@ def test_oracle_bad_action_and_freeze(oracle_lib):
         o.step(np.full((4, 2), 5, np.int8))
     s = o.export()
     assert s["tick"].tolist() == [4, 1, 4, 4] and s["status"].tolist() == [4, 16, 4, 4]
+
+
+def test_ext_separation_damage(oracle_lib):
+    """ORX_EXT_SEPARATION_DAMAGE (readme.md:46-47, parity unpinned): the
+    shallower player loses ceil(k / sep_period) at the end of the k-th
+    consecutive separated tick, reported as an EntityHealthUpdate record."""
+    cfg = dict(width=9, height=9, start_mode=2, p1_depth=0, p2_depth=3, max_ticks=0,
+               flags=1, sep_period=3, autoreset=0)
+    B = 16
+    o = oracle_lib.Oracle(cfg, B, 7, 0, record_events=True)
+    o.reset()
+    assert (o.export()["sep_start"] == -1).all()
+    stay = np.full((B, 2), 5, np.int8)
+    lost = 0
+    for k in range(1, 8):
+        o.step(stay)                               # nobody moves: always separated
+        lost += -(-k // 3)
+        s = o.export()
+        assert (s["p_health"][0] == 10 - lost).all()
+        assert (s["p_health"][1] == 10).all()
+        assert (s["sep_start"] == 1).all()
+        for g in range(B):
+            assert o.events(g) == [(5, 1, -(-(-k // 3)), 0)]
+        if 10 - lost <= 0:
+            assert (s["status"] == 3).all()        # player 2 wins
+            break
+
+
+def test_ext_random_double_death(oracle_lib):
+    """ORX_EXT_RANDOM_DOUBLE_DEATH (readme.md:47-48, parity unpinned): a tick
+    in which both players die ends in a win drawn from stream purpose 6
+    instead of a tie; every other outcome is unchanged."""
+    cfg = dict(width=4, height=5, max_ticks=0, player_health=1, autoreset=1)
+    B, seed = 2048, 31
+    base = oracle_lib.Oracle(cfg, B, seed, 0)
+    ext = oracle_lib.Oracle(dict(cfg, flags=2), B, seed, 0)
+    base.reset()
+    ext.reset()
+    double_deaths, wins = 0, set()
+    for t in range(60):
+        a = base.policy(1, 1)
+        base.step(a)
+        ext.step(a)
+        sb, se = base.export(), ext.export()
+        dd = sb["status"] == 4                     # only double deaths tie (no tick limit)
+        double_deaths += int(dd.sum())
+        wins |= set(se["status"][dd].tolist())
+        assert (se["status"][dd] != 4).all()
+        assert np.array_equal(se["status"][~dd], sb["status"][~dd])
+        for k in ("p_x", "p_y", "p_health", "tick", "episode"):
+            assert np.array_equal(se[k], sb[k]), k
+    assert double_deaths > 10 and wins == {2, 3}
