@@ -76,6 +76,21 @@ extern "C" {
 #define ORX_POLICY_STAIRCASE 2 /* StaircaseBot.move staircasebot.py:9-21       */
 #define ORX_POLICY_STAY 3      /* always Move.Stay                            */
 
+/* word sources (orx_cfg_t.rng)                                             */
+#define ORX_RNG_PHILOX 0  /* keyed Philox4x32-10 streams (default; stateless,
+                             shard-invariant, DESIGN.md "Random streams")   */
+#define ORX_RNG_MT19937 1 /* stock-seed mode: per game the two MT19937 states
+                             of a reference process seeded random.seed(n) and
+                             np.random.seed(n), n = seed + global game id
+                             (orx_seed_mt), consumed in the reference's call
+                             order: CPython random for the bots and shuffles
+                             (randombot.py:21, updater.py:114,127), numpy for
+                             dungeons and spawn cells (worldgen.py:39-40,
+                             world.py:62)                                   */
+#define ORX_DSTORE 256    /* stock-seed mode: dungeons remembered per game
+                             (power of two; the depth gap between the two
+                             players it covers under Unreachable)           */
+
 /* build extensions (orx_cfg_t.flags): mechanics the reference's readme
  * describes but its code does not implement (readme.md:44-48); off = parity.
  * No reference output pins them ("parity unpinned").        */
@@ -157,6 +172,7 @@ typedef struct orx_cfg {
                              randint(L) of orx_state_t.bank_* (an explicit-
                              grid DungeonGenerator plugin, worldgen.py:9-26) */
   int32_t sep_period;     /* ORX_EXT_SEPARATION_DAMAGE: ticks per +1 damage   */
+  int32_t rng;            /* ORX_RNG_*                                       */
 } orx_cfg_t;
 
 /* ---- batch state (SoA, batch axis contiguous; all device pointers) ------- */
@@ -191,6 +207,13 @@ typedef struct orx_state {
   int32_t* sep_start;           /* [B] ORX_EXT_SEPARATION_DAMAGE: tick the
                                    current separation began, -1 = together
                                    (NULL when the extension is off)          */
+  /* stock-seed mode (cfg->rng = ORX_RNG_MT19937; NULL otherwise)            */
+  uint32_t* mt_py;              /* [625][B] CPython random: mt[624] + index   */
+  uint32_t* mt_np;              /* [625][B] numpy RandomState: key[624] + pos */
+  int32_t* dstore;              /* [ORX_DSTORE][2][B] {depth, sx | sy << 8 |
+                                   (layout + 1) << 16} of entered dungeons,
+                                   slot depth % ORX_DSTORE (the staircases a
+                                   keyed stream would regenerate)            */
 } orx_state_t;
 
 /* ---- entry points --------------------------------------------------------- */
@@ -205,6 +228,14 @@ const char* orx_last_error(void);
  * Replaces the constructor checks of Updater / generators
  * (updater.py:65-69, worldgen.py:61-135; ValueError -> ORX_EINVAL). */
 int orx_validate_cfg(const orx_cfg_t* cfg);
+
+/* Stock-seed mode: seeds game b's two MT19937 states as a reference
+ * process would after random.seed(n); np.random.seed(n) with n = seed +
+ * game_offset + b (CPython random_seed -> init_by_array, _randommodule.c;
+ * numpy RandomState._legacy_seeding -> mt19937_seed; n < 2^32).  Call once
+ * before the first orx_reset; later episodes continue the streams. */
+int orx_seed_mt(const orx_cfg_t* cfg, const orx_state_t* st, int64_t n_games, uint64_t seed,
+                int64_t game_offset, void* stream);
 
 /* Starts episode st->episode[b] for every game b with mask[b] != 0
  * (mask == NULL: all games).  Replaces GameStartGenerator.setup_game:

@@ -21,7 +21,8 @@ class OrxState(ctypes.Structure):
     _fields_ = [(n, ctypes.c_void_p) for n in (
         "p_x", "p_y", "p_depth", "p_health", "st_x", "st_y", "tick", "status", "episode",
         "ret_sum", "ep_count", "counters", "npc_pos", "npc_health", "npc_alive",
-        "p_layout", "bank_tiles", "bank_ground", "bank_meta", "sep_start")]
+        "p_layout", "bank_tiles", "bank_ground", "bank_meta", "sep_start", "mt_py", "mt_np",
+        "dstore")]
 
 
 class OrxError(RuntimeError):
@@ -34,7 +35,7 @@ _lib = None
 
 EXPORTS = ("orx_abi_version", "orx_last_error", "orx_validate_cfg", "orx_reset", "orx_step",
            "orx_step_events", "orx_policy", "orx_rollout", "orx_dungeon_stairs",
-           "orx_dungeon_spawn")
+           "orx_dungeon_spawn", "orx_seed_mt")
 
 
 def load() -> ctypes.CDLL:
@@ -71,6 +72,8 @@ def load() -> ctypes.CDLL:
     L.orx_dungeon_spawn.restype = ctypes.c_int
     L.orx_dungeon_spawn.argtypes = [P(OrxCfg), P(OrxState), vp, vp, vp, vp, vp, vp, vp, i64, u64,
                                     vp]
+    L.orx_seed_mt.restype = ctypes.c_int
+    L.orx_seed_mt.argtypes = [P(OrxCfg), P(OrxState), i64, u64, i64, vp]
     v = L.orx_abi_version()
     if v != ABI_VERSION:
         raise RuntimeError(f"liborx.so ABI {v} != expected {ABI_VERSION}")

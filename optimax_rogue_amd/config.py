@@ -22,7 +22,8 @@ from .enums import DungeonDespawningStrategy, StartMode
 
 CFG_FIELDS = ("width", "height", "despawn", "max_ticks", "start_mode", "p1_depth", "p2_depth",
               "n_npcs", "npc_health", "npc_damage", "npc_armor", "player_health",
-              "player_damage", "player_armor", "autoreset", "flags", "n_layouts", "sep_period")
+              "player_damage", "player_armor", "autoreset", "flags", "n_layouts", "sep_period",
+              "rng")
 
 
 class OrxCfg(ctypes.Structure):
@@ -49,6 +50,10 @@ class EnvConfig:
     autoreset: int = 1
     flags: int = 0                  # enums.EXT_* build extensions (readme-only mechanics)
     sep_period: int = 0             # EXT_SEPARATION_DAMAGE: ticks per +1 damage
+    # word source: RNG_PHILOX (keyed streams, batch/sharding invariant) or
+    # RNG_MT19937 (stock seeding: each game's own random / np.random state
+    # seeded with seed + game id, consumed in the reference's call order)
+    rng: int = 0
     # explicit-grid dungeon generator: [L, W, H] Tile codes (None =
     # EmptyDungeonGenerator).  spawn_dungeon(depth) returns layout randint(L).
     layouts: Optional[np.ndarray] = dataclasses.field(default=None, repr=False, compare=False)

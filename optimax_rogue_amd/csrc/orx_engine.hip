@@ -336,16 +336,14 @@ __device__ __forceinline__ void ground_cell(const Cfg& c, uint32_t ch, int32_t l
   y = 1 + (int32_t)(ci - q * (uint32_t)c.ih);
 }
 
-// EmptyDungeonGenerator.spawn_dungeon with words from (episode, depth, gen):
-// randint(1, W-2) then randint(1, H-2); or, with a dungeon bank, layout
-// randint(L) and its staircase.  One loop, one Philox call site.
-template <bool GRID>
-__device__ __forceinline__ void dungeon_stair(const Cfg& c, Key key, uint32_t game, uint32_t ep,
-                                           int32_t depth, uint32_t gen, int32_t& sx, int32_t& sy,
-                                           int32_t& lay, bool& err) {
+// EmptyDungeonGenerator.spawn_dungeon (worldgen.py:33-43) from a word
+// stream: randint(1, W-2) then randint(1, H-2); or, with a dungeon bank,
+// layout randint(L) and its staircase.  S = Stream (keyed Philox) or
+// MtStream (stock-seed numpy state).  One loop, one draw site.
+template <bool GRID, class S>
+__device__ __forceinline__ void dungeon_draw(const Cfg& c, S& s, Key key, int32_t& sx, int32_t& sy,
+                                          int32_t& lay, bool& err) {
   if constexpr (GRID) {
-    Stream s;
-    s.init(game, ep, (uint32_t)depth, tag(PUR_DUNGEON, gen));
     uint32_t v = 0;
     bool ok = c.layout.rng == 0;
     for (uint32_t t = 0; t < kWordCap && !ok; ++t) {
@@ -359,8 +357,6 @@ __device__ __forceinline__ void dungeon_stair(const Cfg& c, Key key, uint32_t ga
     return;
   }
   lay = -1;
-  Stream s;
-  s.init(game, ep, (uint32_t)depth, tag(PUR_DUNGEON, gen));
   int n = 0;
   int32_t v0 = 0, v1 = 0;
   for (uint32_t t = 0; t < 2 * kWordCap && n < 2; ++t) {
@@ -378,27 +374,153 @@ __device__ __forceinline__ void dungeon_stair(const Cfg& c, Key key, uint32_t ga
   sy = 1 + v1;
 }
 
+// The keyed form: words from (episode, depth, generation).
+template <bool GRID>
+__device__ __forceinline__ void dungeon_stair(const Cfg& c, Key key, uint32_t game, uint32_t ep,
+                                           int32_t depth, uint32_t gen, int32_t& sx, int32_t& sy,
+                                           int32_t& lay, bool& err) {
+  Stream s;
+  s.init(game, ep, (uint32_t)depth, tag(PUR_DUNGEON, gen));
+  dungeon_draw<GRID>(c, s, key, sx, sy, lay, err);
+}
+
+// ---------------------------------------------------------------------------
+// Stock-seed mode (cfg.rng = ORX_RNG_MT19937): MT19937 states in HBM
+// ---------------------------------------------------------------------------
+// One game's MT19937 (CPython random or numpy RandomState), column stride B:
+// words [0, 624), index at [624].  Lazy twist: word i of a new round is
+// regenerated when it is first drawn -- it needs word i+1 of the old round
+// and word i+397 mod 624 (old for i < 227, already new otherwise), exactly
+// the in-place order of genrand_uint32's block twist (_randommodule.c), so
+// the outputs are identical while a draw touches 3 words instead of 624.
+struct MtStream {
+  uint32_t* s;
+  uint32_t B, idx;
+  __device__ __forceinline__ void open(uint32_t* base, uint32_t B_, uint32_t i) {
+    s = base + i;
+    B = B_;
+    idx = s[624 * (size_t)B];
+  }
+  __device__ __forceinline__ void close() const { s[624 * (size_t)B] = idx; }
+  __device__ __forceinline__ uint32_t next(Key) {
+    if (idx >= 624u) idx = 0;
+    const uint32_t i = idx++;
+    const uint32_t i1 = i == 623u ? 0u : i + 1u;
+    const uint32_t im = i < 227u ? i + 397u : i - 227u;
+    const uint32_t y = (s[(size_t)i * B] & 0x80000000u) | (s[(size_t)i1 * B] & 0x7fffffffu);
+    uint32_t v = s[(size_t)im * B] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+    s[(size_t)i * B] = v;
+    v ^= v >> 11;
+    v ^= (v << 7) & 0x9d2c5680u;
+    v ^= (v << 15) & 0xefc60000u;
+    v ^= v >> 18;
+    return v;
+  }
+};
+
+// CPython Random._randbelow_with_getrandbits(n): k = n.bit_length(),
+// getrandbits(k) = word >> (32 - k), redraw while >= n (random.py).
+template <class S>
+__device__ __forceinline__ uint32_t py_randbelow(S& s, Key key, uint32_t n, bool& err) {
+  const uint32_t sh = __clz(n);  // 32 - bit_length(n)
+  for (uint32_t t = 0; t < kWordCap; ++t) {
+    const uint32_t r = s.next(key) >> sh;
+    if (r < n) return r;
+  }
+  err = true;
+  return 0;
+}
+
+// Where the world-generation words come from.  PhiloxSrc: keyed streams per
+// purpose (dungeons regenerate from their key, nothing stored).  MtSrc: the
+// game's numpy RandomState, consumed in the reference's call order; a
+// dungeon's staircase cannot be regenerated, so entered dungeons are kept in
+// the dstore ring (slot depth % ORX_DSTORE) for the other player to find.
+struct PhiloxSrc {
+  static constexpr bool kMt = false;
+  Key key;
+  uint32_t game, ep;
+  __device__ __forceinline__ Stream init() const {
+    Stream s;
+    s.init(game, ep, 0, tag(PUR_INIT, 0));
+    return s;
+  }
+  __device__ __forceinline__ Stream spawn(int32_t tick) const {
+    Stream s;
+    s.init(game, ep, (uint32_t)tick, tag(PUR_SPAWN, 0));
+    return s;
+  }
+  template <bool GRID>
+  __device__ __forceinline__ void dungeon(const Cfg& c, int32_t depth, uint32_t gen, int32_t& sx,
+                                          int32_t& sy, int32_t& lay, bool& err) const {
+    dungeon_stair<GRID>(c, key, game, ep, depth, gen, sx, sy, lay, err);
+  }
+  __device__ __forceinline__ bool recall(int32_t, int32_t&, int32_t&, int32_t&) const {
+    return false;  // present dungeons are regenerated from their key
+  }
+  __device__ __forceinline__ void remember(int32_t, int32_t, int32_t, int32_t) const {}
+};
+
+struct MtSrc {
+  static constexpr bool kMt = true;
+  MtStream py, np;  // CPython random (bots, shuffles), numpy RandomState (world)
+  int32_t* ds;      // this game's dstore column, stride B
+  uint32_t B;
+  __device__ __forceinline__ void open(const orx_state_t& st, uint32_t B_, uint32_t i) {
+    py.open(st.mt_py, B_, i);
+    np.open(st.mt_np, B_, i);
+    ds = st.dstore + i;
+    B = B_;
+  }
+  __device__ __forceinline__ void close() const { py.close(); np.close(); }
+  __device__ __forceinline__ MtStream& init() { return np; }
+  __device__ __forceinline__ MtStream& spawn(int32_t) { return np; }
+  template <bool GRID>
+  __device__ __forceinline__ void dungeon(const Cfg& c, int32_t, uint32_t, int32_t& sx,
+                                          int32_t& sy, int32_t& lay, bool& err) {
+    dungeon_draw<GRID>(c, np, Key{0, 0}, sx, sy, lay, err);
+  }
+  __device__ __forceinline__ bool recall(int32_t depth, int32_t& sx, int32_t& sy,
+                                         int32_t& lay) const {
+    const size_t slot = (size_t)(2 * (depth & (ORX_DSTORE - 1))) * B;
+    if (ds[slot] != depth) return false;
+    const uint32_t v = (uint32_t)ds[slot + B];
+    sx = (int32_t)(v & 0xFFu);
+    sy = (int32_t)((v >> 8) & 0xFFu);
+    lay = (int32_t)(v >> 16) - 1;
+    return true;
+  }
+  __device__ __forceinline__ void remember(int32_t depth, int32_t sx, int32_t sy,
+                                           int32_t lay) const {
+    const size_t slot = (size_t)(2 * (depth & (ORX_DSTORE - 1))) * B;
+    ds[slot] = depth;
+    ds[slot + B] = (int32_t)(((uint32_t)sx & 0xFFu) | (((uint32_t)sy & 0xFFu) << 8) |
+                             ((uint32_t)(lay + 1) << 16));
+  }
+};
+
 // ---------------------------------------------------------------------------
 // Game start (setup_game + NPC spawner), all placements in one rejection loop
 // over the INIT stream (one Philox call site, one division site).
 // ---------------------------------------------------------------------------
-template <int NCAP, bool GRID = false>
-__device__ __forceinline__ void setup_game(const Cfg& c, Key key, uint32_t game, uint32_t ep,
-                                        Player& p1, Player& p2, Npcs<NCAP>& npc, int32_t& tick,
+template <int NCAP, bool GRID, class Src>
+__device__ __forceinline__ void setup_game(const Cfg& c, Key key, Src& src, Player& p1,
+                                        Player& p2, Npcs<NCAP>& npc, int32_t& tick,
                                         int32_t& status) {
   bool err = false;
   const bool sep = c.start_mode == ORX_START_SEPARATED;
   p1.d = sep ? c.d1 : 0;
   p2.d = sep ? c.d2 : 0;
-  dungeon_stair<GRID>(c, key, game, ep, p1.d, 0, p1.sx, p1.sy, p1.lay, err);
+  src.template dungeon<GRID>(c, p1.d, 0, p1.sx, p1.sy, p1.lay, err);
+  src.remember(p1.d, p1.sx, p1.sy, p1.lay);
   if (sep) {
-    dungeon_stair<GRID>(c, key, game, ep, p2.d, 0, p2.sx, p2.sy, p2.lay, err);
+    src.template dungeon<GRID>(c, p2.d, 0, p2.sx, p2.sy, p2.lay, err);
+    src.remember(p2.d, p2.sx, p2.sy, p2.lay);
   } else {
     p2.sx = p1.sx; p2.sy = p1.sy; p2.lay = p1.lay;
   }
   npc.clear();
-  Stream s;
-  s.init(game, ep, 0, tag(PUR_INIT, 0));
+  auto&& s = src.init();
   const int total = 2 + (NCAP ? c.K : 0);
   int placed = 0;
   p1.x = p1.y = p2.x = p2.y = 0;
@@ -438,6 +560,14 @@ __device__ __forceinline__ void setup_game(const Cfg& c, Key key, uint32_t game,
   status = err ? ORX_STATUS_RNG_EXHAUSTED : ORX_IN_PROGRESS;
 }
 
+template <int NCAP, bool GRID = false>
+__device__ __forceinline__ void setup_game(const Cfg& c, Key key, uint32_t game, uint32_t ep,
+                                        Player& p1, Player& p2, Npcs<NCAP>& npc, int32_t& tick,
+                                        int32_t& status) {
+  PhiloxSrc src{key, game, ep};
+  setup_game<NCAP, GRID>(c, key, src, p1, p2, npc, tick, status);
+}
+
 // ---------------------------------------------------------------------------
 // Descend (rare): dungeon presence, staircase, spawn cell
 // ---------------------------------------------------------------------------
@@ -447,10 +577,10 @@ __device__ __forceinline__ void setup_game(const Cfg& c, Key key, uint32_t game,
 //   Unused:      World == {p1.d, p2.d}, so nd is present iff other.d == nd;
 //                a fresh copy is generation 1 iff the other player already
 //                passed through nd (other.start <= nd < other.d).
-template <int NCAP, bool EV, bool GRID>
-__device__ __forceinline__ void descend(const Cfg& c, Key key, uint32_t game, uint32_t ep,
-                                     Player& self, const Player& other, int32_t other_start,
-                                     const Npcs<NCAP>& npc, Stream& spawn, Deltas& dl, bool& err,
+template <int NCAP, bool EV, bool GRID, class Src, class S>
+__device__ __forceinline__ void descend(const Cfg& c, Key key, Src& src, Player& self,
+                                     const Player& other, int32_t other_start,
+                                     const Npcs<NCAP>& npc, S& spawn, Deltas& dl, bool& err,
                                      int32_t self_iden, Events<EV>& ev) {
   const int32_t nd = self.d + 1;
   bool present;
@@ -464,9 +594,13 @@ __device__ __forceinline__ void descend(const Cfg& c, Key key, uint32_t game, ui
   int32_t sx, sy, lay;
   if (present && other.d == nd) {
     sx = other.sx; sy = other.sy; lay = other.lay;
-  } else {
-    dungeon_stair<GRID>(c, key, game, ep, nd, gen, sx, sy, lay, err);
+  } else if (!(present && src.recall(nd, sx, sy, lay))) {
+    // keyed: regenerate (present or not); stock-seed: a present dungeon must
+    // be in the ring (a gap beyond ORX_DSTORE stops the game), else draw it
+    if (Src::kMt && present) err = true;
+    src.template dungeon<GRID>(c, nd, gen, sx, sy, lay, err);
   }
+  src.remember(nd, sx, sy, lay);
   if (!present) {
     dl.dungeon += 1;
     ev.emit(ORX_EV_DUNGEON, 0, nd, 0);                 // updater.py:278-280
@@ -619,10 +753,10 @@ struct NpcMem {  // HBM rows of this game's NPC slots (stride B)
 // handle_move for `self` (updater.py:180-243), branch-free except for the
 // rare descend.  Returns true if the target cell holds an NPC (the slot is
 // resolved in npc_hits); combat against the other player is applied here.
-template <int NCAP, bool EV, bool GRID>
-__device__ __forceinline__ bool handle_move(const Cfg& c, Key key, uint32_t game, uint32_t ep,
-                                            Player& self, Player& other, int32_t other_start,
-                                            const Npcs<NCAP>& npc, Stream& spawn, Deltas& dl,
+template <int NCAP, bool EV, bool GRID, class Src, class S>
+__device__ __forceinline__ bool handle_move(const Cfg& c, Key key, Src& src, Player& self,
+                                            Player& other, int32_t other_start,
+                                            const Npcs<NCAP>& npc, S& spawn, Deltas& dl,
                                             bool& err, int32_t self_iden, bool self_first,
                                             Events<EV>& ev) {
   const bool moving = self.move != ORX_MOVE_STAY;
@@ -653,7 +787,7 @@ __device__ __forceinline__ bool handle_move(const Cfg& c, Key key, uint32_t game
     if (step) ev.emit(ORX_EV_POSITION, self_iden, self.d, (tx & 0xFFFF) | (ty << 16));
   }
   if (stairs)
-    descend<NCAP, EV, GRID>(c, key, game, ep, self, other, other_start, npc, spawn, dl, err,
+    descend<NCAP, EV, GRID>(c, key, src, self, other, other_start, npc, spawn, dl, err,
                             self_iden, ev);
   return hit_npc;
 }
@@ -690,11 +824,11 @@ __device__ __forceinline__ void npc_hits(const Cfg& c, Npcs<NCAP>& npc, const Np
 }
 
 // One Updater.update for an in-progress game; p1.move/p2.move = raw moves.
-template <int NCAP, bool EV, bool GRID = false>
-__device__ __forceinline__ void tick_game(const Cfg& c, Key key, uint32_t game, uint32_t ep,
-                                          bool p1_first, bool writer, Player& p1, Player& p2,
-                                          Npcs<NCAP>& npc, const NpcMem& m, int32_t& tick,
-                                          int32_t& status, bool& err, Deltas& dl,
+template <int NCAP, bool EV, bool GRID, class Src>
+__device__ __forceinline__ void tick_game(const Cfg& c, Key key, Src& src, uint32_t game,
+                                          uint32_t ep, bool p1_first, bool writer, Player& p1,
+                                          Player& p2, Npcs<NCAP>& npc, const NpcMem& m,
+                                          int32_t& tick, int32_t& status, bool& err, Deltas& dl,
                                           Events<EV>& ev, int32_t& sep_start) {
   calc_pos(p1.x, p1.y, p1.move, p1.tx, p1.ty);         // updater.py:89-98
   if (blocked<GRID>(c, p1.lay, p1.tx, p1.ty)) p1.move = ORX_MOVE_STAY;
@@ -704,17 +838,16 @@ __device__ __forceinline__ void tick_game(const Cfg& c, Key key, uint32_t game, 
   // p1_first: the player shuffle (updater.py:114).  The NPC shuffle (:127)
   // draws later words of the same per-tick stream and only orders Stay-ing
   // NPCs, so it is unobservable and skipped.
-  Stream spawn;
-  spawn.init(game, ep, (uint32_t)tick, tag(PUR_SPAWN, 0));
+  auto&& spawn = src.spawn(tick);
   Player A = pick(p1_first, p1, p2);
   Player Bp = pick(p1_first, p2, p1);
   const int32_t a_start = p1_first ? c.d1 : c.d2;
   const int32_t b_start = p1_first ? c.d2 : c.d1;
   const int32_t a_iden = p1_first ? 1 : 2;
-  const bool hA = handle_move<NCAP, EV, GRID>(c, key, game, ep, A, Bp, b_start, npc, spawn, dl, err, a_iden, true,
-                              ev);
-  const bool hB = handle_move<NCAP, EV, GRID>(c, key, game, ep, Bp, A, a_start, npc, spawn, dl, err, 3 - a_iden,
-                              false, ev);
+  const bool hA = handle_move<NCAP, EV, GRID>(c, key, src, A, Bp, b_start, npc, spawn, dl, err,
+                                              a_iden, true, ev);
+  const bool hB = handle_move<NCAP, EV, GRID>(c, key, src, Bp, A, a_start, npc, spawn, dl, err,
+                                              3 - a_iden, false, ev);
   if (NCAP > 0 && (hA || hB)) {
     // NPCs never move and are swept only after both moves: the slots found at
     // the targets now are the ones that were attacked.
@@ -760,6 +893,17 @@ __device__ __forceinline__ void tick_game(const Cfg& c, Key key, uint32_t game, 
     dl.ret += status == ORX_PLAYER1_WIN ? 1 : status == ORX_PLAYER2_WIN ? -1 : 0;
     dl.eps += (status >= ORX_PLAYER1_WIN && status <= ORX_TIE) ? 1 : 0;
   }
+}
+
+template <int NCAP, bool EV, bool GRID = false>
+__device__ __forceinline__ void tick_game(const Cfg& c, Key key, uint32_t game, uint32_t ep,
+                                          bool p1_first, bool writer, Player& p1, Player& p2,
+                                          Npcs<NCAP>& npc, const NpcMem& m, int32_t& tick,
+                                          int32_t& status, bool& err, Deltas& dl,
+                                          Events<EV>& ev, int32_t& sep_start) {
+  PhiloxSrc src{key, game, ep};
+  tick_game<NCAP, EV, GRID>(c, key, src, game, ep, p1_first, writer, p1, p2, npc, m, tick, status,
+                            err, dl, ev, sep_start);
 }
 
 // ---------------------------------------------------------------------------
@@ -1284,6 +1428,250 @@ __global__ void __launch_bounds__(128) rollout_pc_kernel(
 
 // Staircases of arbitrary (game, episode, depth, generation) dungeons, for
 // materializing World.dungeons (compat views, wire codec).
+
+// ---------------------------------------------------------------------------
+// Stock-seed mode kernels (cfg.rng = ORX_RNG_MT19937)
+// ---------------------------------------------------------------------------
+// random.seed(n) (CPython random_seed -> init_by_array over the 32-bit words
+// of n) and np.random.seed(n) (numpy mt19937_seed = init_genrand) for
+// n = seed + global game id; both indices at 624 (the first draw twists).
+__global__ void __launch_bounds__(256) mt_seed_kernel(orx_state_t st, uint32_t B, uint64_t seed,
+                                                      uint32_t off) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B) return;
+  const uint64_t n = seed + off + i;
+  uint32_t* np = st.mt_np + i;
+  uint32_t x = (uint32_t)n;
+  for (uint32_t k = 0; k < 624; ++k) {
+    np[(size_t)k * B] = x;
+    x = 1812433253u * (x ^ (x >> 30)) + k + 1u;
+  }
+  np[624 * (size_t)B] = 624;
+  uint32_t* py = st.mt_py + i;
+  const uint32_t key[2] = {(uint32_t)n, (uint32_t)(n >> 32)};
+  const uint32_t klen = key[1] ? 2u : 1u;
+  x = 19650218u;  // init_genrand(19650218)
+  for (uint32_t k = 0; k < 624; ++k) {
+    py[(size_t)k * B] = x;
+    x = 1812433253u * (x ^ (x >> 30)) + k + 1u;
+  }
+  uint32_t idx = 1, j = 0, prev = py[0];
+  for (uint32_t k = 624; k; --k) {
+    const uint32_t v = (py[(size_t)idx * B] ^ ((prev ^ (prev >> 30)) * 1664525u)) + key[j] + j;
+    py[(size_t)idx * B] = v;
+    prev = v;
+    ++idx; ++j;
+    if (idx >= 624) { py[0] = prev; idx = 1; }
+    if (j >= klen) j = 0;
+  }
+  for (uint32_t k = 623; k; --k) {
+    const uint32_t v = (py[(size_t)idx * B] ^ ((prev ^ (prev >> 30)) * 1566083941u)) - idx;
+    py[(size_t)idx * B] = v;
+    prev = v;
+    ++idx;
+    if (idx >= 624) { py[0] = prev; idx = 1; }
+  }
+  py[0] = 0x80000000u;
+  py[624 * (size_t)B] = 624;
+  for (uint32_t k = 0; k < ORX_DSTORE; ++k) st.dstore[(size_t)(2 * k) * B + i] = -1;
+}
+
+// RandomBot.move = random.choice(list(Move)) = Move(1 + _randbelow(5))
+// (randombot.py:21) from the game's CPython stream; StaircaseBot as usual.
+__device__ __forceinline__ void mt_policy_pair(MtStream& py, int32_t pol1, int32_t pol2,
+                                               const Player& p1, const Player& p2, int32_t& a1,
+                                               int32_t& a2, bool& err) {
+  int32_t r[2] = {ORX_MOVE_STAY, ORX_MOVE_STAY};
+  int nr = 0;
+  if (pol1 == ORX_POLICY_RANDOM) r[nr++] = 1 + (int32_t)py_randbelow(py, Key{0, 0}, 5u, err);
+  if (pol2 == ORX_POLICY_RANDOM) r[nr++] = 1 + (int32_t)py_randbelow(py, Key{0, 0}, 5u, err);
+  assign_moves(pol1, pol2, r[0], r[1], p1, p2, a1, a2);
+}
+
+// random.shuffle of the two players (updater.py:114: player 1 first iff
+// _randbelow(2) == 1), then of the NPC updents (:127), whose order cannot
+// matter (they Stay) but whose draws advance the stream.
+template <int NCAP>
+__device__ __forceinline__ bool mt_shuffles(MtStream& py, const Npcs<NCAP>& npc, bool& err) {
+  const bool p1_first = py_randbelow(py, Key{0, 0}, 2u, err) == 1u;
+  if constexpr (NCAP > 0)
+    for (int32_t n = __popc(npc.alive) - 1; n >= 1; --n)
+      py_randbelow(py, Key{0, 0}, (uint32_t)n + 1u, err);
+  return p1_first;
+}
+
+template <int NCAP, bool GRID>
+__global__ void __launch_bounds__(256) mt_reset_kernel(orx_cfg_t hc, orx_state_t st,
+                                                       const uint8_t* __restrict__ mask,
+                                                       uint32_t B) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B) return;
+  if (mask && !mask[i]) return;
+  const Cfg c = make_cfg(hc, st);
+  MtSrc src;
+  src.open(st, B, i);
+  Player p1, p2;
+  Npcs<NCAP> npc;
+  int32_t tick, status;
+  setup_game<NCAP, GRID>(c, Key{0, 0}, src, p1, p2, npc, tick, status);
+  src.close();
+  store_players<GRID>(st, B, i, p1, p2, true);
+  st.tick[i] = tick;
+  st.status[i] = status;
+  if (c.ext & ORX_EXT_SEPARATION_DAMAGE) st.sep_start[i] = -1;
+  if constexpr (NCAP > 0) {
+    st.npc_alive[i] = npc.alive;
+    store_new_npcs(st, c, B, i, npc);
+  }
+}
+
+__global__ void __launch_bounds__(256) mt_policy_kernel(orx_state_t st, int32_t pol1,
+                                                        int32_t pol2,
+                                                        int8_t* __restrict__ actions,
+                                                        uint32_t B) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B) return;
+  Player p1, p2;
+  p1.x = st.p_x[i]; p2.x = st.p_x[B + i];
+  p1.y = st.p_y[i]; p2.y = st.p_y[B + i];
+  p1.sx = st.st_x[i]; p2.sx = st.st_x[B + i];
+  p1.sy = st.st_y[i]; p2.sy = st.st_y[B + i];
+  uint16_t* out = reinterpret_cast<uint16_t*>(actions);
+  int32_t a1 = ORX_MOVE_STAY, a2 = ORX_MOVE_STAY;
+  if (pol1 == ORX_POLICY_NONE || pol2 == ORX_POLICY_NONE) {
+    const uint16_t prev = out[i];
+    a1 = (int8_t)(prev & 0xFF);
+    a2 = (int8_t)(prev >> 8);
+  }
+  MtStream py;
+  py.open(st.mt_py, B, i);
+  bool err = false;
+  mt_policy_pair(py, pol1, pol2, p1, p2, a1, a2, err);
+  py.close();
+  out[i] = pack_actions(a1, a2);
+}
+
+template <int NCAP, bool EV, bool GRID>
+__global__ void __launch_bounds__(256) mt_step_kernel(orx_cfg_t hc, orx_state_t st,
+                                                      const int8_t* __restrict__ actions,
+                                                      uint32_t B, Key key, uint32_t off,
+                                                      int32_t* __restrict__ events,
+                                                      int32_t* __restrict__ n_events) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B) return;
+  const Cfg c = make_cfg(hc, st);
+  const uint32_t game = off + i;
+  int32_t status = st.status[i];
+  Npcs<NCAP> npc;
+  Player p1, p2;
+  if (status != ORX_IN_PROGRESS) {
+    if (EV) n_events[i] = 0;
+    if (!c.autoreset) return;
+    MtSrc src;
+    src.open(st, B, i);
+    const uint32_t ep = (uint32_t)st.episode[i] + 1u;
+    int32_t tick;
+    setup_game<NCAP, GRID>(c, key, src, p1, p2, npc, tick, status);
+    src.close();
+    store_players<GRID>(st, B, i, p1, p2, true);
+    st.tick[i] = tick;
+    st.status[i] = status;
+    st.episode[i] = (int32_t)ep;
+    if (c.ext & ORX_EXT_SEPARATION_DAMAGE) st.sep_start[i] = -1;
+    if constexpr (NCAP > 0) {
+      st.npc_alive[i] = npc.alive;
+      store_new_npcs(st, c, B, i, npc);
+    }
+    return;
+  }
+  const uint16_t a = reinterpret_cast<const uint16_t*>(actions)[i];
+  p1.move = (int8_t)(a & 0xFF);
+  p2.move = (int8_t)(a >> 8);
+  if (!valid_move(p1.move) || !valid_move(p2.move)) {
+    st.status[i] = ORX_STATUS_BAD_ACTION;
+    if (EV) n_events[i] = 0;
+    return;
+  }
+  const uint32_t ep = (uint32_t)st.episode[i];
+  int32_t tick = st.tick[i];
+  load_players<GRID>(st, B, i, p1, p2);
+  load_npcs(st, c, B, i, npc);
+  const NpcMem m{st.npc_pos, st.npc_health, B, i};
+  Deltas dl = {0, 0, 0, 0, 0, 0};
+  Events<EV> ev{EV ? events + (size_t)i * ORX_MAX_EVENTS * 4 : nullptr, 0};
+  bool err = false;
+  MtSrc src;
+  src.open(st, B, i);
+  const bool p1_first = mt_shuffles(src.py, npc, err);
+  int32_t sep = (c.ext & ORX_EXT_SEPARATION_DAMAGE) ? st.sep_start[i] : -1;
+  tick_game<NCAP, EV, GRID>(c, key, src, game, ep, p1_first, true, p1, p2, npc, m, tick, status,
+                            err, dl, ev, sep);
+  src.close();
+  if (c.ext & ORX_EXT_SEPARATION_DAMAGE) st.sep_start[i] = sep;
+  store_players<GRID>(st, B, i, p1, p2, dl.descend != 0);
+  st.tick[i] = tick;
+  st.status[i] = status;
+  if (NCAP > 0 && dl.npc_death) st.npc_alive[i] = npc.alive;
+  flush_deltas(st, B, i, dl);
+  if (EV) n_events[i] = ev.n;
+}
+
+template <int NCAP, bool GRID>
+__global__ void __launch_bounds__(256) mt_rollout_kernel(orx_cfg_t hc, orx_state_t st,
+                                                         int32_t pol1, int32_t pol2,
+                                                         int32_t n_ticks,
+                                                         int32_t* __restrict__ obs,
+                                                         int8_t* __restrict__ act, uint32_t B,
+                                                         Key key, uint32_t off) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B) return;
+  const Cfg c = make_cfg(hc, st);
+  const uint32_t game = off + i;
+  Player p1, p2;
+  load_players<GRID>(st, B, i, p1, p2);
+  int32_t tick = st.tick[i];
+  int32_t status = st.status[i];
+  uint32_t ep = (uint32_t)st.episode[i];
+  Npcs<NCAP> npc;
+  load_npcs(st, c, B, i, npc);
+  const NpcMem m{st.npc_pos, st.npc_health, B, i};
+  Deltas dl = {0, 0, 0, 0, 0, 0};
+  int32_t sep = (c.ext & ORX_EXT_SEPARATION_DAMAGE) ? st.sep_start[i] : -1;
+  bool stairs_dirty = false, npc_dirty = false;
+  MtSrc src;
+  src.open(st, B, i);
+  for (int32_t t = 0; t < n_ticks; ++t) {
+    int32_t a1 = ORX_MOVE_STAY, a2 = ORX_MOVE_STAY;
+    bool err = false;
+    mt_policy_pair(src.py, pol1, pol2, p1, p2, a1, a2, err);
+    if (status == ORX_IN_PROGRESS) {
+      p1.move = a1; p2.move = a2;
+      const int32_t descents = dl.descend;
+      const bool p1_first = mt_shuffles(src.py, npc, err);
+      Events<false> ev{nullptr, 0};
+      tick_game<NCAP, false, GRID>(c, key, src, game, ep, p1_first, true, p1, p2, npc, m, tick,
+                                   status, err, dl, ev, sep);
+      stairs_dirty |= dl.descend != descents;
+    } else if (c.autoreset) {
+      ep += 1;
+      setup_game<NCAP, GRID>(c, key, src, p1, p2, npc, tick, status);
+      if constexpr (NCAP > 0) store_new_npcs(st, c, B, i, npc);
+      stairs_dirty = true;
+      npc_dirty = true;
+      sep = -1;
+    }
+    store_traj<false>(obs, act, t, B, i, p1, p2, tick, status, a1, a2);
+  }
+  src.close();
+  store_players<GRID>(st, B, i, p1, p2, stairs_dirty);
+  st.tick[i] = tick;
+  st.status[i] = status;
+  st.episode[i] = (int32_t)ep;
+  if (c.ext & ORX_EXT_SEPARATION_DAMAGE) st.sep_start[i] = sep;
+  if (NCAP > 0 && (npc_dirty || dl.npc_death)) st.npc_alive[i] = npc.alive;
+  flush_deltas(st, B, i, dl);
+}
+
 template <bool GRID>
 __global__ void __launch_bounds__(256) stairs_kernel(orx_cfg_t hc, orx_state_t st,
                                                      const uint32_t* __restrict__ games,
@@ -1350,6 +1738,10 @@ int check_cfg(const orx_cfg_t* c) {
     return fail(ORX_EINVAL, "unknown extension flag");
   if ((c->flags & ORX_EXT_SEPARATION_DAMAGE) && c->sep_period < 1)
     return fail(ORX_EINVAL, "separation damage needs sep_period >= 1");
+  if (c->rng != ORX_RNG_PHILOX && c->rng != ORX_RNG_MT19937)
+    return fail(ORX_EINVAL, "unknown rng mode");
+  if (c->rng == ORX_RNG_MT19937 && (c->width > 256 || c->height > 256))
+    return fail(ORX_EINVAL, "stock-seed mode stores staircases 8+8 bits: W, H <= 256");
   return ORX_OK;
 }
 
@@ -1366,6 +1758,8 @@ int check_state(const orx_cfg_t* c, const orx_state_t* s, bool full) {
     return fail(ORX_EINVAL, "n_layouts > 0 needs p_layout and the bank_* arrays");
   if ((c->flags & ORX_EXT_SEPARATION_DAMAGE) && !s->sep_start)
     return fail(ORX_EINVAL, "separation damage needs sep_start");
+  if (c->rng == ORX_RNG_MT19937 && (!s->mt_py || !s->mt_np || !s->dstore))
+    return fail(ORX_EINVAL, "stock-seed mode needs mt_py, mt_np and dstore");
   return ORX_OK;
 }
 
@@ -1429,6 +1823,20 @@ int orx_validate_cfg(const orx_cfg_t* cfg) {
   return r;
 }
 
+int orx_seed_mt(const orx_cfg_t* cfg, const orx_state_t* st, int64_t n_games, uint64_t seed,
+                int64_t game_offset, void* stream) {
+  int r;
+  if ((r = check_cfg(cfg)) || (r = check_sizes(n_games, game_offset))) return r;
+  if (cfg->rng != ORX_RNG_MT19937) return fail(ORX_EINVAL, "orx_seed_mt needs cfg->rng = ORX_RNG_MT19937");
+  if (seed + (uint64_t)game_offset + (uint64_t)n_games < seed)
+    return fail(ORX_EINVAL, "seed + game id overflows 64 bits");
+  if (n_games == 0) return ORX_OK;
+  if ((r = check_state(cfg, st, false))) return r;
+  hipLaunchKernelGGL(mt_seed_kernel, grid_for(n_games), dim3(kBlock), 0, (hipStream_t)stream, *st,
+                     (uint32_t)n_games, seed, (uint32_t)game_offset);
+  return launch_status("orx_seed_mt");
+}
+
 int orx_reset(const orx_cfg_t* cfg, const orx_state_t* st, const uint8_t* mask, int64_t n_games,
               uint64_t seed, int64_t game_offset, void* stream) {
   int r;
@@ -1440,6 +1848,15 @@ int orx_reset(const orx_cfg_t* cfg, const orx_state_t* st, const uint8_t* mask, 
   const Key k = make_key(seed);
   const int nc = ncap_for(cfg->n_npcs);
   const bool grid = cfg->n_layouts > 0;
+  if (cfg->rng == ORX_RNG_MT19937) {
+#define ORX_RESET(N, G)                                                                         \
+  if (nc == N && grid == G)                                                                     \
+    hipLaunchKernelGGL((mt_reset_kernel<N, G>), grid_for(B), dim3(kBlock), 0, s, *cfg, *st, mask, B);
+    ORX_RESET(0, false) ORX_RESET(8, false) ORX_RESET(16, false)
+    ORX_RESET(0, true) ORX_RESET(8, true) ORX_RESET(16, true)
+#undef ORX_RESET
+    return launch_status("orx_reset");
+  }
 #define ORX_RESET(N, G)                                                                         \
   if (nc == N && grid == G)                                                                     \
     hipLaunchKernelGGL((reset_kernel<N, G>), grid_for(B), dim3(kBlock), 0, s, *cfg, *st, mask, B, \
@@ -1465,10 +1882,16 @@ static int launch_step(const orx_cfg_t* cfg, const orx_state_t* st, const int8_t
   const Key k = make_key(seed);
   const int nc = ncap_for(cfg->n_npcs);
   const bool grid = cfg->n_layouts > 0;
+  const bool mt = cfg->rng == ORX_RNG_MT19937;
 #define ORX_STEP(NC, E, G)                                                                      \
-  if (nc == NC && ev == E && grid == G)                                                        \
-    hipLaunchKernelGGL((step_kernel<NC, E, G>), grid_for(B), dim3(kBlock), 0, s, *cfg, *st,     \
-                       actions, B, k, off, events, n_events);
+  if (nc == NC && ev == E && grid == G) {                                                      \
+    if (mt)                                                                                     \
+      hipLaunchKernelGGL((mt_step_kernel<NC, E, G>), grid_for(B), dim3(kBlock), 0, s, *cfg, *st, \
+                         actions, B, k, off, events, n_events);                                 \
+    else                                                                                        \
+      hipLaunchKernelGGL((step_kernel<NC, E, G>), grid_for(B), dim3(kBlock), 0, s, *cfg, *st,   \
+                         actions, B, k, off, events, n_events);                                 \
+  }
   ORX_STEP(0, false, false) ORX_STEP(0, true, false) ORX_STEP(8, false, false)
   ORX_STEP(8, true, false) ORX_STEP(16, false, false) ORX_STEP(16, true, false)
   ORX_STEP(0, false, true) ORX_STEP(0, true, true) ORX_STEP(8, false, true)
@@ -1503,6 +1926,11 @@ int orx_policy(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p1, i
   if ((r = check_state(cfg, st, false))) return r;
   if (!actions) return fail(ORX_EINVAL, "actions is NULL");
   const uint32_t B = (uint32_t)n_games, off = (uint32_t)game_offset;
+  if (cfg->rng == ORX_RNG_MT19937) {
+    hipLaunchKernelGGL(mt_policy_kernel, grid_for(B), dim3(kBlock), 0, (hipStream_t)stream, *st,
+                       policy_p1, policy_p2, actions, B);
+    return launch_status("orx_policy");
+  }
   hipLaunchKernelGGL(policy_kernel, grid_for(B), dim3(kBlock), 0, (hipStream_t)stream, *st,
                      policy_p1, policy_p2, actions, B, make_key(seed), off);
   return launch_status("orx_policy");
@@ -1526,11 +1954,21 @@ int orx_rollout(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p1, 
   // the buffer-addressed fast path needs one tick's obs rows below 2 GiB; a
   // dungeon bank runs the generic plain kernel (tile lookups)
   const bool grid = cfg->n_layouts > 0;
+  const int nc = ncap_for(cfg->n_npcs);
+  if (cfg->rng == ORX_RNG_MT19937) {
+#define ORX_ROLLOUT(N, G)                                                                       \
+  if (nc == N && grid == G)                                                                     \
+    hipLaunchKernelGGL((mt_rollout_kernel<N, G>), grid_for(B), dim3(kBlock), 0, s, *cfg, *st,   \
+                       policy_p1, policy_p2, n_ticks, obs, act, B, k, off);
+    ORX_ROLLOUT(0, false) ORX_ROLLOUT(8, false) ORX_ROLLOUT(16, false)
+    ORX_ROLLOUT(0, true) ORX_ROLLOUT(8, true) ORX_ROLLOUT(16, true)
+#undef ORX_ROLLOUT
+    return launch_status("orx_rollout");
+  }
   const bool rr = !grid && cfg->flags == 0 && policy_p1 == ORX_POLICY_RANDOM &&
                   policy_p2 == ORX_POLICY_RANDOM && obs && act &&
                   (uint64_t)B * ORX_OBS_FIELDS * 4u < (1ull << 31);
   const bool pc = !grid && use_pc_rollout(B);
-  const int nc = ncap_for(cfg->n_npcs);
 #define ORX_ROLLOUT(N, R, G)                                                                    \
   if (nc == N && rr == R && grid == G) {                                                        \
     if (pc)                                                                                     \
@@ -1554,6 +1992,8 @@ int orx_dungeon_spawn(const orx_cfg_t* cfg, const orx_state_t* st, const uint32_
   int r;
   if ((r = check_cfg(cfg))) return r;
   if (n < 0 || n > 0x7FFFFFFFLL - kBlock) return fail(ORX_EINVAL, "bad n");
+  if (cfg->rng == ORX_RNG_MT19937)
+    return fail(ORX_EINVAL, "stock-seed dungeons come from the games' numpy streams, not keys");
   if (n == 0) return ORX_OK;
   if (!game_ids || !episodes || !depths || !gens || !sx || !sy)
     return fail(ORX_EINVAL, "a pointer is NULL");

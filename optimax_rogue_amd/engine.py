@@ -17,7 +17,7 @@ import torch
 
 from . import _lib
 from .config import EnvConfig
-from .enums import EXT_SEPARATION_DAMAGE, MAX_EVENTS, N_COUNTERS, OBS_FIELDS, Policy
+from .enums import DSTORE, EXT_SEPARATION_DAMAGE, MAX_EVENTS, RNG_MT19937, N_COUNTERS, OBS_FIELDS, Policy
 
 STATE_FIELDS = ("p_x", "p_y", "p_depth", "p_health", "st_x", "st_y", "tick", "status", "episode",
                 "ret_sum", "ep_count", "counters", "npc_pos", "npc_health", "npc_alive")
@@ -88,7 +88,17 @@ class BatchedEngine:
         if int(cfg.flags) & EXT_SEPARATION_DAMAGE:
             self.sep_start = torch.full((B,), -1, dtype=torch.int32, device=device)
             ptrs["sep_start"] = self.sep_start.data_ptr()
+        # stock-seed mode: each game's CPython random and numpy RandomState
+        # (MT19937 key words + index, column per game) and its remembered
+        # dungeons (depth, sx | sy << 8 | (layout + 1) << 16) by depth mod DSTORE
+        self.mt_py = self.mt_np = self.dstore = None
+        if int(cfg.rng) == RNG_MT19937:
+            self.mt_py, self.mt_np = z(625, B), z(625, B)
+            self.dstore = z(DSTORE, 2, B)
+            ptrs.update({f: getattr(self, f).data_ptr() for f in ("mt_py", "mt_np", "dstore")})
         self._st = _lib.OrxState(**ptrs)
+        if self.mt_py is not None:
+            self.seed_rng()
         if reset:
             self.reset()
 
@@ -102,6 +112,13 @@ class BatchedEngine:
         _lib.check(name, code)
 
     # -- the C-ABI entry points -------------------------------------------
+    def seed_rng(self, seed: Optional[int] = None) -> None:
+        """Stock-seed mode: random.seed(n) and np.random.seed(n) for every game,
+        n = seed + global game id (orx_seed_mt)."""
+        if seed is not None:
+            self.seed = int(seed)
+        self._call("orx_seed_mt", self.B, self.seed, self.game_offset, self._stream())
+
     def reset(self, mask: Optional[torch.Tensor] = None, episode=None) -> None:
         """GameStartGenerator.setup_game for the masked games (all if None).
 
@@ -174,6 +191,10 @@ class BatchedEngine:
             out["p_layout"] = self.p_layout.cpu().numpy()
         if self.sep_start is not None:
             out["sep_start"] = self.sep_start.cpu().numpy()
+        if self.mt_py is not None:
+            for f in ("mt_py", "mt_np"):
+                out[f] = getattr(self, f).cpu().numpy().view(np.uint32)
+            out["dstore"] = self.dstore.cpu().numpy()
         for f in STATE_FIELDS:
             a = getattr(self, f).cpu().numpy()
             if f == "npc_pos":
@@ -191,6 +212,11 @@ class BatchedEngine:
             self.p_layout.copy_(torch.from_numpy(np.ascontiguousarray(snap["p_layout"], np.int16)))
         if self.sep_start is not None and "sep_start" in snap:
             self.sep_start.copy_(torch.from_numpy(np.ascontiguousarray(snap["sep_start"], np.int32)))
+        if self.mt_py is not None:
+            for f in ("mt_py", "mt_np", "dstore"):
+                if f in snap:
+                    a = np.ascontiguousarray(snap[f]).astype(np.uint32).view(np.int32)
+                    getattr(self, f).copy_(torch.from_numpy(a.reshape(getattr(self, f).shape)))
         for f in STATE_FIELDS:
             if f not in snap:
                 continue
@@ -240,7 +266,19 @@ class BatchedEngine:
         snap = self.snapshot() if snap is None else snap
         idx = range(self.B) if indices is None else indices
         extra = {}
-        if full_world:
+        if full_world and self.dstore is not None:
+            # stock-seed mode: the remembered dungeons are the world
+            ds = snap["dstore"]
+            for i in idx:
+                d1, d2 = int(snap["p_depth"][0][i]), int(snap["p_depth"][1][i])
+                for d in world_depths(self.cfg, d1, d2):
+                    if d in (d1, d2):
+                        continue
+                    if int(ds[d % DSTORE, 0, i]) != d:
+                        raise RuntimeError(f"game {i}: depth {d} not in the dungeon store")
+                    v = int(ds[d % DSTORE, 1, i])
+                    extra.setdefault(i, {})[d] = (v & 0xFF, (v >> 8) & 0xFF, (v >> 16) - 1)
+        elif full_world:
             req = []
             for i in idx:
                 d1, d2 = int(snap["p_depth"][0][i]), int(snap["p_depth"][1][i])

@@ -65,6 +65,11 @@ STATUS_RNG_EXHAUSTED = 17
 EXT_SEPARATION_DAMAGE = 1
 EXT_RANDOM_DOUBLE_DEATH = 2
 
+# EnvConfig.rng (orx_cfg_t.rng, include/orx.h ORX_RNG_*)
+RNG_PHILOX = 0
+RNG_MT19937 = 1
+DSTORE = 256        # ORX_DSTORE: remembered dungeons per game in stock-seed mode
+
 # per-game event counter rows (include/orx.h ORX_CNT_*)
 CNT_COMBAT, CNT_DESCEND, CNT_DUNGEON, CNT_NPC_DEATH = range(4)
 N_COUNTERS = 4

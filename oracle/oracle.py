@@ -19,7 +19,8 @@ LIB_PATH = os.path.join(HERE, "liborx_oracle.so")
 # Field order of orx_cfg_t (include/orx.h); tests check it against the header.
 CFG_FIELDS = ["width", "height", "despawn", "max_ticks", "start_mode", "p1_depth", "p2_depth",
               "n_npcs", "npc_health", "npc_damage", "npc_armor", "player_health",
-              "player_damage", "player_armor", "autoreset", "flags", "n_layouts", "sep_period"]
+              "player_damage", "player_armor", "autoreset", "flags", "n_layouts", "sep_period",
+              "rng"]
 
 
 class _Cfg(ctypes.Structure):
@@ -29,7 +30,7 @@ class _Cfg(ctypes.Structure):
 DEFAULT_CFG = dict(width=32, height=32, despawn=1, max_ticks=1000, start_mode=1, p1_depth=0,
                    p2_depth=0, n_npcs=0, npc_health=3, npc_damage=1, npc_armor=0,
                    player_health=10, player_damage=2, player_armor=1, autoreset=1, flags=0,
-                   n_layouts=0, sep_period=0)
+                   n_layouts=0, sep_period=0, rng=0)
 
 _lib = None
 
@@ -67,6 +68,7 @@ def lib():
         L.oracle_set_bank.argtypes = [vp, vp, i32]
         L.oracle_export_layout.argtypes = [vp, vp]
         L.oracle_export_sep.argtypes = [vp, vp]
+        L.oracle_seed_mt.argtypes = [vp, u64]
         _lib = L
     return _lib
 
@@ -99,6 +101,8 @@ class Oracle:
         self._c = _Cfg(**full)
         self._h = lib().oracle_new(ctypes.byref(self._c), self.B, int(seed), int(game_offset),
                                    int(record_events))
+        if full["rng"] == 1:   # stock-seed mode: random.seed / np.random.seed(seed + gid)
+            lib().oracle_seed_mt(self._h, int(seed))
         self.layouts = None
         if layouts is not None:
             self.layouts = np.ascontiguousarray(layouts, np.uint8)

@@ -35,6 +35,12 @@ output:
   ``get_random_unblocked``, ``staircase`` and ``handle_move`` then run on
   walls, open borders and several staircases.  The bank is saved with the
   fixture.
+* Stock-seed cases (``rng=1``) inject nothing: every game is a reference
+  process of its own seeded with ``random.seed(n)`` and ``np.random.seed(n)``
+  (n = seed + global game id) -- the module-level CPython ``random`` and numpy
+  ``RandomState`` run unmodified (their states are swapped in and out per
+  game), dungeons come from the stock ``EmptyDungeonGenerator``.  The
+  engine's ORX_RNG_MT19937 mode must reproduce them from the seed alone.
 * NPCs ("enemies") come from ``NpcGameStart``, a ``GameStartGenerator``
   (worldgen.py:47-58) that calls the reference's Together/Separated
   ``setup_game`` and then places K NPCs with the reference's
@@ -178,7 +184,31 @@ def import_reference():
         updater=updater_mod, worldgen=worldgen_mod, world=world_mod,
         randombot=randombot_mod, staircasebot=staircasebot_mod, state=state_mod,
         entities=entities_mod, updates=updates_mod, moves=moves_mod,
-        pyrand=pyrand, nprand=nprand)
+        pyrand=pyrand, nprand=nprand, injected=(pyrand, NpProxy(nprand)))
+
+
+@contextlib.contextmanager
+def stock_rng(R, h):
+    """Runs reference code with the real module-level random / np.random
+    holding game h's own states (a separate seeded process per game)."""
+    mods_py = (R.updater, R.randombot)
+    mods_np = (R.worldgen, R.world)
+    saved = [m.random for m in mods_py], [m.np for m in mods_np]
+    for m in mods_py:
+        m.random = random
+    for m in mods_np:
+        m.np = np
+    random.setstate(h.py_state)
+    np.random.set_state(h.np_state)
+    try:
+        yield
+    finally:
+        h.py_state = random.getstate()
+        h.np_state = np.random.get_state()
+        for m, v in zip(mods_py, saved[0]):
+            m.random = v
+        for m, v in zip(mods_np, saved[1]):
+            m.np = v
 
 
 # --------------------------------------------------------------------------
@@ -191,6 +221,11 @@ class Harness:
         self.R, self.cfg, self.seed, self.gid = R, cfg, seed, game_id
         self.episode = 0
         self.gens = {}
+        self.stock = cfg.get("rng", 0) == 1
+        if self.stock:
+            n = seed + game_id
+            self.py_state = random.Random(n).getstate()
+            self.np_state = np.random.RandomState(n).get_state()
         R_ = R
 
         harness = self
@@ -240,8 +275,21 @@ class Harness:
                     R_.nprand.stream = saved
                 return R_.world.Dungeon(self.layouts[idx].astype(np.int32))
 
+        class StockBankGenerator(R_.worldgen.DungeonGenerator):
+            def __init__(self, width, height, layouts):
+                super().__init__(width, height)
+                self.layouts = layouts
+
+            def spawn_dungeon(self, depth):
+                idx = R_.worldgen.np.random.randint(len(self.layouts))
+                return R_.world.Dungeon(self.layouts[idx].astype(np.int32))
+
         self.layouts = cfg.get("layouts")
-        if self.layouts is not None:
+        if self.stock:
+            self.dgen = (StockBankGenerator(cfg["width"], cfg["height"], self.layouts)
+                         if self.layouts is not None
+                         else R_.worldgen.EmptyDungeonGenerator(cfg["width"], cfg["height"]))
+        elif self.layouts is not None:
             self.dgen = KeyedBankGenerator(cfg["width"], cfg["height"], self.layouts)
         else:
             self.dgen = KeyedDungeonGenerator(cfg["width"], cfg["height"])
@@ -270,12 +318,22 @@ class Harness:
 
     def setup(self):
         self.gens = {}
-        self.R.nprand.stream = Stream(self.seed, self.gid, self.episode, 0, PUR_INIT)
-        self.gs = self.start.setup_game()
+        if self.stock:
+            with stock_rng(self.R, self):
+                self.gs = self.start.setup_game()
+        else:
+            self.R.nprand.stream = Stream(self.seed, self.gid, self.episode, 0, PUR_INIT)
+            self.gs = self.start.setup_game()
         self.status = 1
 
     def policy(self, given=None):
+        if self.stock:
+            with stock_rng(self.R, self):
+                return self._policy(given)
         self.R.pyrand.stream = Stream(self.seed, self.gid, self.episode, self.gs.tick, PUR_POLICY)
+        return self._policy(given)
+
+    def _policy(self, given):
         acts = []
         for p in range(2):
             bot = self.bots[p]
@@ -295,10 +353,16 @@ class Harness:
                 self.setup()
             return events
         self.gs.on_tick()
-        R.pyrand.stream = Stream(self.seed, self.gid, self.episode, self.gs.tick, PUR_SHUFFLE)
-        R.nprand.stream = Stream(self.seed, self.gid, self.episode, self.gs.tick, PUR_SPAWN)
-        with contextlib.redirect_stdout(io.StringIO()):
-            res, upds = self.updater.update(self.gs, R.moves.Move(acts[0]), R.moves.Move(acts[1]))
+        if self.stock:
+            with stock_rng(R, self), contextlib.redirect_stdout(io.StringIO()):
+                res, upds = self.updater.update(self.gs, R.moves.Move(acts[0]),
+                                                R.moves.Move(acts[1]))
+        else:
+            R.pyrand.stream = Stream(self.seed, self.gid, self.episode, self.gs.tick, PUR_SHUFFLE)
+            R.nprand.stream = Stream(self.seed, self.gid, self.episode, self.gs.tick, PUR_SPAWN)
+            with contextlib.redirect_stdout(io.StringIO()):
+                res, upds = self.updater.update(self.gs, R.moves.Move(acts[0]),
+                                                R.moves.Move(acts[1]))
         self.status = int(res)
         if self.status == 2:
             self.ret_sum += 1
@@ -438,6 +502,17 @@ CASES = {
                                         policy=(2, 1), n_npcs=2,
                                         layouts=make_layouts(8, 9, 3, 102, n_stairs=(1, 3, 2))),
                                seed=13, games=16, ticks=320),
+    # stock-seed mode: the unmodified reference with random.seed(n) / np.random.seed(n)
+    "stock_c1_random": dict(cfg=dict(rng=1), seed=1000, games=4, ticks=1100),
+    "stock_npc_stairs": dict(cfg=dict(rng=1, width=7, height=8, max_ticks=150, n_npcs=3,
+                                      policy=(2, 1)), seed=2000, games=16, ticks=320),
+    "stock_unused_separated": dict(cfg=dict(rng=1, width=6, height=6, max_ticks=120, despawn=2,
+                                            start_mode=2, p1_depth=0, p2_depth=2, n_npcs=2,
+                                            policy=(1, 2)), seed=3000, games=16, ticks=260),
+    "stock_bank_unreachable": dict(cfg=dict(rng=1, width=8, height=9, max_ticks=150,
+                                            policy=(2, 2), n_npcs=2,
+                                            layouts=make_layouts(8, 9, 3, 104, n_stairs=(1, 2))),
+                                   seed=4000, games=12, ticks=320),
     # a one-layout bank (no dungeon draw), Separated start, both StaircaseBots
     "bank_single_separated": dict(cfg=dict(width=7, height=7, max_ticks=100, start_mode=2,
                                            p1_depth=1, p2_depth=0, policy=(2, 2),

@@ -34,6 +34,9 @@ class Fixture:
         self.T, self.G = self.actions.shape[:2]
         self.K = int(self.cfg["n_npcs"])
         self.policy = tuple(self.cfg["policy"])
+        # stock-seed fixture (cfg.rng = MT19937): bots and shuffles share each
+        # game's random stream, so a step must follow that tick's policy draws
+        self.stock = int(self.cfg.get("rng", 0)) == 1
         # explicit-grid cases: the dungeon bank ([L, W, H] Tile codes), else None
         self.layouts = self.z.get("layouts")
         wl = self.z["world_len"]

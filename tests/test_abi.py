@@ -38,7 +38,7 @@ def test_library_exports_every_declared_symbol(lib):
     decl = declared_functions()
     assert decl == sorted(["orx_abi_version", "orx_last_error", "orx_validate_cfg", "orx_reset",
                            "orx_step", "orx_step_events", "orx_policy", "orx_rollout",
-                           "orx_dungeon_stairs", "orx_dungeon_spawn"])
+                           "orx_dungeon_stairs", "orx_dungeon_spawn", "orx_seed_mt"])
     from optimax_rogue_amd import _lib
     assert sorted(_lib.EXPORTS) == decl
     for name in decl:
@@ -95,6 +95,9 @@ def test_validate_cfg(lib):
     # build extensions: known bits only; separation damage needs a period
     ok.append(EnvConfig(flags=3, sep_period=5))
     bad += [EnvConfig(flags=4), EnvConfig(flags=1, sep_period=0)]
+    # stock-seed word source (MT19937): staircases pack 8+8 bits
+    ok.append(EnvConfig(rng=1, n_npcs=3))
+    bad += [EnvConfig(rng=2), EnvConfig(rng=1, width=300, height=8)]
     for c in ok:
         assert lib.orx_validate_cfg(ctypes.byref(c.to_c())) == 0, c
     for c in bad:
@@ -110,7 +113,7 @@ def test_plain_c_consumer(lib, tmp_path):
                     "-Wl,-rpath," + os.path.join(ROOT, "optimax_rogue_amd")], check=True)
     r = subprocess.run([str(exe)], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert "sizeof(orx_cfg_t)=72" in r.stdout
+    assert "sizeof(orx_cfg_t)=76" in r.stdout
 
 
 def test_engine_refuses_cpu():

@@ -100,6 +100,9 @@ def test_engine_game_states_codec(name, oracle_lib):
                 else:
                     assert views[g] == oracle_view(o, g, cfg), (name, t, g)
         if t < fx.T:
+            if fx.stock:   # the bots' draws share each game's random stream
+                eng.policy(*fx.policy)
+                o.policy(*fx.policy)
             eng.step(acts[t].contiguous())
             o.step(fx.actions[t])
 

@@ -41,6 +41,8 @@ def test_golden_update_events(name):
     eng = _engine(fx.cfg, fx.G, fx.seed, fx.game_offset, layouts=fx.layouts)
     acts = torch.from_numpy(fx.actions).to(eng.device)
     for t in range(fx.T):
+        if fx.stock:
+            eng.policy(*fx.policy)   # the bots' draws share the game's random stream
         _, ev, n = eng.step(acts[t].contiguous(), events=True)
         ev, n = ev.cpu().numpy(), n.cpu().numpy()
         for g in range(fx.G):
@@ -57,6 +59,8 @@ def test_golden_step_given_actions(name):
     eng = _engine(fx.cfg, fx.G, fx.seed, fx.game_offset, layouts=fx.layouts)
     acts = torch.from_numpy(fx.actions).to(eng.device)
     for t in range(fx.T):
+        if fx.stock:
+            eng.policy(*fx.policy)
         eng.step(acts[t].contiguous())
     compare_state(eng.snapshot(), fx.state(fx.T), fx.K, f"{name} final")
 
@@ -127,8 +131,17 @@ ORACLE_CASES = {
                             max_ticks=300, flags=1, sep_period=4), (2, 1), 2048, 400, 17),
     "ext_double_death": (dict(width=4, height=5, max_ticks=0, player_health=1, flags=3,
                               sep_period=2), (1, 1), 2048, 200, 18),
+    # stock-seed mode (MT19937 per game, reference call order)
+    "stock_npc_unused": (dict(width=10, height=9, n_npcs=4, despawn=2, max_ticks=150, rng=1),
+                         (1, 2), 2048, 400, 19),
+    "stock_c5_stairs": (dict(width=128, height=128, rng=1), (2, 2), 1024, 600, 20),
+    "stock_bank_separated": (dict(width=12, height=10, n_npcs=2, start_mode=2, p1_depth=3,
+                                  p2_depth=0, max_ticks=200, rng=1), (2, 1), 2048, 400, 21),
+    "stock_ext": (dict(width=4, height=5, max_ticks=0, player_health=1, flags=3, sep_period=2,
+                       rng=1), (1, 1), 2048, 200, 23),
 }
-ORACLE_BANKS = {"bank_64_npc": (64, 64, 16, 21, (1,)), "bank_stairs_unused": (12, 10, 5, 22, (1, 3))}
+ORACLE_BANKS = {"bank_64_npc": (64, 64, 16, 21, (1,)), "bank_stairs_unused": (12, 10, 5, 22, (1, 3)),
+                "stock_bank_separated": (12, 10, 7, 24, (1, 2))}
 
 
 @pytest.mark.parametrize("name", sorted(ORACLE_CASES))
