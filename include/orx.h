@@ -18,9 +18,10 @@
  *  - Randomness is Philox4x32-10 keyed by (seed) with the counter
  *    (global game id, episode, tick-or-depth, purpose|block); global game id =
  *    game_offset + local index, so results do not depend on how games are
- *    sharded across GPUs.  The 32-bit words are consumed through the exact
- *    CPython random._randbelow / numpy RandomState.randint transforms used at
- *    the reference's draw sites ("Random streams").
+ *    sharded across GPUs.  The words are consumed through the exact CPython
+ *    random._randbelow / numpy RandomState.randint transforms used at the
+ *    reference's draw sites; a tick's CPython-random draws (bots, shuffles)
+ *    first take bits of one "tick block" ("Random streams").
  */
 #ifndef ORX_H
 #define ORX_H

@@ -57,7 +57,8 @@ namespace {
 // ---------------------------------------------------------------------------
 enum : uint32_t {
   PUR_INIT = 1, PUR_DUNGEON = 2, PUR_SHUFFLE = 3, PUR_SPAWN = 4, PUR_POLICY = 5,
-  PUR_RESOLVE = 6  // ORX_EXT_RANDOM_DOUBLE_DEATH
+  PUR_RESOLVE = 6,  // ORX_EXT_RANDOM_DOUBLE_DEATH
+  PUR_TICK = 7      // the tick's CPython-random bit reservoir (bots, shuffles)
 };
 constexpr uint32_t kWordCap = 4096;  // per stream; exceeding it stops the game
 constexpr int32_t kStartTick = 1;     // GameState.tick of a fresh game (worldgen.py:87,133)
@@ -627,43 +628,44 @@ __device__ __forceinline__ void descend(const Cfg& c, Key key, Src& src, Player&
 }
 
 // ---------------------------------------------------------------------------
-// Random words of one tick
+// Random bits of one tick
 // ---------------------------------------------------------------------------
-// The per-tick streams are consumed through two packed forms (8 words = two
-// Philox blocks; lanes still short after 8 words take the generic stream loop):
-//  * POLICY: RandomBot.move = Move(1 + randbelow(5)), k = 3: r = w >> 29 as
-//    3-bit fields, rejected iff r >= 5 (bit2 & (bit1 | bit0)); p1 then p2.
-//  * SHUFFLE: random.shuffle([p1, p2]) = randbelow(2), k = 2: r = w >> 30 as
-//    2-bit fields, accepted iff the high bit is clear; player 1 acts first iff
-//    the first accepted r == 1 (updater.py:114).
-// pack_words(b0, b1, 29 + s, 3 - s) with s = 0 (policy) or 1 (shuffle).
-__device__ __forceinline__ uint32_t pack_words(const W4& b0, const W4& b1, uint32_t sh,
-                                               uint32_t width) {
-  return (b0.a >> sh) | ((b0.b >> sh) << width) | ((b0.c >> sh) << (2 * width)) |
-         ((b0.d >> sh) << (3 * width)) | ((b1.a >> sh) << (4 * width)) |
-         ((b1.b >> sh) << (5 * width)) | ((b1.c >> sh) << (6 * width)) |
-         ((b1.d >> sh) << (7 * width));
+// A tick's CPython-random draws (getrandbits(k), k <= 32) come first from the
+// bit reservoir of ONE Philox block, the tick block (game, episode, tick,
+// TICK), consumed least-significant bits first; a draw that no longer fits
+// takes the top k bits of the next word of the purpose's own stream
+// (SHUFFLE / POLICY, from word 0).  DESIGN.md §4, make_golden.TickBits.
+//  * word a (32 bits): the updater's shuffles.  random.shuffle([p1, p2]) =
+//    randbelow(2), k = 2: 16 two-bit fields, accepted iff the high bit is
+//    clear; player 1 acts first iff the first accepted field == 1
+//    (updater.py:114).  All 16 rejected: 2^-16.
+//  * words b | c << 32 (64 bits): the bots.  RandomBot.move =
+//    Move(1 + randbelow(5)), k = 3: 21 three-bit fields, rejected iff >= 5
+//    (bit2 & (bit1 | bit0)); p1's draws then p2's.  Fewer than two accepted
+//    of 21: ~1e-8.
+// One block per game-tick (the per-purpose whole-word streams needed four).
+__device__ __forceinline__ W4 tick_block(Key key, uint32_t game, uint32_t ep, int32_t tick) {
+  return philox(game, ep, (uint32_t)tick, tag(PUR_TICK, 0), key);
+}
+__device__ __forceinline__ uint64_t policy_bits(const W4& tb) {
+  return (uint64_t)tb.b | ((uint64_t)tb.c << 32);
 }
 
-__device__ __forceinline__ W4 tick_block(Key key, uint32_t game, uint32_t ep, int32_t tick,
-                                         uint32_t purpose, uint32_t blk) {
-  return philox(game, ep, (uint32_t)tick, tag(purpose, 0) | blk, key);
-}
-
-__device__ __forceinline__ void moves_from_packed(uint32_t pk, int need, Key key, uint32_t game,
+__device__ __forceinline__ void moves_from_packed(uint64_t pk, int need, Key key, uint32_t game,
                                                   uint32_t ep, int32_t tick, int32_t& m0,
                                                   int32_t& m1, bool& err) {
-  constexpr uint32_t kF = 0x249249u;  // bit 0 of each 3-bit field
-  const uint32_t acc = ~((pk >> 2) & (pk | (pk >> 1))) & kF;
-  const uint32_t acc2 = acc & (acc - 1u);
-  m0 = (int32_t)((pk >> (__ffs(acc) - 1)) & 7u) + 1;
-  m1 = (int32_t)((pk >> (__ffs(acc2) - 1)) & 7u) + 1;
+  constexpr uint64_t kF = 0x1249249249249249ull;  // bit 0 of each 3-bit field (21 fields)
+  const uint64_t acc = ~((pk >> 2) & (pk | (pk >> 1))) & kF;
+  const uint64_t acc2 = acc & (acc - 1u);
+  // (| bit 63: a defined shift when the mask is empty; the value is then unused)
+  m0 = (int32_t)((pk >> __builtin_ctzll(acc | (1ull << 63))) & 7u) + 1;
+  m1 = (int32_t)((pk >> __builtin_ctzll(acc2 | (1ull << 63))) & 7u) + 1;
   const int got = acc == 0 ? 0 : acc2 == 0 ? 1 : 2;
-  if (got < need) {  // rare: continue the stream at word 8
+  if (got < need) {  // rare: the POLICY stream's words
     int g = got;
     Stream s;
-    s.init(game, ep, (uint32_t)tick, tag(PUR_POLICY, 0), 8);
-    for (uint32_t i = 8; i < kWordCap && g < need; ++i) {
+    s.init(game, ep, (uint32_t)tick, tag(PUR_POLICY, 0), 0);
+    for (uint32_t i = 0; i < kWordCap && g < need; ++i) {
       const uint32_t r = s.next(key) >> 29;
       if (r >= 5u) continue;
       if (g == 0) m0 = (int32_t)r + 1; else m1 = (int32_t)r + 1;
@@ -675,12 +677,12 @@ __device__ __forceinline__ void moves_from_packed(uint32_t pk, int need, Key key
 
 __device__ __forceinline__ bool first_from_packed(uint32_t pk, Key key, uint32_t game, uint32_t ep,
                                                   int32_t tick, bool& err) {
-  const uint32_t acc = ~(pk >> 1) & 0x5555u;
-  int res = acc ? (int)((pk >> (__ffs(acc) - 1)) & 1u) : -1;
-  if (res < 0) {  // rare (1/256): continue the stream at word 8
+  const uint32_t acc = ~(pk >> 1) & 0x55555555u;
+  int res = acc ? (int)((pk >> __builtin_ctz(acc | 0x80000000u)) & 1u) : -1;
+  if (res < 0) {  // rare (2^-16): the SHUFFLE stream's words
     Stream s;
-    s.init(game, ep, (uint32_t)tick, tag(PUR_SHUFFLE, 0), 8);
-    for (uint32_t i = 8; i < kWordCap && res < 0; ++i) {
+    s.init(game, ep, (uint32_t)tick, tag(PUR_SHUFFLE, 0), 0);
+    for (uint32_t i = 0; i < kWordCap && res < 0; ++i) {
       const uint32_t r = s.next(key) >> 30;
       if (r < 2u) res = (int)r;
     }
@@ -689,20 +691,9 @@ __device__ __forceinline__ bool first_from_packed(uint32_t pk, Key key, uint32_t
   return res == 1;
 }
 
-__device__ __forceinline__ uint32_t policy_packed(Key key, uint32_t game, uint32_t ep, int32_t tick) {
-  return pack_words(tick_block(key, game, ep, tick, PUR_POLICY, 0),
-                    tick_block(key, game, ep, tick, PUR_POLICY, 1), 29, 3);
-}
-
-__device__ __forceinline__ uint32_t shuffle_packed(Key key, uint32_t game, uint32_t ep,
-                                                   int32_t tick) {
-  return pack_words(tick_block(key, game, ep, tick, PUR_SHUFFLE, 0),
-                    tick_block(key, game, ep, tick, PUR_SHUFFLE, 1), 30, 2);
-}
-
 __device__ __forceinline__ bool p1_first_draw(Key key, uint32_t game, uint32_t ep, int32_t tick,
                                               bool& err) {
-  return first_from_packed(shuffle_packed(key, game, ep, tick), key, game, ep, tick, err);
+  return first_from_packed(tick_block(key, game, ep, tick).a, key, game, ep, tick, err);
 }
 
 // RandomBot / StaircaseBot moves for both players (policy codes ORX_POLICY_*)
@@ -729,9 +720,9 @@ __device__ __forceinline__ void assign_moves(int32_t pol1, int32_t pol2, int32_t
   }
 }
 
-// pk_pol: policy_packed() of this tick (ignored when no player is random).
+// pk_pol: policy_bits() of this tick's block (ignored when no player is random).
 __device__ __forceinline__ void policy_pair(Key key, uint32_t game, uint32_t ep, int32_t tick,
-                                            int32_t pol1, int32_t pol2, uint32_t pk_pol,
+                                            int32_t pol1, int32_t pol2, uint64_t pk_pol,
                                             const Player& p1, const Player& p2, int32_t& a1,
                                             int32_t& a2) {
   const int need = (pol1 == ORX_POLICY_RANDOM) + (pol2 == ORX_POLICY_RANDOM);
@@ -1116,7 +1107,7 @@ __global__ void __launch_bounds__(256) policy_kernel(orx_state_t st, int32_t pol
     a1 = (int8_t)(prev & 0xFF);
     a2 = (int8_t)(prev >> 8);
   }
-  const uint32_t pk = need_rng ? policy_packed(key, off + i, ep, tick) : 0u;
+  const uint64_t pk = need_rng ? policy_bits(tick_block(key, off + i, ep, tick)) : 0u;
   policy_pair(key, off + i, ep, tick, pol1, pol2, pk, p1, p2, a1, a2);
   out[i] = pack_actions(a1, a2);
 }
@@ -1192,11 +1183,12 @@ __global__ void __launch_bounds__(256) rollout_kernel(orx_cfg_t hc, orx_state_t 
   bool stairs_dirty = false, npc_dirty = false;
   const bool any_random = pol1 == ORX_POLICY_RANDOM || pol2 == ORX_POLICY_RANDOM;
   for (int32_t t = 0; t < n_ticks; ++t) {
-    const uint32_t pk_pol = (ORX_DIAG & 1) ? ((uint32_t)tick * 0x9E3779B9u) ^ (game * 0x85EBCA6Bu)
-                            : any_random ? policy_packed(key, game, ep, tick) : 0u;
-    // initiative words drawn beside the policy words (one basic block: the
-    // four Philox chains interleave) although only in-progress games use them
-    const uint32_t pk_shf = (ORX_DIAG & 2) ? 0u : shuffle_packed(key, game, ep, tick);
+    // one tick block: the bots' bits and the initiative bits (drawn although
+    // only in-progress games use the latter)
+    const W4 tb = tick_block(key, game, ep, tick);
+    const uint64_t pk_pol = (ORX_DIAG & 1) ? ((uint32_t)tick * 0x9E3779B9u) ^ (game * 0x85EBCA6Bu)
+                            : any_random ? policy_bits(tb) : 0u;
+    const uint32_t pk_shf = (ORX_DIAG & 2) ? 0u : tb.a;
     int32_t a1 = ORX_MOVE_STAY, a2 = ORX_MOVE_STAY;
     policy_pair(key, game, ep, tick, pol1, pol2, pk_pol, p1, p2, a1, a2);
     if (status == ORX_IN_PROGRESS) {
@@ -1262,9 +1254,9 @@ __device__ __forceinline__ uint32_t pc_word(Key key, uint32_t game, uint32_t ep,
                                             int need) {
   int32_t r0 = ORX_MOVE_STAY, r1 = ORX_MOVE_STAY;
   bool perr = false, err = false;
-  if (need)
-    moves_from_packed(policy_packed(key, game, ep, tick), need, key, game, ep, tick, r0, r1, perr);
-  const bool first = p1_first_draw(key, game, ep, tick, err);
+  const W4 tb = tick_block(key, game, ep, tick);
+  if (need) moves_from_packed(policy_bits(tb), need, key, game, ep, tick, r0, r1, perr);
+  const bool first = first_from_packed(tb.a, key, game, ep, tick, err);
   return (uint32_t)r0 | ((uint32_t)r1 << 3) | (first ? 64u : 0u) | (err ? 128u : 0u);
 }
 

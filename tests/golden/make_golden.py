@@ -16,7 +16,7 @@ output:
 
 * ``optimax_rogue.logic.updater.random`` and ``optimax_rogue_bots.randombot.random``
   are replaced by a ``random.Random`` subclass whose ``getrandbits(k)`` returns
-  ``word >> (32 - k)``.  CPython's own ``shuffle``/``choice``/``_randbelow``
+  the next k bits of the tick's reservoir, then ``word >> (32 - k)``.  CPython's own ``shuffle``/``choice``/``_randbelow``
   (Lib/random.py, 3.10) run unchanged on top of it (updater.py:114,127,
   randombot.py:21).
 * ``np`` in ``optimax_rogue.logic.worldgen`` and ``optimax_rogue.game.world`` is
@@ -55,7 +55,9 @@ to '_', lower-case) is put in sys.modules.
 Stream keys (must match include/orx.h / DESIGN.md): Philox key = seed;
 counter = (global game id, episode, c2, purpose << 28 | gen << 24 | block)
 with purposes INIT=1 (c2 = 0), DUNGEON=2 (c2 = depth), SHUFFLE=3, SPAWN=4,
-POLICY=5 (c2 = tick before the update).
+POLICY=5, TICK=7 (c2 = tick before the update).  The CPython-random draws of a
+tick (bots, shuffles) come from the TICK block's bit reservoir first
+(``TickBits``).
 """
 from __future__ import annotations
 
@@ -92,6 +94,7 @@ def philox4x32_10(ctr, key):
 
 
 PUR_INIT, PUR_DUNGEON, PUR_SHUFFLE, PUR_SPAWN, PUR_POLICY = 1, 2, 3, 4, 5
+PUR_TICK = 7
 
 
 class Stream:
@@ -109,6 +112,73 @@ class Stream:
         self.idx += 1
         return w
 
+    def getrandbits(self, k):
+        return self.next() >> (32 - k)
+
+
+class TickBits:
+    """The bit source of one tick's CPython-random draws: the
+    tick block Philox(game, episode, tick, TICK << 28) holds a reservoir --
+    word 0 for the updater's shuffles, words 1 | 2 << 32 for the bots --
+    consumed least-significant bits first; a getrandbits(k) that no longer
+    fits takes the top k bits of the next word of the purpose's own stream."""
+
+    def __init__(self, seed, game, episode, tick, purpose):
+        w = philox4x32_10((game & M, episode & M, tick & M, PUR_TICK << 28),
+                          (seed & M, (seed >> 32) & M))
+        if purpose == PUR_SHUFFLE:
+            self.res, self.bits = w[0], 32
+        else:
+            self.res, self.bits = w[1] | (w[2] << 32), 64
+        self.words = Stream(seed, game, episode, tick, purpose)
+
+    def getrandbits(self, k):
+        if k <= self.bits:
+            r = self.res & ((1 << k) - 1)
+            self.res >>= k
+            self.bits -= k
+            return r
+        return self.words.getrandbits(k)
+
+
+def philox_np(c0, c1, c2, c3, key):
+    """Vectorized Philox4x32-10 over uint32 counter arrays (numpy uint64 math)."""
+    c = [np.asarray(v, np.uint64) & M for v in (c0, c1, c2, c3)]
+    k0, k1 = key
+    for _ in range(10):
+        p0 = c[0] * np.uint64(0xD2511F53)
+        p1 = c[2] * np.uint64(0xCD9E8D57)
+        c = [(p1 >> np.uint64(32)) ^ c[1] ^ np.uint64(k0), p1 & np.uint64(M),
+             (p0 >> np.uint64(32)) ^ c[3] ^ np.uint64(k1), p0 & np.uint64(M)]
+        k0 = (k0 + 0x9E3779B9) & M
+        k1 = (k1 + 0xBB67AE85) & M
+    return c
+
+
+def find_reservoir_overflow(seed, episode, tick, kind, chunk=1 << 22):
+    """First global game id whose tick block cannot serve the tick's draws:
+    kind "shuffle" = all 16 two-bit fields of word 0 rejected (2^-16);
+    "policy" = fewer than two of word 1 | 2 << 32's 21 three-bit fields
+    accepted (~4e-8).  Those games exercise the fallback word streams."""
+    key = (seed & M, (seed >> 32) & M)
+    for start in range(0, 1 << 32, chunk):
+        g = np.arange(start, start + chunk, dtype=np.uint64)
+        w = philox_np(g, episode, tick, PUR_TICK << 28, key)
+        if kind == "shuffle":
+            bad = (~(w[0] >> np.uint64(1)) & np.uint64(0x55555555)) == 0
+        else:
+            pk = w[1] | (w[2] << np.uint64(32))
+            rej = (pk >> np.uint64(2)) & (pk | (pk >> np.uint64(1)))
+            acc = ~rej & np.uint64(0x1249249249249249)
+            n = np.zeros(len(g), np.int64)
+            for j in range(21):
+                n += ((acc >> np.uint64(3 * j)) & np.uint64(1)).astype(np.int64)
+            bad = n < 2
+        hit = np.flatnonzero(bad)
+        if len(hit):
+            return int(g[hit[0]])
+    raise RuntimeError("no overflow found")
+
 
 class PhiloxRandom(random.Random):
     """random.Random whose bits come from the current Philox stream."""
@@ -119,7 +189,7 @@ class PhiloxRandom(random.Random):
 
     def getrandbits(self, k):
         assert 0 < k <= 32
-        return self.stream.next() >> (32 - k)
+        return self.stream.getrandbits(k)
 
 
 class NpRandom:
@@ -330,7 +400,7 @@ class Harness:
         if self.stock:
             with stock_rng(self.R, self):
                 return self._policy(given)
-        self.R.pyrand.stream = Stream(self.seed, self.gid, self.episode, self.gs.tick, PUR_POLICY)
+        self.R.pyrand.stream = TickBits(self.seed, self.gid, self.episode, self.gs.tick, PUR_POLICY)
         return self._policy(given)
 
     def _policy(self, given):
@@ -358,7 +428,7 @@ class Harness:
                 res, upds = self.updater.update(self.gs, R.moves.Move(acts[0]),
                                                 R.moves.Move(acts[1]))
         else:
-            R.pyrand.stream = Stream(self.seed, self.gid, self.episode, self.gs.tick, PUR_SHUFFLE)
+            R.pyrand.stream = TickBits(self.seed, self.gid, self.episode, self.gs.tick, PUR_SHUFFLE)
             R.nprand.stream = Stream(self.seed, self.gid, self.episode, self.gs.tick, PUR_SPAWN)
             with contextlib.redirect_stdout(io.StringIO()):
                 res, upds = self.updater.update(self.gs, R.moves.Move(acts[0]),
@@ -514,6 +584,11 @@ CASES = {
                                             layouts=make_layouts(8, 9, 3, 104, n_stairs=(1, 2))),
                                    seed=4000, games=12, ticks=320),
     # a one-layout bank (no dungeon draw), Separated start, both StaircaseBots
+    # games whose first tick's draws overflow the tick block (fallback streams)
+    "overflow_shuffle": dict(cfg=dict(width=6, height=6, max_ticks=30), seed=5, games=3,
+                             ticks=40, offset=("shuffle", 5, 0, 1)),
+    "overflow_policy": dict(cfg=dict(width=6, height=6, max_ticks=30), seed=5, games=3,
+                            ticks=40, offset=("policy", 5, 0, 1)),
     "bank_single_separated": dict(cfg=dict(width=7, height=7, max_ticks=100, start_mode=2,
                                            p1_depth=1, p2_depth=0, policy=(2, 2),
                                            layouts=make_layouts(7, 7, 1, 103, n_stairs=(2,))),
@@ -530,6 +605,10 @@ def run_case(R, name, spec):
     cfg.update(spec["cfg"])
     seed, G, T = spec["seed"], spec["games"], spec["ticks"]
     off = spec.get("offset", 0)
+    if isinstance(off, tuple):   # (kind, seed, episode, tick): search the game id
+        kind, s_, e_, t_ = off
+        off = find_reservoir_overflow(s_, e_, t_, kind)
+        print(f"{name}: game {off} overflows the {kind} reservoir at tick {t_}")
     hs = [Harness(R, cfg, seed, off + g) for g in range(G)]
     bank = cfg.get("layouts")
     keys = SNAP_KEYS_I32 + (["p_layout"] if bank is not None else [])
