@@ -630,48 +630,60 @@ __device__ __forceinline__ void descend(const Cfg& c, Key key, Src& src, Player&
 // ---------------------------------------------------------------------------
 // Random bits of one tick
 // ---------------------------------------------------------------------------
-// A tick's CPython-random draws (getrandbits(k), k <= 32) come first from the
-// bit reservoir of ONE Philox block, the tick block (game, episode, tick,
-// TICK), consumed least-significant bits first; a draw that no longer fits
-// takes the top k bits of the next word of the purpose's own stream
-// (SHUFFLE / POLICY, from word 0).  DESIGN.md §4, make_golden.TickBits.
+// A tick's CPython-random draws (getrandbits(k), k <= 32) come first from
+// reservoir segments of ONE Philox block, the tick block (game, episode,
+// tick, TICK), consumed least-significant bits first; a segment with fewer
+// than k bits left is skipped, and once none is left a draw takes the top k
+// bits of the next word of the purpose's own stream (SHUFFLE / POLICY, from
+// word 0).  DESIGN.md §4, make_golden.TickBits.
 //  * word a (32 bits): the updater's shuffles.  random.shuffle([p1, p2]) =
 //    randbelow(2), k = 2: 16 two-bit fields, accepted iff the high bit is
 //    clear; player 1 acts first iff the first accepted field == 1
 //    (updater.py:114).  All 16 rejected: 2^-16.
-//  * words b | c << 32 (64 bits): the bots.  RandomBot.move =
-//    Move(1 + randbelow(5)), k = 3: 21 three-bit fields, rejected iff >= 5
-//    (bit2 & (bit1 | bit0)); p1's draws then p2's.  Fewer than two accepted
-//    of 21: ~1e-8.
-// One block per game-tick (the per-purpose whole-word streams needed four).
+//  * bits 0-29 of word b, then of word c: the bots.  RandomBot.move =
+//    Move(1 + randbelow(5)), k = 3: ten three-bit fields per word, rejected
+//    iff >= 5 (bit2 & (bit1 | bit0)); p1's draws then p2's.  Fewer than two
+//    accepted in word b: ~1e-3; in both words: ~1e-7.
+// One block per game-tick (per-purpose whole-word streams needed four).
 __device__ __forceinline__ W4 tick_block(Key key, uint32_t game, uint32_t ep, int32_t tick) {
   return philox(game, ep, (uint32_t)tick, tag(PUR_TICK, 0), key);
 }
-__device__ __forceinline__ uint64_t policy_bits(const W4& tb) {
-  return (uint64_t)tb.b | ((uint64_t)tb.c << 32);
+
+// bit 0 of each accepted three-bit field among a word's low ten
+__device__ __forceinline__ uint32_t accepted3(uint32_t w) {
+  return ~((w >> 2) & (w | (w >> 1))) & 0x09249249u;
 }
 
-__device__ __forceinline__ void moves_from_packed(uint64_t pk, int need, Key key, uint32_t game,
-                                                  uint32_t ep, int32_t tick, int32_t& m0,
-                                                  int32_t& m1, bool& err) {
-  constexpr uint64_t kF = 0x1249249249249249ull;  // bit 0 of each 3-bit field (21 fields)
-  const uint64_t acc = ~((pk >> 2) & (pk | (pk >> 1))) & kF;
-  const uint64_t acc2 = acc & (acc - 1u);
-  // (| bit 63: a defined shift when the mask is empty; the value is then unused)
-  m0 = (int32_t)((pk >> __builtin_ctzll(acc | (1ull << 63))) & 7u) + 1;
-  m1 = (int32_t)((pk >> __builtin_ctzll(acc2 | (1ull << 63))) & 7u) + 1;
+// RandomBot draws r0, r1 (`need` of them) from the tick block's bot segments.
+__device__ __forceinline__ void moves_from_block(const W4& tb, int need, Key key, uint32_t game,
+                                                 uint32_t ep, int32_t tick, int32_t& m0,
+                                                 int32_t& m1, bool& err) {
+  const uint32_t acc = accepted3(tb.b);
+  const uint32_t acc2 = acc & (acc - 1u);
+  // (| bit 31: a defined shift when the mask is empty; the value is then unused)
+  m0 = (int32_t)((tb.b >> __builtin_ctz(acc | 0x80000000u)) & 7u) + 1;
+  m1 = (int32_t)((tb.b >> __builtin_ctz(acc2 | 0x80000000u)) & 7u) + 1;
   const int got = acc == 0 ? 0 : acc2 == 0 ? 1 : 2;
-  if (got < need) {  // rare: the POLICY stream's words
+  if (got < need) {  // rare: word c's segment, then the POLICY stream's words
     int g = got;
-    Stream s;
-    s.init(game, ep, (uint32_t)tick, tag(PUR_POLICY, 0), 0);
-    for (uint32_t i = 0; i < kWordCap && g < need; ++i) {
-      const uint32_t r = s.next(key) >> 29;
-      if (r >= 5u) continue;
-      if (g == 0) m0 = (int32_t)r + 1; else m1 = (int32_t)r + 1;
+    uint32_t ac = accepted3(tb.c);
+    for (int j = 0; j < 2 && g < need && ac; ++j) {
+      const int32_t v = (int32_t)((tb.c >> __builtin_ctz(ac)) & 7u) + 1;
+      if (g == 0) m0 = v; else m1 = v;
       ++g;
+      ac &= ac - 1u;
     }
-    if (g < need) err = true;
+    if (g < need) {
+      Stream s;
+      s.init(game, ep, (uint32_t)tick, tag(PUR_POLICY, 0), 0);
+      for (uint32_t i = 0; i < kWordCap && g < need; ++i) {
+        const uint32_t r = s.next(key) >> 29;
+        if (r >= 5u) continue;
+        if (g == 0) m0 = (int32_t)r + 1; else m1 = (int32_t)r + 1;
+        ++g;
+      }
+      if (g < need) err = true;
+    }
   }
 }
 
@@ -720,15 +732,15 @@ __device__ __forceinline__ void assign_moves(int32_t pol1, int32_t pol2, int32_t
   }
 }
 
-// pk_pol: policy_bits() of this tick's block (ignored when no player is random).
+// tb: this tick's block (its bot segments are ignored when no player is random).
 __device__ __forceinline__ void policy_pair(Key key, uint32_t game, uint32_t ep, int32_t tick,
-                                            int32_t pol1, int32_t pol2, uint64_t pk_pol,
+                                            int32_t pol1, int32_t pol2, const W4& tb,
                                             const Player& p1, const Player& p2, int32_t& a1,
                                             int32_t& a2) {
   const int need = (pol1 == ORX_POLICY_RANDOM) + (pol2 == ORX_POLICY_RANDOM);
   int32_t r0 = ORX_MOVE_STAY, r1 = ORX_MOVE_STAY;
   bool err = false;
-  if (need) moves_from_packed(pk_pol, need, key, game, ep, tick, r0, r1, err);
+  if (need) moves_from_block(tb, need, key, game, ep, tick, r0, r1, err);
   assign_moves(pol1, pol2, r0, r1, p1, p2, a1, a2);
 }
 
@@ -1107,8 +1119,8 @@ __global__ void __launch_bounds__(256) policy_kernel(orx_state_t st, int32_t pol
     a1 = (int8_t)(prev & 0xFF);
     a2 = (int8_t)(prev >> 8);
   }
-  const uint64_t pk = need_rng ? policy_bits(tick_block(key, off + i, ep, tick)) : 0u;
-  policy_pair(key, off + i, ep, tick, pol1, pol2, pk, p1, p2, a1, a2);
+  const W4 tb = need_rng ? tick_block(key, off + i, ep, tick) : W4{0, 0, 0, 0};
+  policy_pair(key, off + i, ep, tick, pol1, pol2, tb, p1, p2, a1, a2);
   out[i] = pack_actions(a1, a2);
 }
 
@@ -1181,16 +1193,14 @@ __global__ void __launch_bounds__(256) rollout_kernel(orx_cfg_t hc, orx_state_t 
   Deltas dl = {0, 0, 0, 0, 0, 0};
   int32_t sep = (c.ext & ORX_EXT_SEPARATION_DAMAGE) ? st.sep_start[i] : -1;
   bool stairs_dirty = false, npc_dirty = false;
-  const bool any_random = pol1 == ORX_POLICY_RANDOM || pol2 == ORX_POLICY_RANDOM;
   for (int32_t t = 0; t < n_ticks; ++t) {
     // one tick block: the bots' bits and the initiative bits (drawn although
     // only in-progress games use the latter)
-    const W4 tb = tick_block(key, game, ep, tick);
-    const uint64_t pk_pol = (ORX_DIAG & 1) ? ((uint32_t)tick * 0x9E3779B9u) ^ (game * 0x85EBCA6Bu)
-                            : any_random ? policy_bits(tb) : 0u;
+    W4 tb = tick_block(key, game, ep, tick);
+    if (ORX_DIAG & 1) tb.b = tb.c = ((uint32_t)tick * 0x9E3779B9u) ^ (game * 0x85EBCA6Bu);
     const uint32_t pk_shf = (ORX_DIAG & 2) ? 0u : tb.a;
     int32_t a1 = ORX_MOVE_STAY, a2 = ORX_MOVE_STAY;
-    policy_pair(key, game, ep, tick, pol1, pol2, pk_pol, p1, p2, a1, a2);
+    policy_pair(key, game, ep, tick, pol1, pol2, tb, p1, p2, a1, a2);
     if (status == ORX_IN_PROGRESS) {
       p1.move = a1; p2.move = a2;
       const int32_t descents = dl.descend;
@@ -1255,7 +1265,7 @@ __device__ __forceinline__ uint32_t pc_word(Key key, uint32_t game, uint32_t ep,
   int32_t r0 = ORX_MOVE_STAY, r1 = ORX_MOVE_STAY;
   bool perr = false, err = false;
   const W4 tb = tick_block(key, game, ep, tick);
-  if (need) moves_from_packed(policy_bits(tb), need, key, game, ep, tick, r0, r1, perr);
+  if (need) moves_from_block(tb, need, key, game, ep, tick, r0, r1, perr);
   const bool first = first_from_packed(tb.a, key, game, ep, tick, err);
   return (uint32_t)r0 | ((uint32_t)r1 << 3) | (first ? 64u : 0u) | (err ? 128u : 0u);
 }

@@ -118,27 +118,32 @@ class Stream:
 
 class TickBits:
     """The bit source of one tick's CPython-random draws: the
-    tick block Philox(game, episode, tick, TICK << 28) holds a reservoir --
-    word 0 for the updater's shuffles, words 1 | 2 << 32 for the bots --
-    consumed least-significant bits first; a getrandbits(k) that no longer
-    fits takes the top k bits of the next word of the purpose's own stream."""
+    tick block Philox(game, episode, tick, TICK << 28) holds reservoir
+    segments -- word 0 (32 bits) for the updater's shuffles; bits 0-29 of
+    word 1, then bits 0-29 of word 2 for the bots -- consumed
+    least-significant bits first.  A getrandbits(k) skips a segment with
+    fewer than k bits left; once none is left it takes the top k bits of the
+    next word of the purpose's own stream."""
 
     def __init__(self, seed, game, episode, tick, purpose):
         w = philox4x32_10((game & M, episode & M, tick & M, PUR_TICK << 28),
                           (seed & M, (seed >> 32) & M))
         if purpose == PUR_SHUFFLE:
-            self.res, self.bits = w[0], 32
+            self.segs = [[w[0], 32]]
         else:
-            self.res, self.bits = w[1] | (w[2] << 32), 64
+            self.segs = [[w[1] & 0x3FFFFFFF, 30], [w[2] & 0x3FFFFFFF, 30]]
         self.words = Stream(seed, game, episode, tick, purpose)
 
     def getrandbits(self, k):
-        if k <= self.bits:
-            r = self.res & ((1 << k) - 1)
-            self.res >>= k
-            self.bits -= k
-            return r
-        return self.words.getrandbits(k)
+        while self.segs and self.segs[0][1] < k:
+            self.segs.pop(0)
+        if not self.segs:
+            return self.words.getrandbits(k)
+        seg = self.segs[0]
+        r = seg[0] & ((1 << k) - 1)
+        seg[0] >>= k
+        seg[1] -= k
+        return r
 
 
 def philox_np(c0, c1, c2, c3, key):
@@ -158,8 +163,8 @@ def philox_np(c0, c1, c2, c3, key):
 def find_reservoir_overflow(seed, episode, tick, kind, chunk=1 << 22):
     """First global game id whose tick block cannot serve the tick's draws:
     kind "shuffle" = all 16 two-bit fields of word 0 rejected (2^-16);
-    "policy" = fewer than two of word 1 | 2 << 32's 21 three-bit fields
-    accepted (~4e-8).  Those games exercise the fallback word streams."""
+    "policy" = fewer than two of the 20 three-bit fields in bits 0-29 of
+    words 1 and 2 accepted (~1e-7).  Those games exercise the fallback word streams."""
     key = (seed & M, (seed >> 32) & M)
     for start in range(0, 1 << 32, chunk):
         g = np.arange(start, start + chunk, dtype=np.uint64)
@@ -167,12 +172,12 @@ def find_reservoir_overflow(seed, episode, tick, kind, chunk=1 << 22):
         if kind == "shuffle":
             bad = (~(w[0] >> np.uint64(1)) & np.uint64(0x55555555)) == 0
         else:
-            pk = w[1] | (w[2] << np.uint64(32))
-            rej = (pk >> np.uint64(2)) & (pk | (pk >> np.uint64(1)))
-            acc = ~rej & np.uint64(0x1249249249249249)
             n = np.zeros(len(g), np.int64)
-            for j in range(21):
-                n += ((acc >> np.uint64(3 * j)) & np.uint64(1)).astype(np.int64)
+            for v in (w[1], w[2]):
+                rej = (v >> np.uint64(2)) & (v | (v >> np.uint64(1)))
+                acc = ~rej & np.uint64(0x09249249)
+                for j in range(10):
+                    n += ((acc >> np.uint64(3 * j)) & np.uint64(1)).astype(np.int64)
             bad = n < 2
         hit = np.flatnonzero(bad)
         if len(hit):
