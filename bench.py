@@ -66,13 +66,10 @@ def bytes_per_game(kernel: str, K: int, ticks: int = 1) -> int:
 
 
 def rollout_kernel_name(B: int, K: int) -> str:
-    """The kernel orx_rollout launches for this batch (orx_engine.hip
-    use_pc_rollout: producer/consumer form up to 4 x 65,536 games; the
-    RandomBot + trajectory specialization FAST=1)."""
+    """The kernel orx_rollout launches for this workload: rollout_kernel with
+    the RandomBot + trajectory specialization (FAST=1), NPC capacity 0/8/16."""
     ncap = 0 if K == 0 else 8 if K <= 8 else 16
-    mode = os.environ.get("ORX_ROLLOUT")
-    pc = (B <= 4 * 65536) if mode not in ("pc", "plain") else mode == "pc"
-    return f"{'rollout_pc_kernel' if pc else 'rollout_kernel'}<{ncap}, true>"
+    return f"rollout_kernel<{ncap}, true, false>"
 
 
 def cpu_baseline(cfg_dict: dict, seconds: float) -> dict:

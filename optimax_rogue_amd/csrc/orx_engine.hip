@@ -60,14 +60,16 @@ enum : uint32_t {
   PUR_RESOLVE = 6,  // ORX_EXT_RANDOM_DOUBLE_DEATH
   PUR_TICK = 7      // the tick's CPython-random bit reservoir (bots, shuffles)
 };
+#define ORX_LIKELY(x) __builtin_expect(!!(x), 1)
+#define ORX_UNLIKELY(x) __builtin_expect(!!(x), 0)
+
 constexpr uint32_t kWordCap = 4096;  // per stream; exceeding it stops the game
 constexpr int32_t kStartTick = 1;     // GameState.tick of a fresh game (worldgen.py:87,133)
 constexpr uint32_t kDeadSlot = 0xFFFFu;
 
 // Diagnostic builds only (-DORX_DIAG=bits; results are wrong): rollout_kernel
 // 1 no policy RNG, 2 no initiative RNG, 4 no move logic, 8 no reset, 16 no
-// trajectory; rollout_pc_kernel 16 no trajectory, 32 trivial producer, 64 no
-// move logic.  Used by tools/ab_rollout.py to attribute time.
+// trajectory.  Used by tools/ab_rollout.py to attribute time.
 #ifndef ORX_DIAG
 #define ORX_DIAG 0
 #endif
@@ -664,7 +666,7 @@ __device__ __forceinline__ void moves_from_block(const W4& tb, int need, Key key
   m0 = (int32_t)((tb.b >> __builtin_ctz(acc | 0x80000000u)) & 7u) + 1;
   m1 = (int32_t)((tb.b >> __builtin_ctz(acc2 | 0x80000000u)) & 7u) + 1;
   const int got = acc == 0 ? 0 : acc2 == 0 ? 1 : 2;
-  if (got < need) {  // rare: word c's segment, then the POLICY stream's words
+  if (ORX_UNLIKELY(got < need)) {  // rare: word c's segment, then the POLICY stream's words
     int g = got;
     uint32_t ac = accepted3(tb.c);
     for (int j = 0; j < 2 && g < need && ac; ++j) {
@@ -691,7 +693,7 @@ __device__ __forceinline__ bool first_from_packed(uint32_t pk, Key key, uint32_t
                                                   int32_t tick, bool& err) {
   const uint32_t acc = ~(pk >> 1) & 0x55555555u;
   int res = acc ? (int)((pk >> __builtin_ctz(acc | 0x80000000u)) & 1u) : -1;
-  if (res < 0) {  // rare (2^-16): the SHUFFLE stream's words
+  if (ORX_UNLIKELY(res < 0)) {  // rare (2^-16): the SHUFFLE stream's words
     Stream s;
     s.init(game, ep, (uint32_t)tick, tag(PUR_SHUFFLE, 0), 0);
     for (uint32_t i = 0; i < kWordCap && res < 0; ++i) {
@@ -765,8 +767,9 @@ __device__ __forceinline__ bool handle_move(const Cfg& c, Key key, Src& src, Pla
   const bool moving = self.move != ORX_MOVE_STAY;
   const int32_t tx = self.tx, ty = self.ty;
   const bool occ_other = moving && other.d == self.d && other.x == tx && other.y == ty;
-  const bool hit_npc = NCAP > 0 && moving && !occ_other && self.d == c.d1 &&
-                       npc.any(pack_xy(tx, ty));
+  // bitwise, not short-circuit: no branch around the slot scan
+  const bool hit_npc = NCAP > 0 && (moving & !occ_other & (self.d == c.d1) &
+                                    npc.any(pack_xy(tx, ty)));
   const bool free = moving && !occ_other && !hit_npc;
   const bool stairs = free && stair_tile<GRID>(c, self, tx, ty);
   const bool step = free && !stairs;
@@ -789,7 +792,7 @@ __device__ __forceinline__ bool handle_move(const Cfg& c, Key key, Src& src, Pla
     if (hit_npc) ev.emit(ORX_EV_COMBAT, self_iden, 3 + npc.find(pack_xy(tx, ty)), ORX_FLAG_BLOCK);
     if (step) ev.emit(ORX_EV_POSITION, self_iden, self.d, (tx & 0xFFFF) | (ty << 16));
   }
-  if (stairs)
+  if (ORX_UNLIKELY(stairs))
     descend<NCAP, EV, GRID>(c, key, src, self, other, other_start, npc, spawn, dl, err,
                             self_iden, ev);
   return hit_npc;
@@ -851,7 +854,7 @@ __device__ __forceinline__ void tick_game(const Cfg& c, Key key, Src& src, uint3
                                               a_iden, true, ev);
   const bool hB = handle_move<NCAP, EV, GRID>(c, key, src, Bp, A, a_start, npc, spawn, dl, err,
                                               3 - a_iden, false, ev);
-  if (NCAP > 0 && (hA || hB)) {
+  if (NCAP > 0 && ORX_UNLIKELY(hA || hB)) {
     // NPCs never move and are swept only after both moves: the slots found at
     // the targets now are the ones that were attacked.
     const int h0 = hA ? npc.find(pack_xy(A.tx, A.ty)) : -1;
@@ -881,21 +884,19 @@ __device__ __forceinline__ void tick_game(const Cfg& c, Key key, Src& src, uint3
   }
 
   tick += 1;                                           // updater.py:148-162
-  if (p1.hp <= 0)
-    status = p2.hp > 0 ? ORX_PLAYER2_WIN
-             : !(c.ext & ORX_EXT_RANDOM_DOUBLE_DEATH) ? ORX_TIE
-             : p2_wins_draw ? ORX_PLAYER2_WIN : ORX_PLAYER1_WIN;
-  else if (p2.hp <= 0)
-    status = ORX_PLAYER1_WIN;
-  else if (c.max_ticks && tick >= c.max_ticks)
-    status = ORX_TIE;
-  else
-    status = ORX_IN_PROGRESS;
-  if (err) status = ORX_STATUS_RNG_EXHAUSTED;
-  if (status != ORX_IN_PROGRESS) {
-    dl.ret += status == ORX_PLAYER1_WIN ? 1 : status == ORX_PLAYER2_WIN ? -1 : 0;
-    dl.eps += (status >= ORX_PLAYER1_WIN && status <= ORX_TIE) ? 1 : 0;
-  }
+  // as selects, lowest precedence first (a divergent if-chain here costs the
+  // lone wave taken branches every tick)
+  const bool dead1 = p1.hp <= 0, dead2 = p2.hp <= 0;
+  const int32_t both = !(c.ext & ORX_EXT_RANDOM_DOUBLE_DEATH) ? ORX_TIE
+                       : p2_wins_draw                         ? ORX_PLAYER2_WIN
+                                                              : ORX_PLAYER1_WIN;
+  int32_t s = (c.max_ticks && tick >= c.max_ticks) ? ORX_TIE : ORX_IN_PROGRESS;
+  s = dead2 ? ORX_PLAYER1_WIN : s;
+  s = dead1 ? (dead2 ? both : ORX_PLAYER2_WIN) : s;
+  s = err ? ORX_STATUS_RNG_EXHAUSTED : s;
+  status = s;
+  dl.ret += (s == ORX_PLAYER1_WIN ? 1 : 0) - (s == ORX_PLAYER2_WIN ? 1 : 0);
+  dl.eps += (uint32_t)(s - ORX_PLAYER1_WIN) <= (uint32_t)(ORX_TIE - ORX_PLAYER1_WIN) ? 1 : 0;
 }
 
 template <int NCAP, bool EV, bool GRID = false>
@@ -1125,16 +1126,23 @@ __global__ void __launch_bounds__(256) policy_kernel(orx_state_t st, int32_t pol
 }
 
 // Fused rollout: n_ticks x (policy, step); state and NPC positions stay in
-// registers; tick t's observation row is streamed out to obs/act.
-// (Splitting a game's two random streams over two lanes -- two waves per SIMD
-// at 65,536 games -- was measured 22% slower: the replicated game logic costs
-// more than the halved Philox saves.)
+// registers; tick t's observation row is streamed out to obs/act.  At the
+// headline batch (65,536 games) this is ONE wave per SIMD, so the tick loop is
+// bound by that wave's own issue and stalls: the common path is laid out
+// straight (rare blocks -- descends, NPC hits, resets, RNG fallbacks -- marked
+// unlikely and placed out of line: -13%), and every per-tick decision that
+// can be a select is one.  (Rejected, measured: splitting a game over two
+// lanes; a producer wave drawing the RNG ahead through an LDS ring -- won
+// while a tick took four Philox blocks, lost once it took one.)
 
 // One tick's trajectory rows: obs[t][f][i] (ORX_OBS_* fields) and act[t][i].
 // FAST (both present): buffer stores -- one resource per tick row block, the
 // field stride in the scalar offset, so the lane's address is one VGPR
 // computed once; otherwise per-pointer checks and flat stores.
 constexpr int32_t kBufferDword3 = 0x00020000;  // gfx9 raw buffer, 32-bit elements
+// trajectory rows are written once and read by the caller later: nontemporal
+// stores (cache-policy nt) keep them from churning L2 (measured -4% per launch)
+constexpr int32_t kStreamAux = 2;
 template <bool FAST>
 __device__ __forceinline__ void store_traj(int32_t* obs, int8_t* act, int32_t t, uint32_t B,
                                            uint32_t i, const Player& p1, const Player& p2,
@@ -1151,19 +1159,23 @@ __device__ __forceinline__ void store_traj(int32_t* obs, int8_t* act, int32_t t,
     const int32_t b4 = (int32_t)(B * 4u);
 #pragma unroll
     for (int f = 0; f < ORX_OBS_FIELDS; ++f) {
-      __builtin_amdgcn_raw_buffer_store_b32(vals[f], ro, (int32_t)(i * 4u), so, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(vals[f], ro, (int32_t)(i * 4u), so, kStreamAux);
       asm volatile("s_add_u32 %0, %0, %1" : "+s"(so) : "s"(b4));
     }
     const auto ra = __builtin_amdgcn_make_buffer_rsrc(act + (size_t)t * 2 * B, 0, (int32_t)(B * 2u),
                                                       kBufferDword3);
-    __builtin_amdgcn_raw_buffer_store_b16(pack_actions(a1, a2), ra, (int32_t)(i * 2u), 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b16(pack_actions(a1, a2), ra, (int32_t)(i * 2u), 0,
+                                          kStreamAux);
   } else {
     if (obs) {
       int32_t* o = obs + (size_t)t * ORX_OBS_FIELDS * B;  // uniform row base + lane index
 #pragma unroll
-      for (int f = 0; f < ORX_OBS_FIELDS; ++f) (o + (size_t)f * B)[i] = vals[f];
+      for (int f = 0; f < ORX_OBS_FIELDS; ++f)
+        __builtin_nontemporal_store(vals[f], (o + (size_t)f * B) + i);
     }
-    if (act) reinterpret_cast<uint16_t*>(act)[(size_t)t * B + i] = pack_actions(a1, a2);
+    if (act)
+      __builtin_nontemporal_store(pack_actions(a1, a2),
+                                  reinterpret_cast<uint16_t*>(act) + (size_t)t * B + i);
   }
 }
 
@@ -1201,7 +1213,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(orx_cfg_t hc, orx_state_t 
     const uint32_t pk_shf = (ORX_DIAG & 2) ? 0u : tb.a;
     int32_t a1 = ORX_MOVE_STAY, a2 = ORX_MOVE_STAY;
     policy_pair(key, game, ep, tick, pol1, pol2, tb, p1, p2, a1, a2);
-    if (status == ORX_IN_PROGRESS) {
+    if (ORX_LIKELY(status == ORX_IN_PROGRESS)) {
       p1.move = a1; p2.move = a2;
       const int32_t descents = dl.descend;
       bool err = false;
@@ -1239,193 +1251,6 @@ __global__ void __launch_bounds__(256) rollout_kernel(orx_cfg_t hc, orx_state_t 
   if (c.ext & ORX_EXT_SEPARATION_DAMAGE) st.sep_start[i] = sep;
   if (NCAP > 0 && (npc_dirty || dl.npc_death)) st.npc_alive[i] = npc.alive;
   flush_deltas(st, B, i, dl);
-}
-
-// Producer/consumer form of rollout_kernel for batches that put at most a few
-// waves on a SIMD (the headline 65,536 games = one wave per SIMD, which
-// cannot hide its own latencies).  A 128-thread workgroup owns 64 games:
-// wave 0 draws the RandomBot moves and the initiative bits -- they depend only
-// on (game, episode, tick), never on the board -- and wave 1 resolves the
-// ticks.  (Splitting the draws over two producer waves measured slower: three
-// waves per SIMD contend for issue.)  The waves are decoupled through LDS rings of kRing ticks with one
-// progress counter per wave (no barrier in the loop): a producer runs ahead
-// on a predicted key sequence -- tick+1 while in progress, the game ends when
-// max_ticks is reached, then (episode+1, kStartTick) under autoreset -- which
-// is exact except after a player death.  Every slot carries the key it was
-// drawn for; the consumer checks it and on a mismatch draws the words itself
-// and posts its true key, from which the producer re-predicts.  Results are
-// therefore identical to rollout_kernel whatever the timing.
-constexpr int kRing = 8;        // ticks the producer may run ahead
-constexpr int kBackoff = 8;     // producer poll back-off, units of 64 cycles
-
-// producer word: bits 0-2 first RandomBot move, 3-5 second, 6 p1 first,
-// 7 RNG exhausted
-__device__ __forceinline__ uint32_t pc_word(Key key, uint32_t game, uint32_t ep, int32_t tick,
-                                            int need) {
-  int32_t r0 = ORX_MOVE_STAY, r1 = ORX_MOVE_STAY;
-  bool perr = false, err = false;
-  const W4 tb = tick_block(key, game, ep, tick);
-  if (need) moves_from_block(tb, need, key, game, ep, tick, r0, r1, perr);
-  const bool first = first_from_packed(tb.a, key, game, ep, tick, err);
-  return (uint32_t)r0 | ((uint32_t)r1 << 3) | (first ? 64u : 0u) | (err ? 128u : 0u);
-}
-
-struct KeyPred {   // predicted (episode, tick) at the start of an iteration
-  uint32_t ep;
-  int32_t tick;
-  bool ended;      // status != InProgress: the iteration is a reset (or frozen)
-  __device__ __forceinline__ void advance(const Cfg& c) {
-    if (!ended) {
-      tick += 1;
-      ended = c.max_ticks && tick >= c.max_ticks;
-    } else if (c.autoreset) {
-      ep += 1;
-      tick = kStartTick;
-      ended = false;
-    }
-  }
-};
-
-__device__ __forceinline__ uint32_t lds_acquire(uint32_t* p) {
-  return __builtin_amdgcn_readfirstlane(
-      __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
-}
-__device__ __forceinline__ void lds_release(uint32_t* p, uint32_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-template <int NCAP, bool FAST>
-__global__ void __launch_bounds__(128) rollout_pc_kernel(
-    orx_cfg_t hc, orx_state_t st, int32_t pol1_, int32_t pol2_, int32_t n_ticks,
-    int32_t* __restrict__ obs, int8_t* __restrict__ act, uint32_t B, Key key, uint32_t off) {
-  const int32_t pol1 = FAST ? (int32_t)ORX_POLICY_RANDOM : pol1_;
-  const int32_t pol2 = FAST ? (int32_t)ORX_POLICY_RANDOM : pol2_;
-  struct Slot {
-    uint32_t word, ep;
-    int32_t tick, pad;
-  };
-  __shared__ Slot ring[kRing][64];
-  __shared__ int32_t rec_t[64];            // consumer's posted true key: iteration,
-  __shared__ uint32_t rec_ep[64];          // episode, tick, ended
-  __shared__ int32_t rec_tick[64];
-  __shared__ uint32_t rec_ended[64];
-  __shared__ uint32_t produced, consumed;  // iterations written / read
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t wave = threadIdx.x >> 6;  // wave-uniform role
-  const uint32_t i = blockIdx.x * 64u + lane;
-  const bool valid = i < B;                 // no early return: every wave runs every iteration
-  Cfg c = make_cfg(hc, st);
-  if (FAST) c.ext = 0;  // FAST launches require flags == 0
-  const int need = (pol1 == ORX_POLICY_RANDOM) + (pol2 == ORX_POLICY_RANDOM);
-  if (wave == 0) {
-    rec_t[lane] = -1;
-    if (lane == 0) { produced = 0; consumed = 0; }
-  }
-  __syncthreads();
-
-  // lanes past B shadow game B-1 (uniform control flow; nothing is stored)
-  const uint32_t ic = valid ? i : B - 1u;
-  const uint32_t gc = off + ic;
-  if (wave == 0) {
-    KeyPred pk{(uint32_t)st.episode[ic], st.tick[ic], st.status[ic] != ORX_IN_PROGRESS};
-    int32_t seen = -1;
-    for (int32_t t = 0; t < n_ticks; ++t) {
-      // slot t % kRing is free once iteration t - kRing was read.  A full ring
-      // means the producer is a whole ring ahead: sleep long (each poll takes
-      // issue slots from the consumer on the same SIMD).
-      if (t >= kRing)
-        while ((int32_t)lds_acquire(&consumed) <= t - kRing) __builtin_amdgcn_s_sleep(kBackoff);
-      {
-        const int32_t rt = __hip_atomic_load(&rec_t[lane], __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (rt != seen) {  // rare: re-predict from the consumer's posted key
-          seen = rt;
-          pk.ep = rec_ep[lane];
-          pk.tick = rec_tick[lane];
-          pk.ended = rec_ended[lane] != 0;
-          for (int32_t k = rt; k < t; ++k) pk.advance(c);
-        }
-        const uint32_t word = (ORX_DIAG & 32) ? 0x09u ^ ((uint32_t)pk.tick & 64u)
-                                               : pc_word(key, gc, pk.ep, pk.tick, need);
-        ring[(uint32_t)t % kRing][lane] = Slot{word, pk.ep, pk.tick, 0};
-        pk.advance(c);
-      }
-      if (lane == 0) lds_release(&produced, (uint32_t)t + 1);
-    }
-    return;
-  }
-
-  // consumer
-  Player p1, p2;
-  load_players(st, B, ic, p1, p2);
-  int32_t tick = st.tick[ic];
-  int32_t status = st.status[ic];
-  uint32_t ep = (uint32_t)st.episode[ic];
-  Npcs<NCAP> npc;
-  load_npcs(st, c, B, ic, npc);
-  Deltas dl = {0, 0, 0, 0, 0, 0};
-  int32_t sep = (c.ext & ORX_EXT_SEPARATION_DAMAGE) ? st.sep_start[ic] : -1;
-  bool stairs_dirty = false, npc_dirty = false;
-  const NpcMem m{st.npc_pos, st.npc_health, B, ic};
-  int32_t avail;  // iterations known to be produced
-  while ((avail = (int32_t)lds_acquire(&produced)) <= 0) __builtin_amdgcn_s_sleep(1);
-  Slot sl = ring[0][lane];
-  for (int32_t t = 0; t < n_ticks; ++t) {
-    // slot t was read last iteration: hand it back, then prefetch slot t+1 so
-    // its LDS latency hides under this tick
-    if (lane == 0) lds_release(&consumed, (uint32_t)t + 1);
-    Slot nx = sl;
-    if (t + 1 < n_ticks) {
-      if (t + 1 >= avail)
-        while ((avail = (int32_t)lds_acquire(&produced)) <= t + 1) __builtin_amdgcn_s_sleep(1);
-      nx = ring[(uint32_t)(t + 1) % kRing][lane];
-    }
-    uint32_t w = sl.word;
-    if (sl.ep != ep || sl.tick != tick) {
-      // rare (after a death): draw here, post the true key
-      w = pc_word(key, gc, ep, tick, need);
-      rec_ep[lane] = ep;
-      rec_tick[lane] = tick;
-      rec_ended[lane] = status != ORX_IN_PROGRESS;
-      __hip_atomic_store(&rec_t[lane], t, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    int32_t a1 = ORX_MOVE_STAY, a2 = ORX_MOVE_STAY;
-    assign_moves(pol1, pol2, (int32_t)(w & 7u), (int32_t)((w >> 3) & 7u), p1, p2, a1, a2);
-    if (status == ORX_IN_PROGRESS) {
-      p1.move = a1; p2.move = a2;
-      const int32_t descents = dl.descend;
-      bool err = (w & 128u) != 0;
-      Events<false> ev{nullptr, 0};
-      if (ORX_DIAG & 64) {
-        tick += 1;
-        p1.x ^= (w >> 6) & 1u;
-        status = (c.max_ticks && tick >= c.max_ticks) ? ORX_TIE : ORX_IN_PROGRESS;
-      } else {
-        tick_game(c, key, gc, ep, (w & 64u) != 0, valid, p1, p2, npc, m, tick, status, err, dl,
-                  ev, sep);
-      }
-      stairs_dirty |= dl.descend != descents;
-    } else if (c.autoreset) {
-      ep += 1;
-      setup_game(c, key, gc, ep, p1, p2, npc, tick, status);
-      if constexpr (NCAP > 0) if (valid) store_new_npcs(st, c, B, i, npc);
-      stairs_dirty = true;
-      npc_dirty = true;
-      sep = -1;
-    }
-    if (!(ORX_DIAG & 16) && valid)
-      store_traj<FAST>(obs, act, t, B, i, p1, p2, tick, status, a1, a2);
-    sl = nx;
-  }
-  if (valid) {
-    store_players(st, B, i, p1, p2, stairs_dirty);
-    st.tick[i] = tick;
-    st.status[i] = status;
-    st.episode[i] = (int32_t)ep;
-    if (c.ext & ORX_EXT_SEPARATION_DAMAGE) st.sep_start[i] = sep;
-    if (NCAP > 0 && (npc_dirty || dl.npc_death)) st.npc_alive[i] = npc.alive;
-    flush_deltas(st, B, i, dl);
-  }
 }
 
 // Staircases of arbitrary (game, episode, depth, generation) dungeons, for
@@ -1784,20 +1609,6 @@ constexpr int kBlock = 256;
 
 inline dim3 grid_for(int64_t B) { return dim3((unsigned)((B + kBlock - 1) / kBlock)); }
 
-// rollout form: ORX_ROLLOUT=plain|pc overrides (diagnostics); by default the
-// producer/consumer kernel runs up to kPcMaxGames games (4 waves per SIMD for
-// the plain kernel), where the plain kernel cannot hide its own latencies.
-constexpr int64_t kPcMaxGames = 4 * 65536;
-inline bool use_pc_rollout(int64_t B) {
-  static const int forced = [] {
-    const char* e = getenv("ORX_ROLLOUT");
-    if (!e) return -1;
-    return strcmp(e, "pc") == 0 ? 1 : strcmp(e, "plain") == 0 ? 0 : -1;
-  }();
-  if (forced >= 0) return forced == 1;
-  return B <= kPcMaxGames;
-}
-
 inline Key make_key(uint64_t seed) { return Key{(uint32_t)seed, (uint32_t)(seed >> 32)}; }
 
 int check_sizes(int64_t B, int64_t off) {
@@ -1970,16 +1781,10 @@ int orx_rollout(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p1, 
   const bool rr = !grid && cfg->flags == 0 && policy_p1 == ORX_POLICY_RANDOM &&
                   policy_p2 == ORX_POLICY_RANDOM && obs && act &&
                   (uint64_t)B * ORX_OBS_FIELDS * 4u < (1ull << 31);
-  const bool pc = !grid && use_pc_rollout(B);
 #define ORX_ROLLOUT(N, R, G)                                                                    \
-  if (nc == N && rr == R && grid == G) {                                                        \
-    if (pc)                                                                                     \
-      hipLaunchKernelGGL((rollout_pc_kernel<N, R>), dim3((B + 63) / 64), dim3(128), 0, s, *cfg, \
-                         *st, policy_p1, policy_p2, n_ticks, obs, act, B, k, off);              \
-    else                                                                                        \
-      hipLaunchKernelGGL((rollout_kernel<N, R, G>), grid_for(B), dim3(kBlock), 0, s, *cfg, *st, \
-                         policy_p1, policy_p2, n_ticks, obs, act, B, k, off);                   \
-  }
+  if (nc == N && rr == R && grid == G)                                                          \
+    hipLaunchKernelGGL((rollout_kernel<N, R, G>), grid_for(B), dim3(kBlock), 0, s, *cfg, *st,   \
+                       policy_p1, policy_p2, n_ticks, obs, act, B, k, off);
   ORX_ROLLOUT(0, false, false) ORX_ROLLOUT(0, true, false) ORX_ROLLOUT(8, false, false)
   ORX_ROLLOUT(8, true, false) ORX_ROLLOUT(16, false, false) ORX_ROLLOUT(16, true, false)
   ORX_ROLLOUT(0, false, true) ORX_ROLLOUT(8, false, true) ORX_ROLLOUT(16, false, true)

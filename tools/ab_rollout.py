@@ -3,7 +3,7 @@ a fresh child process times the C3 headline rollout (65,536 games, 50-tick
 launches with obs+act) and, with --large, 2^21 games x 20 ticks.
 
     python tools/ab_rollout.py optimax_rogue_amd/liborx.so /tmp/liborx_b.so \
-        optimax_rogue_amd/liborx.so@ORX_ROLLOUT=plain
+        tools/ab_libs/diag4.so
 
 An argument ``path@VAR=value[@...]`` runs that library with environment
 variables set; ``@OBS=0`` drops the trajectory outputs.

@@ -1,6 +1,6 @@
 """Launch sequence for rocprofv3 counter passes (profiles/README.md):
   rollout at the bench config (C3, B=65536, 50 ticks with obs/act, x4:
-  rollout_pc_kernel<8, true>), then policy_kernel + step_kernel<8> at B=2^21
+  rollout_kernel<8, true, false>), then policy_kernel + step_kernel<8> at B=2^21
   (x6) and the plain rollout_kernel<8, true> at 2^21 x 20 ticks (x2)."""
 import os
 import sys
