@@ -176,10 +176,11 @@ def extras(torch, cfg, dev, B_cfg, K):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=2000, help="ticks in the timed region")
-    ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--steps", type=int, default=2048, help="ticks in the timed region")
+    ap.add_argument("--warmup", type=int, default=256)
     ap.add_argument("--batch", type=int, default=65536, help="games per GPU")
-    ap.add_argument("--chunk", type=int, default=50, help="ticks per rollout launch")
+    ap.add_argument("--chunk", type=int, default=128,
+                    help="ticks per rollout launch (the trajectory horizon a learner consumes)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true")

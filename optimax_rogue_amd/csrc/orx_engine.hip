@@ -73,6 +73,10 @@ constexpr uint32_t kDeadSlot = 0xFFFFu;
 #ifndef ORX_DIAG
 #define ORX_DIAG 0
 #endif
+#ifndef ORX_ROLLOUT_BLOCK
+#define ORX_ROLLOUT_BLOCK 256
+#endif
+constexpr int kRolloutBlock = ORX_ROLLOUT_BLOCK;  // rollout_kernel workgroup size
 
 struct Key {
   uint32_t k0, k1;
@@ -1182,7 +1186,8 @@ __device__ __forceinline__ void store_traj(int32_t* obs, int8_t* act, int32_t t,
 // FAST: both players are RandomBots and obs/act are both given (compile-time,
 // the common case: no per-tick uniform branches on policy codes or pointers).
 template <int NCAP, bool FAST, bool GRID>
-__global__ void __launch_bounds__(256) rollout_kernel(orx_cfg_t hc, orx_state_t st, int32_t pol1_,
+__global__ void __launch_bounds__(kRolloutBlock) rollout_kernel(orx_cfg_t hc, orx_state_t st,
+                                                                int32_t pol1_,
                                                       int32_t pol2_, int32_t n_ticks,
                                                       int32_t* __restrict__ obs,
                                                       int8_t* __restrict__ act, uint32_t B,
@@ -1783,7 +1788,8 @@ int orx_rollout(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p1, 
                   (uint64_t)B * ORX_OBS_FIELDS * 4u < (1ull << 31);
 #define ORX_ROLLOUT(N, R, G)                                                                    \
   if (nc == N && rr == R && grid == G)                                                          \
-    hipLaunchKernelGGL((rollout_kernel<N, R, G>), grid_for(B), dim3(kBlock), 0, s, *cfg, *st,   \
+    hipLaunchKernelGGL((rollout_kernel<N, R, G>), dim3((B + kRolloutBlock - 1) / kRolloutBlock),  \
+                       dim3(kRolloutBlock), 0, s, *cfg, *st,                                    \
                        policy_p1, policy_p2, n_ticks, obs, act, B, k, off);
   ORX_ROLLOUT(0, false, false) ORX_ROLLOUT(0, true, false) ORX_ROLLOUT(8, false, false)
   ORX_ROLLOUT(8, true, false) ORX_ROLLOUT(16, false, false) ORX_ROLLOUT(16, true, false)

@@ -1,5 +1,5 @@
 """Launch sequence for rocprofv3 counter passes (profiles/README.md):
-  rollout at the bench config (C3, B=65536, 50 ticks with obs/act, x4:
+  rollout at the bench config (C3, B=65536, 128 ticks with obs/act, x4:
   rollout_kernel<8, true, false>), then policy_kernel + step_kernel<8> at B=2^21
   (x6) and the plain rollout_kernel<8, true> at 2^21 x 20 ticks (x2)."""
 import os
@@ -12,7 +12,7 @@ from optimax_rogue_amd import EnvConfig
 from optimax_rogue_amd.engine import BatchedEngine
 
 dev = torch.device("cuda", 0)
-B, T = 65536, 50
+B, T = 65536, 128
 e = BatchedEngine(EnvConfig.c3(), B, seed=3, device=dev)
 obs = torch.empty((T, 14, B), dtype=torch.int32, device=dev)
 act = torch.empty((T, B, 2), dtype=torch.int8, device=dev)

@@ -31,6 +31,12 @@ def run(B, T=20, warm=40, reps=5, with_obs=True, cfg=None):
 
 
 def main():
+    if "--ticks" in sys.argv:   # per-launch intercept vs per-tick slope at the config batch
+        for T in (10, 25, 50, 100, 200):
+            us, v = run(65536, T=T, warm=200, reps=10)
+            print(json.dumps({"B": 65536, "T": T, "us": round(us, 2),
+                              "steps_per_s": f"{v:.3e}"}), flush=True)
+        return
     for B in (65536, 131072, 262144, 524288, 1 << 20, 1 << 21):
         for obs in (True, False):
             us, v = run(B, with_obs=obs)
