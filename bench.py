@@ -170,6 +170,36 @@ def extras(torch, cfg, dev, B_cfg, K):
     }
     del eng, obs, act
     torch.cuda.empty_cache()
+    # (3) the other BASELINE.json GPU configs, fused rollout with trajectories:
+    # C2 (4,096 games, 32x32, RandomBot) and C5 (128x128, StaircaseBot "ladder"
+    # policy, separation damage off and on) at its per-GPU share of 131,072
+    # games on 8 GPUs and at the whole 131,072 on this one
+    from optimax_rogue_amd import EnvConfig
+    from optimax_rogue_amd.enums import EXT_SEPARATION_DAMAGE
+
+    def rollout_rate(c, games, pol, T=128, reps=4):
+        e = BatchedEngine(c, games, seed=5, device=dev)
+        o = torch.empty((T, len(OBS_FIELDS), games), dtype=torch.int32, device=dev)
+        a = torch.empty((T, games, 2), dtype=torch.int8, device=dev)
+        e.rollout(T, pol, pol, obs=o, act=a)
+        d = timed_launches(torch, lambda: e.rollout(T, pol, pol, obs=o, act=a), reps)
+        us = sorted(d)[len(d) // 2]
+        del e, o, a
+        return {"games": games, "ticks_per_launch": T, "us_per_launch": us * 1e6,
+                "env_steps_per_s": games * T / us}
+
+    out["c2"] = dict(rollout_rate(EnvConfig.c2(), 4096, 1), policy="2x RandomBot", grid="32x32")
+    c5 = {}
+    for flag in (0, EXT_SEPARATION_DAMAGE):
+        c = EnvConfig.c5()
+        if flag:
+            c.flags, c.sep_period = flag, 8
+        key = "separation_damage_on" if flag else "separation_damage_off"
+        c5[key] = [rollout_rate(c, g, 2) for g in (131072 // 8, 131072)]
+    out["c5"] = dict(c5, policy="2x StaircaseBot", grid="128x128",
+                     note="separation damage = build extension EXT_SEPARATION_DAMAGE, "
+                          "sep_period 8 (parity unpinned: engine vs oracle only)")
+    torch.cuda.empty_cache()
     return out
 
 
