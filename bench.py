@@ -72,26 +72,66 @@ def rollout_kernel_name(B: int, K: int) -> str:
     return f"rollout_kernel<{ncap}, true, false>"
 
 
+def _cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or platform.machine()
+
+
 def cpu_baseline(cfg_dict: dict, seconds: float) -> dict:
-    """The C oracle (scalar port of the reference updater), one host core,
-    same workload shape; bounded to about `seconds` of CPU work."""
+    """The C oracle (scalar port of the reference updater) on the host cores,
+    same workload shape: one core for `seconds` * 0.4, then one thread per
+    core of this job's CPU share (at most 16, the GPU box's share per GPU) for
+    `seconds` * 1.5 / cores each -- about `seconds` * 2 of CPU work in all.
+    Each thread owns an oracle of 256 games (disjoint game ids); ctypes
+    releases the GIL inside the C calls, so the threads run in parallel."""
+    import threading
     from oracle.oracle import Oracle, build
     build()
     B = 256
-    ora = Oracle(cfg_dict, B, 3, 0)
-    ora.reset()
+
+    def leg(k, wall, out):
+        ora = Oracle(cfg_dict, B, 3, k * B)
+        ora.reset()
+        t0 = time.perf_counter()
+        ticks = 0
+        while True:
+            ora.rollout(1, 1, 50)
+            ticks += 50
+            el = time.perf_counter() - t0
+            if el >= wall:
+                break
+        out[k] = (ticks, el)
+
+    one = {}
+    leg(0, 0.4 * seconds, one)
+    single = B * one[0][0] / one[0][1]
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    cores = max(1, min(16, avail))
+    wall = max(1.0, 1.5 * seconds / cores)
+    res = {}
+    th = [threading.Thread(target=leg, args=(k, wall, res)) for k in range(cores)]
     t0 = time.perf_counter()
-    ticks = 0
-    while True:
-        ora.rollout(1, 1, 50)
-        ticks += 50
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
-    return {"value": B * ticks / el, "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": f"C oracle (scalar C restatement of Updater.update + RandomBot), {B} games x "
-                      f"{ticks} ticks of the same C3 workload on 1 host core "
-                      f"({platform.processor() or platform.machine()}), {el:.1f} s"}
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    el = time.perf_counter() - t0
+    total = sum(B * n for n, _ in res.values())
+    return {"value": total / el, "unit": "env-steps/s", "cores": cores, "kind": "port",
+            "per_core": total / el / cores, "single_core": single,
+            "sample": f"C oracle (scalar C restatement of Updater.update + RandomBot) on the "
+                      f"same C3 workload: {cores} threads x 256 games for {el:.1f} s "
+                      f"({total} env-steps), plus 1 core alone for "
+                      f"{one[0][1]:.1f} s; host {_cpu_model()}, {os.cpu_count()} CPUs visible, "
+                      f"{avail} in this job's affinity"}
 
 
 def timed_launches(torch, launch, n):
