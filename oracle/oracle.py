@@ -63,6 +63,7 @@ def lib():
             getattr(L, fn).argtypes = [vp, i64, vp, i32]
             getattr(L, fn).restype = i32
         L.oracle_philox.argtypes = [vp, vp, vp]
+        L.oracle_set_game.argtypes = [vp, i64, vp, i32, i32, i32]
         L.oracle_rollout.argtypes = [vp, i32, i32, i32, vp]
         L.oracle_set_rng.argtypes = [vp, u64, i64]
         L.oracle_set_bank.argtypes = [vp, vp, i32]
@@ -128,6 +129,12 @@ class Oracle:
              else np.ascontiguousarray(actions, np.int8).reshape(self.B, 2).copy())
         lib().oracle_policy(self._h, int(pol1), int(pol2), _ptr(a))
         return a
+
+    def set_game(self, g: int, ents, stairs):
+        """Test hook: game g becomes a hand-built depth-0 state (entities
+        [n][5] {iden, depth, x, y, health}, staircase (sx, sy)) at tick 1."""
+        e = np.ascontiguousarray(np.asarray(ents, np.int32).reshape(-1, 5))
+        lib().oracle_set_game(self._h, g, _ptr(e), len(e), int(stairs[0]), int(stairs[1]))
 
     def rollout(self, pol1: int, pol2: int, n_ticks: int):
         scratch = np.full((self.B, 2), 5, np.int8)

@@ -689,6 +689,95 @@ def run_case(R, name, spec):
           f"bytes={os.path.getsize(path)}")
 
 
+# --------------------------------------------------------------------------
+# Known-answer scenarios (SURVEY.md s4's semantics probes): hand-built states
+# on an 8x8 board (staircase at (5, 5); players health 10, damage 2, armor 1)
+# stepped once by the reference updater, initiative chosen by the seed
+# --------------------------------------------------------------------------
+KAT_CFG = dict(DEFAULT_CFG, width=8, height=8, n_npcs=2, npc_health=3, npc_damage=1,
+               npc_armor=0, max_ticks=1000)
+# name: (p1 (x, y, hp), p2 (x, y, hp), NPCs [(x, y, hp)], (m1, m2), p1 first)
+KAT_SCENARIOS = {
+    "swap_p1_first": ((2, 2, 10), (3, 2, 10), [], (2, 4), True),
+    "swap_p2_first": ((2, 2, 10), (3, 2, 10), [], (2, 4), False),
+    "block": ((2, 2, 10), (3, 2, 10), [], (2, 5), True),
+    "same_target_p1_first": ((2, 2, 10), (4, 2, 10), [], (2, 4), True),
+    "same_target_p2_first": ((2, 2, 10), (4, 2, 10), [], (2, 4), False),
+    "chase_p1_first": ((2, 2, 10), (3, 2, 10), [], (2, 2), True),
+    "chase_p2_first": ((2, 2, 10), (3, 2, 10), [], (2, 2), False),
+    "wall": ((1, 3, 10), (4, 4, 10), [], (4, 5), True),
+    "descend": ((4, 5, 10), (2, 2, 10), [], (2, 5), True),
+    "both_descend_p1_first": ((4, 5, 10), (5, 4, 10), [], (2, 3), True),
+    "both_descend_p2_first": ((4, 5, 10), (5, 4, 10), [], (2, 3), False),
+    "npc_kill": ((2, 4, 10), (6, 6, 10), [(3, 4, 1)], (2, 5), True),
+    "npc_both_hit": ((2, 3, 10), (4, 3, 10), [(3, 3, 2), (6, 6, 3)], (2, 4), False),
+    "mutual_kill": ((2, 2, 1), (3, 2, 1), [], (2, 4), True),
+    "kill_then_step": ((2, 2, 10), (3, 2, 1), [], (2, 1), True),
+}
+
+
+def kat_seed(p1_first):
+    """Smallest seed whose tick block (game 0, episode 0, tick 1) lets player
+    1 act first (CPython shuffle of [p1, p2]: randbelow(2) == 1) or not."""
+    for seed in range(1 << 20):
+        tb = TickBits(seed, 0, 0, 1, PUR_SHUFFLE)
+        r = tb.getrandbits(2)
+        while r >= 2:
+            r = tb.getrandbits(2)
+        if (r == 1) == p1_first:
+            return seed
+    raise RuntimeError("no seed")
+
+
+def make_scenarios(R):
+    names = list(KAT_SCENARIOS)
+    n = len(names)
+    init = np.zeros((n, 4, 5), np.int32)       # entities {iden, depth, x, y, health}, -1 = none
+    init[:, :, 0] = -1
+    moves = np.zeros((n, 2), np.int8)
+    seeds = np.zeros(n, np.uint64)
+    ev_len = np.zeros(n, np.int32)
+    events = []
+    final = {k: [] for k in ("p_x", "p_y", "p_depth", "p_health", "st_x", "st_y", "tick",
+                             "status", "npc_health", "npc_alive")}
+    ent_len = np.zeros(n, np.int32)
+    ents = []
+    for i, name in enumerate(names):
+        (x1, y1, h1), (x2, y2, h2), npcs, (m1, m2), first = KAT_SCENARIOS[name]
+        seed = kat_seed(first)
+        h = Harness(R, KAT_CFG, seed, 0)
+        tiles = np.full((8, 8), int(R.world.Tile.Ground), np.int32)
+        tiles[[0, -1], :] = int(R.world.Tile.Wall)
+        tiles[:, [0, -1]] = int(R.world.Tile.Wall)
+        tiles[5, 5] = int(R.world.Tile.StaircaseDown)
+        Ent = R.entities.Entity
+        es = [Ent(1, 0, x1, y1, h1, 10, 2, 1, [], dict()), Ent(2, 0, x2, y2, h2, 10, 2, 1, [], dict())]
+        for k, (nx, ny, nh) in enumerate(npcs):
+            es.append(Ent(3 + k, 0, nx, ny, nh, 3, 1, 0, [], dict()))
+        h.gs = R.state.GameState(True, 1, 1, 2, R.world.World({0: R.world.Dungeon(tiles)}), es)
+        h.gens = {0: 1}
+        for j, e in enumerate(es):
+            init[i, j] = (e.iden, e.depth, e.x, e.y, e.health)
+        moves[i] = (m1, m2)
+        seeds[i] = seed
+        evs = h.step([m1, m2])
+        ev_len[i] = len(evs)
+        events.extend(evs)
+        snap = h.snapshot()
+        for k in final:
+            final[k].append(snap[k])
+        ent_len[i] = len(snap["entities"])
+        ents.extend(snap["entities"])
+        print(f"kat {name}: seed {seed}, events {evs}, status {snap['status']}")
+    out = dict(names=np.array(names), init=init, moves=moves, seeds=seeds, ev_len=ev_len,
+               events=np.array(events, np.int32).reshape(-1, 4), ent_len=ent_len,
+               ents=np.array(ents, np.int32).reshape(-1, 5),
+               cfg_json=np.frombuffer(json.dumps(KAT_CFG).encode(), np.uint8))
+    for k, v in final.items():
+        out["final_" + k] = np.array(v, np.int64)
+    np.savez_compressed(os.path.join(HERE, "kat_scenarios.npz"), **out)
+
+
 def philox_kat():
     """Random123 known-answer vectors for Philox4x32-10 (kat_vectors)."""
     return [
@@ -704,6 +793,8 @@ def main():
         assert philox4x32_10(ctr, key) == want
     R = import_reference()
     only = sys.argv[1:]
+    if not only or "kat" in only:
+        make_scenarios(R)
     for name, spec in CASES.items():
         if only and name not in only:
             continue

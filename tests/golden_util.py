@@ -18,8 +18,10 @@ STATE_KEYS = ["p_x", "p_y", "p_depth", "p_health", "st_x", "st_y", "tick", "stat
 
 
 def case_names():
+    """Trajectory fixtures (every npz but the known-answer scenario table)."""
     return sorted(os.path.splitext(os.path.basename(p))[0]
-                  for p in glob.glob(os.path.join(GOLDEN_DIR, "*.npz")))
+                  for p in glob.glob(os.path.join(GOLDEN_DIR, "*.npz"))
+                  if not os.path.basename(p).startswith("kat_"))
 
 
 class Fixture:
@@ -97,3 +99,26 @@ def compare_state(got: dict, want: dict, K: int, where: str = ""):
             bad = np.argwhere(g.astype(np.int64) != w.astype(np.int64)) if g.shape == w.shape else None
             raise AssertionError(f"{where}: field {k} differs; first mismatches {bad[:5] if bad is not None else 'shape'}"
                                  f"\n got={g.ravel()[:16]}\nwant={w.ravel()[:16]}")
+
+
+class Kat:
+    """tests/golden/kat_scenarios.npz: SURVEY.md s4's semantics probes (swap,
+    block, same target, chase, wall, descend, NPC kill ...) as hand-built
+    one-tick states stepped by the reference updater (make_golden.py
+    make_scenarios)."""
+
+    def __init__(self):
+        self.z = np.load(os.path.join(GOLDEN_DIR, "kat_scenarios.npz"))
+        self.cfg = json.loads(bytes(self.z["cfg_json"]).decode())
+        self.names = [str(n) for n in self.z["names"]]
+        self._ev = np.concatenate([[0], np.cumsum(self.z["ev_len"])])
+        self._en = np.concatenate([[0], np.cumsum(self.z["ent_len"])])
+
+    def case(self, i):
+        z = self.z
+        ents = [tuple(int(v) for v in e) for e in z["init"][i] if e[0] >= 0]
+        events = [tuple(int(v) for v in r) for r in z["events"][self._ev[i]:self._ev[i + 1]]]
+        final = {k[6:]: z[k][i] for k in z.files if k.startswith("final_")}
+        out_ents = [tuple(int(v) for v in r) for r in z["ents"][self._en[i]:self._en[i + 1]]]
+        return dict(name=self.names[i], ents=ents, moves=[int(v) for v in z["moves"][i]],
+                    seed=int(z["seeds"][i]), events=events, final=final, entities=out_ents)

@@ -296,3 +296,55 @@ def test_empty_batch():
     eng = _engine(dict(width=8, height=8), 0, 1)
     eng.step(eng.policy(1, 1))
     eng.rollout(3, 1, 1)
+
+
+def _kat_cases():
+    from golden_util import Kat
+    k = Kat()
+    return [k.case(i) for i in range(len(k.names))]
+
+
+@pytest.mark.parametrize("case", _kat_cases(), ids=lambda c: c["name"])
+def test_known_answer_scenarios(case):
+    """SURVEY.md s4's semantics probes through orx_step_events and orx_step:
+    the hand-built state loaded into the engine, one tick, events and state
+    equal to the reference's (tests/golden/kat_scenarios.npz)."""
+    import torch
+    from golden_util import Kat
+    cfg = Kat().cfg
+    K = cfg["n_npcs"]
+    for events in (True, False):
+        eng = _engine(cfg, 1, case["seed"])
+        snap = eng.snapshot()
+        npc_pos = np.full((K, 1), 0xFFFF, np.int64)
+        npc_hp = np.zeros((K, 1), np.int64)
+        alive = 0
+        for iden, d, x, y, hp in case["ents"]:
+            if iden <= 2:
+                for f, v in (("p_x", x), ("p_y", y), ("p_depth", d), ("p_health", hp)):
+                    snap[f][iden - 1][0] = v
+            else:
+                npc_pos[iden - 3, 0] = x | (y << 8)
+                npc_hp[iden - 3, 0] = hp
+                alive |= 1 << (iden - 3)
+        snap.update(st_x=np.full((2, 1), 5), st_y=np.full((2, 1), 5), tick=np.array([1]),
+                    status=np.array([1]), episode=np.array([0]), npc_pos=npc_pos,
+                    npc_health=npc_hp, npc_alive=np.array([alive]))
+        eng.load_snapshot(snap)
+        acts = torch.tensor([case["moves"]], dtype=torch.int8, device=eng.device)
+        if events:
+            _, ev, n = eng.step(acts, events=True)
+            ev, n = ev.cpu().numpy(), int(n.cpu().numpy()[0])
+            assert [tuple(int(v) for v in r) for r in ev[0, :n]] == case["events"], case["name"]
+        else:
+            eng.step(acts)
+        s = eng.snapshot()
+        for k, v in case["final"].items():
+            got = np.asarray(s[k])
+            got = got[:, 0] if got.ndim == 2 else got[:1]
+            want = np.asarray(v).reshape(-1)[: got.size].reshape(got.shape)
+            if k == "npc_health":   # dead slots keep their last value; compare live ones
+                live = [j for j in range(K) if (int(case["final"]["npc_alive"]) >> j) & 1]
+                got, want = got[live], want[live]
+            assert np.array_equal(got, want), (case["name"], events, k, got, want)
+        torch.cuda.synchronize()

@@ -140,3 +140,31 @@ def test_ext_random_double_death(oracle_lib):
         for k in ("p_x", "p_y", "p_health", "tick", "episode"):
             assert np.array_equal(se[k], sb[k]), k
     assert double_deaths > 10 and wins == {2, 3}
+
+
+def _kat_cases():
+    from golden_util import Kat
+    k = Kat()
+    return [k.case(i) for i in range(len(k.names))]
+
+
+@pytest.mark.parametrize("case", _kat_cases(), ids=lambda c: c["name"])
+def test_known_answer_scenarios(oracle_lib, case):
+    """SURVEY.md s4's semantics probes (swap / block / same target / chase in
+    both initiative orders, wall, descend, both players descending in one
+    tick, NPC kill, NPC hit by both, mutual kill, a dead player still moving):
+    the oracle's one tick from the hand-built state equals the reference's."""
+    from golden_util import Kat
+    cfg = Kat().cfg
+    o = oracle_lib.Oracle(cfg, 1, case["seed"], 0, record_events=True)
+    o.set_game(0, case["ents"], (5, 5))
+    o.step(np.array([case["moves"]], np.int8))
+    assert o.events(0) == case["events"]
+    assert [e[:5] for e in o.entities(0)] == case["entities"]
+    s = o.export()
+    for k, v in case["final"].items():
+        if k in ("npc_health",):
+            continue
+        got = np.asarray(s[k])
+        got = got[:, 0] if got.ndim == 2 else got[0]
+        assert np.array_equal(got, np.asarray(v).reshape(got.shape)), (case["name"], k)
