@@ -73,10 +73,28 @@ constexpr uint32_t kDeadSlot = 0xFFFFu;
 #ifndef ORX_DIAG
 #define ORX_DIAG 0
 #endif
+// -DORX_STAMPS (diagnostic builds): rollout_kernel lane 0 of each wave
+// records s_memtime at 8 points into g_stamps; orx_diag_stamps copies them out.
+#ifdef ORX_STAMPS
+__device__ uint64_t g_stamps[65536 * 8];
+#define ORX_STAMP(j)                                                               \
+  if ((threadIdx.x & 63) == 0)                                                     \
+    g_stamps[(size_t)((blockIdx.x * blockDim.x + threadIdx.x) >> 6) * 8 + (j)] =   \
+        __builtin_amdgcn_s_memtime()
+#else
+#define ORX_STAMP(j) ((void)0)
+#endif
 #ifndef ORX_ROLLOUT_BLOCK
 #define ORX_ROLLOUT_BLOCK 256
 #endif
 constexpr int kRolloutBlock = ORX_ROLLOUT_BLOCK;  // rollout_kernel workgroup size
+#ifndef ORX_ROLLOUT_LANES
+#define ORX_ROLLOUT_LANES 64
+#endif
+// games per rollout wave (experiment: < 64 leaves lanes idle to put more waves
+// on each SIMD at a fixed batch)
+constexpr int kRolloutLanes = ORX_ROLLOUT_LANES;
+constexpr int kRolloutGamesPerBlock = kRolloutBlock / 64 * kRolloutLanes;
 
 struct Key {
   uint32_t k0, k1;
@@ -260,11 +278,35 @@ struct Npcs {
 #pragma unroll
       for (int r = 0; r < kRegs; ++r) {
         const uint32_t x = rd(r) ^ k2;
-        const uint32_t lo = (x & 0xFFFFu) == 0 ? 1u : 0u;
-        const uint32_t hi = (x >> 16) == 0 ? 2u : 0u;
-        hitmask |= (lo | hi) << (2 * r);
+        // zero-halfword flags as in any(): a low half is flagged iff zero; a
+        // high half can be falsely flagged only above a true low-half match,
+        // and the lowest flag wins
+        const uint32_t z = (x - 0x00010001u) & ~x & 0x80008000u;
+        hitmask |= ((z >> 15) | (z >> 30)) << (2 * r);  // bit 2r: low half, 2r+1: high
       }
-      return hitmask ? (int)__ffs(hitmask) - 1 : -1;
+      return hitmask ? (int)__builtin_ctz(hitmask) : -1;
+    }
+  }
+  // slot k := dead for a runtime k: 64-bit shifts over register pairs (a
+  // switch on k lowers to a branch ladder)
+  __device__ __forceinline__ void kill(int k) {
+    if constexpr (NCAP > 0) {
+      const uint64_t m = 0xFFFFull << (16 * (k & 3));
+      const int j = k >> 2;
+      uint64_t p = (uint64_t)q0 | ((uint64_t)q1 << 32);
+      p |= j == 0 ? m : 0ull;
+      q0 = (uint32_t)p; q1 = (uint32_t)(p >> 32);
+      p = (uint64_t)q2 | ((uint64_t)q3 << 32);
+      p |= j == 1 ? m : 0ull;
+      q2 = (uint32_t)p; q3 = (uint32_t)(p >> 32);
+      if constexpr (NCAP > 8) {
+        p = (uint64_t)q4 | ((uint64_t)q5 << 32);
+        p |= j == 2 ? m : 0ull;
+        q4 = (uint32_t)p; q5 = (uint32_t)(p >> 32);
+        p = (uint64_t)q6 | ((uint64_t)q7 << 32);
+        p |= j == 3 ? m : 0ull;
+        q6 = (uint32_t)p; q7 = (uint32_t)(p >> 32);
+      }
     }
   }
 };
@@ -753,10 +795,66 @@ __device__ __forceinline__ void policy_pair(Key key, uint32_t game, uint32_t ep,
 // ---------------------------------------------------------------------------
 // The tick
 // ---------------------------------------------------------------------------
-struct NpcMem {  // HBM rows of this game's NPC slots (stride B)
+// NPC health, two stores with one interface (get: the int8 value sign-extended;
+// put: its low byte).  NpcMem: the HBM rows (stride B), read only when a hit
+// happens -- the step kernels, where other waves hide that load.  NpcHpRegs:
+// one byte per slot in registers, loaded and stored once per launch -- the
+// rollout, whose lone wave per SIMD would otherwise stall a full HBM round
+// trip on every tick in which one of its 64 games hits an NPC.
+struct NpcMem {
   uint16_t* pos;
   int8_t* hp;
   uint32_t B, i;
+  __device__ __forceinline__ int get(int k) const { return hp[(size_t)k * B + i]; }
+  __device__ __forceinline__ void put(int k, int v) const { hp[(size_t)k * B + i] = (int8_t)v; }
+};
+
+template <int NCAP>
+struct NpcHpRegs {
+  // slot k: byte k & 3 of h[k >> 2], i.e. byte k & 7 of the 64-bit pair
+  // (h0, h1) or (h2, h3) by k >> 3 -- a runtime k through 64-bit shifts, no
+  // switch (which lowers to a branch ladder)
+  uint32_t h0, h1, h2, h3;
+  __device__ __forceinline__ int get(int k) const {
+    const uint64_t p = (NCAP <= 8 || (k >> 3) == 0) ? ((uint64_t)h0 | ((uint64_t)h1 << 32))
+                                                    : ((uint64_t)h2 | ((uint64_t)h3 << 32));
+    return (int)(int8_t)(p >> (8 * (k & 7)));
+  }
+  __device__ __forceinline__ void put(int k, int v) {
+    const int sh = 8 * (k & 7);
+    const uint64_t m = 0xFFull << sh, b = (uint64_t)((uint32_t)v & 0xFFu) << sh;
+    uint64_t p = (uint64_t)h0 | ((uint64_t)h1 << 32);
+    p = (k >> 3) == 0 ? ((p & ~m) | b) : p;
+    h0 = (uint32_t)p; h1 = (uint32_t)(p >> 32);
+    if constexpr (NCAP > 8) {
+      p = (uint64_t)h2 | ((uint64_t)h3 << 32);
+      p = (k >> 3) == 1 ? ((p & ~m) | b) : p;
+      h2 = (uint32_t)p; h3 = (uint32_t)(p >> 32);
+    }
+  }
+  __device__ __forceinline__ void fill(int v) {
+    h0 = h1 = h2 = h3 = ((uint32_t)v & 0xFFu) * 0x01010101u;
+  }
+  // unconditional loads, as load_npcs (slots >= K hold a copy of slot K-1)
+  __device__ __forceinline__ void load(const int8_t* hp, int K, uint32_t B, uint32_t i) {
+    uint32_t v[NCAP];
+#pragma unroll
+    for (int k = 0; k < NCAP; ++k) v[k] = (uint8_t)hp[(size_t)min(k, K - 1) * B + i];
+    h0 = h1 = h2 = h3 = 0;
+#pragma unroll
+    for (int k = 0; k < NCAP; ++k) h0 = k < 4 ? (h0 | v[k] << (8 * k)) : h0;
+#pragma unroll
+    for (int k = 4; k < NCAP; ++k) h1 = k < 8 ? (h1 | v[k] << (8 * (k - 4))) : h1;
+#pragma unroll
+    for (int k = 8; k < NCAP; ++k) h2 = k < 12 ? (h2 | v[k] << (8 * (k - 8))) : h2;
+#pragma unroll
+    for (int k = 12; k < NCAP; ++k) h3 = h3 | v[k] << (8 * (k - 12));
+  }
+  __device__ __forceinline__ void store(int8_t* hp, int K, uint32_t B, uint32_t i) const {
+#pragma unroll
+    for (int k = 0; k < NCAP; ++k)
+      if (k < K) hp[(size_t)k * B + i] = (int8_t)get(k);
+  }
 };
 
 // handle_move for `self` (updater.py:180-243), branch-free except for the
@@ -804,19 +902,15 @@ __device__ __forceinline__ bool handle_move(const Cfg& c, Key key, Src& src, Pla
 
 // handle_combat on NPC defenders, then the death sweep (updater.py:136-145):
 // only NPCs hit this tick can reach health <= 0.
-template <int NCAP, bool EV>
-__device__ __forceinline__ void npc_hits(const Cfg& c, Npcs<NCAP>& npc, const NpcMem& m, int h0,
-                                         int h1, bool writer, Deltas& dl, Events<EV>& ev) {
+template <int NCAP, bool EV, class M>
+__device__ __forceinline__ void npc_hits(const Cfg& c, Npcs<NCAP>& npc, M& m, int h0, int h1,
+                                         Deltas& dl, Events<EV>& ev) {
   const int dmg = c.player_dmg_net > 0 ? c.player_dmg_net : 0;
-  int8_t* p0 = m.hp + (size_t)(h0 >= 0 ? h0 : h1) * m.B + m.i;
-  int8_t* p1 = m.hp + (size_t)(h1 >= 0 ? h1 : h0) * m.B + m.i;
-  int v0 = *p0, v1 = *p1;
+  int v0 = m.get(h0 >= 0 ? h0 : h1), v1 = m.get(h1 >= 0 ? h1 : h0);
   if (h0 >= 0) v0 -= dmg;
   if (h1 >= 0) { v1 = (h1 == h0) ? v0 - dmg : v1 - dmg; if (h1 == h0) v0 = v1; }
-  if (writer) {
-    if (h0 >= 0) *p0 = (int8_t)v0;
-    if (h1 >= 0 && h1 != h0) *p1 = (int8_t)v1;
-  }
+  if (h0 >= 0) m.put(h0, v0);
+  if (h1 >= 0 && h1 != h0) m.put(h1, v1);
   // the sweep walks GameState.entities backwards: higher slot first
   const bool swap = h1 > h0;
   const int ks[2] = {swap ? h1 : h0, swap ? h0 : h1};
@@ -826,7 +920,7 @@ __device__ __forceinline__ void npc_hits(const Cfg& c, Npcs<NCAP>& npc, const Np
     const int k = ks[j];
     if (k >= 0 && (int8_t)vs[j] <= 0 && ((npc.alive >> k) & 1u)) {
       npc.alive &= ~(1u << k);
-      npc.set(k, kDeadSlot);
+      npc.kill(k);
       dl.npc_death += 1;
       ev.emit(ORX_EV_DEATH, 3 + k, 0, 0);
     }
@@ -834,12 +928,12 @@ __device__ __forceinline__ void npc_hits(const Cfg& c, Npcs<NCAP>& npc, const Np
 }
 
 // One Updater.update for an in-progress game; p1.move/p2.move = raw moves.
-template <int NCAP, bool EV, bool GRID, class Src>
+template <int NCAP, bool EV, bool GRID, class Src, class M>
 __device__ __forceinline__ void tick_game(const Cfg& c, Key key, Src& src, uint32_t game,
-                                          uint32_t ep, bool p1_first, bool writer, Player& p1,
-                                          Player& p2, Npcs<NCAP>& npc, const NpcMem& m,
-                                          int32_t& tick, int32_t& status, bool& err, Deltas& dl,
-                                          Events<EV>& ev, int32_t& sep_start) {
+                                          uint32_t ep, bool p1_first, Player& p1, Player& p2,
+                                          Npcs<NCAP>& npc, M& m, int32_t& tick, int32_t& status,
+                                          bool& err, Deltas& dl, Events<EV>& ev,
+                                          int32_t& sep_start) {
   calc_pos(p1.x, p1.y, p1.move, p1.tx, p1.ty);         // updater.py:89-98
   if (blocked<GRID>(c, p1.lay, p1.tx, p1.ty)) p1.move = ORX_MOVE_STAY;
   calc_pos(p2.x, p2.y, p2.move, p2.tx, p2.ty);
@@ -863,7 +957,7 @@ __device__ __forceinline__ void tick_game(const Cfg& c, Key key, Src& src, uint3
     // the targets now are the ones that were attacked.
     const int h0 = hA ? npc.find(pack_xy(A.tx, A.ty)) : -1;
     const int h1 = hB ? npc.find(pack_xy(Bp.tx, Bp.ty)) : -1;
-    npc_hits(c, npc, m, h0, h1, writer, dl, ev);
+    npc_hits(c, npc, m, h0, h1, dl, ev);
   }
   p1 = pick(p1_first, A, Bp);
   p2 = pick(p1_first, Bp, A);
@@ -903,15 +997,110 @@ __device__ __forceinline__ void tick_game(const Cfg& c, Key key, Src& src, uint3
   dl.eps += (uint32_t)(s - ORX_PLAYER1_WIN) <= (uint32_t)(ORX_TIE - ORX_PLAYER1_WIN) ? 1 : 0;
 }
 
-template <int NCAP, bool EV, bool GRID = false>
+template <int NCAP, bool EV, bool GRID = false, class M>
 __device__ __forceinline__ void tick_game(const Cfg& c, Key key, uint32_t game, uint32_t ep,
-                                          bool p1_first, bool writer, Player& p1, Player& p2,
-                                          Npcs<NCAP>& npc, const NpcMem& m, int32_t& tick,
+                                          bool p1_first, Player& p1, Player& p2,
+                                          Npcs<NCAP>& npc, M& m, int32_t& tick,
                                           int32_t& status, bool& err, Deltas& dl,
                                           Events<EV>& ev, int32_t& sep_start) {
   PhiloxSrc src{key, game, ep};
-  tick_game<NCAP, EV, GRID>(c, key, src, game, ep, p1_first, writer, p1, p2, npc, m, tick, status,
-                            err, dl, ev, sep_start);
+  tick_game<NCAP, EV, GRID>(c, key, src, game, ep, p1_first, p1, p2, npc, m, tick, status, err,
+                            dl, ev, sep_start);
+}
+
+// The rollout's tick: Updater.update (updater.py:76-162) with a straight
+// common path.  When neither player can meet the other this tick -- other
+// depth, or neither target is the other's cell nor the other's target --
+// the move order drawn by the initiative shuffle (:114) is unobservable: each
+// handle_move (:180-243) resolves against the other's unchanged cell, and NPCs
+// never move and are swept only after both moves (:136-145), so a hit does not
+// depend on the order either.  Such ticks (all but a few per thousand) skip the
+// shuffle decode and the ordered pair of moves.  The ordered path (tick_game)
+// takes the rest: a possible meeting, a step onto a staircase (descend draws
+// the SPAWN stream in move order), extension flags, and a tick whose shuffle
+// bits all reject (its stream fallback can stop the game).  Player health only
+// changes on the ordered path, so the common path's status is the max_ticks
+// test alone.  Invariants used: two players on one depth never share a cell,
+// and no player stands on its depth's staircase or on an NPC (spawns and moves
+// exclude them).  Counters: the ordered path counts the game's end itself.
+template <int NCAP, bool GRID, class M>
+__device__ __forceinline__ void tick_rollout(const Cfg& c, Key key, uint32_t game, uint32_t ep,
+                                             uint32_t pk_shf, Player& p1, Player& p2,
+                                             Npcs<NCAP>& npc, M& m, int32_t& tick,
+                                             int32_t& status, Deltas& dl, int32_t& sep) {
+  // effective targets: the player's own cell when staying or blocked
+  calc_pos(p1.x, p1.y, p1.move, p1.tx, p1.ty);
+  calc_pos(p2.x, p2.y, p2.move, p2.tx, p2.ty);
+  const bool b1 = blocked<GRID>(c, p1.lay, p1.tx, p1.ty);
+  const bool b2 = blocked<GRID>(c, p2.lay, p2.tx, p2.ty);
+  const int32_t t1x = b1 ? p1.x : p1.tx, t1y = b1 ? p1.y : p1.ty;
+  const int32_t t2x = b2 ? p2.x : p2.tx, t2y = b2 ? p2.y : p2.ty;
+  // meet: same depth and (target 1 == cell 2 or target 2 == cell 1 or
+  // target 1 == target 2), as one zero test over xor differences
+  const uint32_t e12 = (uint32_t)(t1x ^ p2.x) | (uint32_t)(t1y ^ p2.y);
+  const uint32_t e21 = (uint32_t)(t2x ^ p1.x) | (uint32_t)(t2y ^ p1.y);
+  const uint32_t e11 = (uint32_t)(t1x ^ t2x) | (uint32_t)(t1y ^ t2y);
+  const bool meet = ((uint32_t)(p1.d ^ p2.d) | min(e12, min(e21, e11))) == 0u;
+  const uint32_t k1 = pack_xy(t1x, t1y), k2 = pack_xy(t2x, t2y);  // NPC keys (W, H <= 256)
+  const bool hit1 = NCAP > 0 && ((p1.d == c.d1) & npc.any(k1));
+  const bool hit2 = NCAP > 0 && ((p2.d == c.d1) & npc.any(k2));
+  const bool st1 = stair_tile<GRID>(c, p1, t1x, t1y), st2 = stair_tile<GRID>(c, p2, t2x, t2y);
+  const bool shf_reject = (~(pk_shf >> 1) & 0x55555555u) == 0u;
+  // a descend into the other player's depth depends on the move order (the
+  // spawn cell's occupancy test, and the other's later move into the spawn cell)
+  const bool desc_meet = (st1 & (p2.d == p1.d + 1)) | (st2 & (p1.d == p2.d + 1));
+  const bool ordered = meet | (st1 & st2) | desc_meet | shf_reject | (c.ext != 0);
+  // The ordered lanes run first, in an if without else placed out of line;
+  // the common path below is gated by selects (an if/else would put a taken
+  // branch around one of the two bodies on every tick).  `fast` is laundered
+  // so the compiler cannot rebuild the if/else from the two conditions.
+  uint32_t fast = ordered ? 0u : 1u;
+  asm volatile("" : "+v"(fast));
+  if (ORX_UNLIKELY(ordered)) {
+    bool err = false;
+    const bool p1_first = first_from_packed(pk_shf, key, game, ep, tick, err);
+    Events<false> ev{nullptr, 0};
+    tick_game<NCAP, false, GRID>(c, key, game, ep, p1_first, p1, p2, npc, m, tick, status, err,
+                                 dl, ev, sep);
+  }
+  const bool f = fast != 0u;
+  const bool s1 = f & !hit1 & !st1, s2 = f & !hit2 & !st2;
+  p1.x = s1 ? t1x : p1.x;
+  p1.y = s1 ? t1y : p1.y;
+  p2.x = s2 ? t2x : p2.x;
+  p2.y = s2 ? t2y : p2.y;
+  if (NCAP > 0 && ORX_UNLIKELY(f & (hit1 | hit2))) {
+    Events<false> ev{nullptr, 0};
+    dl.combat += (hit1 ? 1 : 0) + (hit2 ? 1 : 0);
+    npc_hits(c, npc, m, hit1 ? npc.find(k1) : -1, hit2 ? npc.find(k2) : -1, dl, ev);
+  }
+  // One player steps onto its staircase (updater.py:205-208) and descends
+  // (handle_descend, :259-296) to a depth the other player is not on: then
+  // nothing in it depends on the move order (dungeon presence reads only the
+  // other's depths, the spawn cell's occupancy test never matches the other,
+  // NPCs are swept after both moves, and the SPAWN stream has one consumer).
+  const int32_t t0 = tick;
+  const int32_t ft = tick + 1;
+  const bool end = c.max_ticks && ft >= c.max_ticks;
+  tick = f ? ft : tick;
+  status = f ? (end ? ORX_TIE : ORX_IN_PROGRESS) : status;
+  dl.eps += (f & end) ? 1 : 0;
+  if (ORX_UNLIKELY(f & (st1 | st2))) {
+    PhiloxSrc src{key, game, ep};
+    auto spawn = src.spawn(t0);
+    Events<false> ev{nullptr, 0};
+    bool err = false;
+    Player S = pick(st1, p1, p2);
+    const Player O = pick(st1, p2, p1);
+    descend<NCAP, false, GRID>(c, key, src, S, O, st1 ? c.d2 : c.d1, npc, spawn, dl, err,
+                               st1 ? 1 : 2, ev);
+    p1 = pick(st1, S, p1);
+    p2 = pick(st1, p2, S);
+    if (err) {  // an exhausted spawn stream stops the game (never observed)
+      dl.eps -= end ? 1 : 0;
+      status = ORX_STATUS_RNG_EXHAUSTED;
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -947,43 +1136,60 @@ __device__ __forceinline__ void store_players(const orx_state_t& st, uint32_t B,
   }
 }
 
+// Every slot's row is loaded unconditionally (slot k >= K re-reads row K-1
+// and is masked off): a `k < K` guard would put each load behind a branch and
+// a vmcnt(0) wait, and a lone wave per SIMD then pays one HBM round trip per
+// slot (measured: a dozen serialized round trips per rollout launch).
 template <int NCAP>
 __device__ __forceinline__ void load_npcs(const orx_state_t& st, const Cfg& c, uint32_t B,
                                           uint32_t i, Npcs<NCAP>& npc) {
   npc.clear();
   if constexpr (NCAP > 0) {
+    uint32_t v[NCAP];
+#pragma unroll
+    for (int k = 0; k < NCAP; ++k)
+      v[k] = st.npc_pos[(size_t)min(k, c.K - 1) * B + i];
     npc.alive = st.npc_alive[i];
 #pragma unroll
-    for (int k = 0; k < NCAP; ++k) {
-      const uint32_t v = k < c.K ? (uint32_t)st.npc_pos[(size_t)k * B + i] : kDeadSlot;
-      npc.set(k, ((npc.alive >> k) & 1u) ? v : kDeadSlot);
-    }
+    for (int k = 0; k < NCAP; ++k)
+      npc.set(k, (k < c.K && ((npc.alive >> k) & 1u)) ? v[k] : kDeadSlot);
   }
 }
 
 // After a game start: NPC positions and health to HBM.
 template <int NCAP>
 __device__ __forceinline__ void store_new_npcs(const orx_state_t& st, const Cfg& c, uint32_t B,
-                                            uint32_t i, const Npcs<NCAP>& npc) {
+                                            uint32_t i, const Npcs<NCAP>& npc,
+                                            bool health = true) {
   if constexpr (NCAP > 0) {
     for (int k = 0; k < c.K; ++k) {
       st.npc_pos[(size_t)k * B + i] = (uint16_t)npc.get(k);
-      st.npc_health[(size_t)k * B + i] = (int8_t)c.npc_hp;
+      if (health) st.npc_health[(size_t)k * B + i] = (int8_t)c.npc_hp;
     }
   }
 }
 
+// All reads first, then all writes: interleaved read-modify-writes of
+// may-alias int32 rows would serialize into one HBM round trip each.
 __device__ __forceinline__ void flush_deltas(const orx_state_t& st, uint32_t B, uint32_t i,
                                              const Deltas& dl) {
-  if (st.counters && (dl.combat | dl.descend | dl.dungeon | dl.npc_death)) {
-    st.counters[i] += dl.combat;
-    st.counters[B + i] += dl.descend;
-    st.counters[2 * (size_t)B + i] += dl.dungeon;
-    st.counters[3 * (size_t)B + i] += dl.npc_death;
-  }
-  if (dl.eps) {
-    st.ret_sum[i] += dl.ret;
-    st.ep_count[i] += dl.eps;
+  const bool cnt = st.counters && (dl.combat | dl.descend | dl.dungeon | dl.npc_death);
+  if (cnt || dl.eps) {
+    // without counters the four reads hit ret_sum[i] (valid, unused)
+    const int32_t* c = (st.counters ? st.counters : st.ret_sum) + i;
+    const size_t cs = st.counters ? B : 0;
+    const int32_t c0 = c[0], c1 = c[cs], c2 = c[2 * cs], c3 = c[3 * cs];
+    const int32_t r = st.ret_sum[i], e = st.ep_count[i];
+    if (cnt) {
+      st.counters[i] = c0 + dl.combat;
+      st.counters[B + i] = c1 + dl.descend;
+      st.counters[2 * (size_t)B + i] = c2 + dl.dungeon;
+      st.counters[3 * (size_t)B + i] = c3 + dl.npc_death;
+    }
+    if (dl.eps) {
+      st.ret_sum[i] = r + dl.ret;
+      st.ep_count[i] = e + dl.eps;
+    }
   }
 }
 
@@ -1085,13 +1291,13 @@ __global__ void __launch_bounds__(256) step_kernel(orx_cfg_t hc, orx_state_t st,
   int32_t tick = st.tick[i];
   load_players<GRID>(st, B, i, p1, p2);
   load_npcs(st, c, B, i, npc);
-  const NpcMem m{st.npc_pos, st.npc_health, B, i};
+  NpcMem m{st.npc_pos, st.npc_health, B, i};
   Deltas dl = {0, 0, 0, 0, 0, 0};
   Events<EV> ev{EV ? events + (size_t)i * ORX_MAX_EVENTS * 4 : nullptr, 0};
   bool err = false;
   const bool p1_first = p1_first_draw(key, game, ep, tick, err);
   int32_t sep = (c.ext & ORX_EXT_SEPARATION_DAMAGE) ? st.sep_start[i] : -1;
-  tick_game<NCAP, EV, GRID>(c, key, game, ep, p1_first, true, p1, p2, npc, m, tick, status, err,
+  tick_game<NCAP, EV, GRID>(c, key, game, ep, p1_first, p1, p2, npc, m, tick, status, err,
                             dl, ev, sep);
   if (c.ext & ORX_EXT_SEPARATION_DAMAGE) st.sep_start[i] = sep;
   store_players<GRID>(st, B, i, p1, p2, dl.descend != 0);
@@ -1207,11 +1413,16 @@ __global__ void __launch_bounds__(kRolloutBlock) rollout_kernel(orx_cfg_t hc, or
                                                       Key key, uint32_t off) {
   const int32_t pol1 = FAST ? (int32_t)ORX_POLICY_RANDOM : pol1_;
   const int32_t pol2 = FAST ? (int32_t)ORX_POLICY_RANDOM : pol2_;
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if constexpr (kRolloutLanes < 64) {
+    if ((threadIdx.x & 63u) >= (uint32_t)kRolloutLanes) return;
+    i = (i >> 6) * kRolloutLanes + (threadIdx.x & 63u);
+  }
   if (i >= B) return;
   Cfg c = make_cfg(hc, st);
   if (FAST) c.ext = 0;  // FAST launches require flags == 0
   const uint32_t game = off + i;
+  ORX_STAMP(0);
   Player p1, p2;
   load_players<GRID>(st, B, i, p1, p2);
   int32_t tick = st.tick[i];
@@ -1219,35 +1430,36 @@ __global__ void __launch_bounds__(kRolloutBlock) rollout_kernel(orx_cfg_t hc, or
   uint32_t ep = (uint32_t)st.episode[i];
   Npcs<NCAP> npc;
   load_npcs(st, c, B, i, npc);
-  const NpcMem m{st.npc_pos, st.npc_health, B, i};
+  NpcHpRegs<NCAP> hp;
+  if constexpr (NCAP > 0) hp.load(st.npc_health, c.K, B, i);
   Deltas dl = {0, 0, 0, 0, 0, 0};
   int32_t sep = (c.ext & ORX_EXT_SEPARATION_DAMAGE) ? st.sep_start[i] : -1;
-  bool stairs_dirty = false, npc_dirty = false;
+  bool restarted = false;
   TrajWriter<FAST> traj(obs, act, B, i);
+#ifdef ORX_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+  ORX_STAMP(1);
   for (int32_t t = 0; t < n_ticks; ++t) {
+#ifdef ORX_STAMPS
+    if (t == 64) { ORX_STAMP(2); }
+#endif
     // one tick block: the bots' bits and the initiative bits (drawn although
     // only in-progress games use the latter)
     W4 tb = tick_block(key, game, ep, tick);
     if (ORX_DIAG & 1) tb.b = tb.c = ((uint32_t)tick * 0x9E3779B9u) ^ (game * 0x85EBCA6Bu);
-    const uint32_t pk_shf = (ORX_DIAG & 2) ? 0u : tb.a;
+    const uint32_t pk_shf = (ORX_DIAG & 2) ? 0x55555555u : tb.a;
     int32_t a1 = ORX_MOVE_STAY, a2 = ORX_MOVE_STAY;
     policy_pair(key, game, ep, tick, pol1, pol2, tb, p1, p2, a1, a2);
     if (ORX_LIKELY(status == ORX_IN_PROGRESS)) {
       p1.move = a1; p2.move = a2;
-      const int32_t descents = dl.descend;
-      bool err = false;
-      const bool p1_first = (ORX_DIAG & 2) ? (((uint32_t)tick ^ game) & 1u) != 0
-                                           : first_from_packed(pk_shf, key, game, ep, tick, err);
-      Events<false> ev{nullptr, 0};
       if (ORX_DIAG & 4) {
         tick += 1;
-        p1.x ^= p1_first;
+        p1.x ^= (int32_t)(pk_shf & 1u);
         status = (c.max_ticks && tick >= c.max_ticks) ? ORX_TIE : ORX_IN_PROGRESS;
       } else {
-        tick_game<NCAP, false, GRID>(c, key, game, ep, p1_first, true, p1, p2, npc, m, tick,
-                                     status, err, dl, ev, sep);
+        tick_rollout<NCAP, GRID>(c, key, game, ep, pk_shf, p1, p2, npc, hp, tick, status, dl, sep);
       }
-      stairs_dirty |= dl.descend != descents;
     } else if (c.autoreset) {
       ep += 1;
       if (ORX_DIAG & 8) {
@@ -1255,21 +1467,31 @@ __global__ void __launch_bounds__(kRolloutBlock) rollout_kernel(orx_cfg_t hc, or
         status = ORX_IN_PROGRESS;
       } else {
         setup_game<NCAP, GRID>(c, key, game, ep, p1, p2, npc, tick, status);
-        if constexpr (NCAP > 0) store_new_npcs(st, c, B, i, npc);
+        if constexpr (NCAP > 0) {
+          store_new_npcs(st, c, B, i, npc, false);  // health: from hp at the end
+          hp.fill(c.npc_hp);
+        }
       }
-      stairs_dirty = true;
-      npc_dirty = true;
+      restarted = true;
       sep = -1;
     }
     if (!(ORX_DIAG & 16)) traj.write(t, p1, p2, tick, status, a1, a2);
   }
-  store_players<GRID>(st, B, i, p1, p2, stairs_dirty);
+  ORX_STAMP(3);
+  store_players<GRID>(st, B, i, p1, p2, restarted || dl.descend != 0);
   st.tick[i] = tick;
   st.status[i] = status;
   st.episode[i] = (int32_t)ep;
   if (c.ext & ORX_EXT_SEPARATION_DAMAGE) st.sep_start[i] = sep;
-  if (NCAP > 0 && (npc_dirty || dl.npc_death)) st.npc_alive[i] = npc.alive;
+  if constexpr (NCAP > 0) {
+    if (restarted || dl.npc_death) st.npc_alive[i] = npc.alive;
+    if (restarted || dl.combat) hp.store(st.npc_health, c.K, B, i);
+  }
   flush_deltas(st, B, i, dl);
+#ifdef ORX_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+  ORX_STAMP(4);
 }
 
 // Staircases of arbitrary (game, episode, depth, generation) dungeons, for
@@ -1442,7 +1664,7 @@ __global__ void __launch_bounds__(256) mt_step_kernel(orx_cfg_t hc, orx_state_t 
   int32_t tick = st.tick[i];
   load_players<GRID>(st, B, i, p1, p2);
   load_npcs(st, c, B, i, npc);
-  const NpcMem m{st.npc_pos, st.npc_health, B, i};
+  NpcMem m{st.npc_pos, st.npc_health, B, i};
   Deltas dl = {0, 0, 0, 0, 0, 0};
   Events<EV> ev{EV ? events + (size_t)i * ORX_MAX_EVENTS * 4 : nullptr, 0};
   bool err = false;
@@ -1450,7 +1672,7 @@ __global__ void __launch_bounds__(256) mt_step_kernel(orx_cfg_t hc, orx_state_t 
   src.open(st, B, i);
   const bool p1_first = mt_shuffles(src.py, npc, err);
   int32_t sep = (c.ext & ORX_EXT_SEPARATION_DAMAGE) ? st.sep_start[i] : -1;
-  tick_game<NCAP, EV, GRID>(c, key, src, game, ep, p1_first, true, p1, p2, npc, m, tick, status,
+  tick_game<NCAP, EV, GRID>(c, key, src, game, ep, p1_first, p1, p2, npc, m, tick, status,
                             err, dl, ev, sep);
   src.close();
   if (c.ext & ORX_EXT_SEPARATION_DAMAGE) st.sep_start[i] = sep;
@@ -1480,7 +1702,7 @@ __global__ void __launch_bounds__(256) mt_rollout_kernel(orx_cfg_t hc, orx_state
   uint32_t ep = (uint32_t)st.episode[i];
   Npcs<NCAP> npc;
   load_npcs(st, c, B, i, npc);
-  const NpcMem m{st.npc_pos, st.npc_health, B, i};
+  NpcMem m{st.npc_pos, st.npc_health, B, i};
   Deltas dl = {0, 0, 0, 0, 0, 0};
   int32_t sep = (c.ext & ORX_EXT_SEPARATION_DAMAGE) ? st.sep_start[i] : -1;
   bool stairs_dirty = false, npc_dirty = false;
@@ -1496,7 +1718,7 @@ __global__ void __launch_bounds__(256) mt_rollout_kernel(orx_cfg_t hc, orx_state
       const int32_t descents = dl.descend;
       const bool p1_first = mt_shuffles(src.py, npc, err);
       Events<false> ev{nullptr, 0};
-      tick_game<NCAP, false, GRID>(c, key, src, game, ep, p1_first, true, p1, p2, npc, m, tick,
+      tick_game<NCAP, false, GRID>(c, key, src, game, ep, p1_first, p1, p2, npc, m, tick,
                                    status, err, dl, ev, sep);
       stairs_dirty |= dl.descend != descents;
     } else if (c.autoreset) {
@@ -1803,7 +2025,8 @@ int orx_rollout(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p1, 
                   (uint64_t)B * ORX_OBS_FIELDS * 4u < (1ull << 31);
 #define ORX_ROLLOUT(N, R, G)                                                                    \
   if (nc == N && rr == R && grid == G)                                                          \
-    hipLaunchKernelGGL((rollout_kernel<N, R, G>), dim3((B + kRolloutBlock - 1) / kRolloutBlock),  \
+    hipLaunchKernelGGL((rollout_kernel<N, R, G>),                                               \
+                       dim3((B + kRolloutGamesPerBlock - 1) / kRolloutGamesPerBlock),            \
                        dim3(kRolloutBlock), 0, s, *cfg, *st,                                    \
                        policy_p1, policy_p2, n_ticks, obs, act, B, k, off);
   ORX_ROLLOUT(0, false, false) ORX_ROLLOUT(0, true, false) ORX_ROLLOUT(8, false, false)
@@ -1812,6 +2035,13 @@ int orx_rollout(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p1, 
 #undef ORX_ROLLOUT
   return launch_status("orx_rollout");
 }
+
+#ifdef ORX_STAMPS
+int orx_diag_stamps(uint64_t* host, int64_t n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), (size_t)n * 8, 0, hipMemcpyDeviceToHost)
+             == hipSuccess ? 0 : -1;
+}
+#endif
 
 int orx_dungeon_spawn(const orx_cfg_t* cfg, const orx_state_t* st, const uint32_t* game_ids,
                       const int32_t* episodes, const int32_t* depths, const int32_t* gens,

@@ -16,7 +16,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def child(arg, large):
+def child(arg, large, ticks=50):
     lib, *envs = arg.split("@")
     with_obs = True
     abi = None
@@ -38,34 +38,38 @@ def child(arg, large):
     from optimax_rogue_amd.enums import OBS_FIELDS
     dev = torch.device("cuda", 0)
     out = {"lib": arg}
-    shapes = [(65536, 50, 40)] + ([(1 << 21, 20, 6)] if large else [])
-    for B, T, reps in shapes:
-        e = BatchedEngine(EnvConfig.c3(), B, seed=1, device=dev)
+    shapes = [(65536, ticks, 40, "c3", 1)] + ([(1 << 21, 20, 6, "c3", 1)] if large else [])
+    if os.environ.get("AB_C5"):   # C5: 128x128 StaircaseBot at 16,384 and 131,072 games
+        shapes += [(16384, 128, 20, "c5", 2), (131072, 128, 10, "c5", 2)]
+    for B, T, reps, cname, pol in shapes:
+        e = BatchedEngine(getattr(EnvConfig, cname)(), B, seed=1, device=dev)
         obs = torch.empty((T, len(OBS_FIELDS), B), dtype=torch.int32, device=dev) \
             if with_obs else None
         act = torch.empty((T, B, 2), dtype=torch.int8, device=dev) if with_obs else None
         for _ in range(3):
-            e.rollout(T, 1, 1, obs=obs, act=act)
+            e.rollout(T, pol, pol, obs=obs, act=act)
         torch.cuda.synchronize()
         s, f = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
         for _ in range(reps):
-            e.rollout(T, 1, 1, obs=obs, act=act)
+            e.rollout(T, pol, pol, obs=obs, act=act)
         f.record()
         torch.cuda.synchronize()
         us = s.elapsed_time(f) * 1e3 / reps
-        out[f"B{B}"] = {"us_per_launch": round(us, 2), "env_steps_per_s": B * T / us * 1e6}
+        out[f"{cname}_B{B}"] = {"us_per_launch": round(us, 2), "env_steps_per_s": B * T / us * 1e6}
     print(json.dumps(out), flush=True)
 
 
 def main():
+    ticks = [int(a.split("=")[1]) for a in sys.argv if a.startswith("--ticks=")] or [50]
     if sys.argv[1] == "--child":
-        child(sys.argv[2], "--large" in sys.argv)
+        child(sys.argv[2], "--large" in sys.argv, ticks[0])
         return
     large = "--large" in sys.argv
     for lib in [a for a in sys.argv[1:] if not a.startswith("--")]:
         for _ in range(2):
-            r = subprocess.run([sys.executable, __file__, "--child", lib] + (["--large"] if large else []),
+            r = subprocess.run([sys.executable, __file__, "--child", lib, f"--ticks={ticks[0]}"]
+                               + (["--large"] if large else []),
                                timeout=300)
             if r.returncode:
                 sys.exit(r.returncode)

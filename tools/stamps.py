@@ -1,0 +1,68 @@
+"""In-kernel timeline of one rollout launch (diagnostics; needs a build with
+-DORX_STAMPS): lane 0 of each wave records s_memtime at kernel entry (0),
+after the state loads landed (1), at tick 64 (2), after the tick loop (3) and
+after the epilogue's stores drained (4).
+
+    python tools/stamps.py tools/ab_libs/stamps.so [B] [ticks]
+"""
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    lib = os.path.abspath(sys.argv[1])
+    B = int(sys.argv[2]) if len(sys.argv) > 2 else 65536
+    T = int(sys.argv[3]) if len(sys.argv) > 3 else 128
+    import torch
+    from optimax_rogue_amd import _lib, EnvConfig
+    _lib.LIB_PATH = lib
+    from optimax_rogue_amd.engine import BatchedEngine
+    dev = torch.device("cuda", 0)
+    e = BatchedEngine(EnvConfig.c3(), B, seed=1, device=dev)
+    obs = torch.empty((T, 14, B), dtype=torch.int32, device=dev)
+    act = torch.empty((T, B, 2), dtype=torch.int8, device=dev)
+    for _ in range(4):
+        e.rollout(T, 1, 1, obs=obs, act=act)
+    torch.cuda.synchronize()
+    s, f = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    e.rollout(T, 1, 1, obs=obs, act=act)
+    f.record()
+    torch.cuda.synchronize()
+    W = B // 64
+    buf = np.zeros(W * 8, dtype=np.uint64)
+    dl = ctypes.CDLL(lib)
+    dl.orx_diag_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+    assert dl.orx_diag_stamps(buf.ctypes.data, W * 8) == 0
+    st = buf.reshape(W, 8)[:, :5].astype(np.int64)
+    t0 = st[:, 0].min()
+    st = st - t0
+    # s_memtime counts the shader clock; report cycles and the event time
+    out = {"B": B, "ticks": T, "event_us": round(s.elapsed_time(f) * 1e3, 2)}
+    names = ["entry", "loaded", "tick64", "loop_end", "drained"]
+    for j, n in enumerate(names):
+        v = st[:, j]
+        out[n] = {"min": int(v.min()), "p50": int(np.median(v)), "max": int(v.max())}
+    d = np.diff(st, axis=1)
+    for j, n in enumerate(["prologue", "ticks0_64", "ticks64_T", "epilogue"]):
+        out["d_" + n] = {"min": int(d[:, j].min()), "p50": int(np.median(d[:, j])),
+                         "max": int(d[:, j].max())}
+    tot = d[:, 1] + d[:, 2]
+    xcd = (np.arange(W) // 4) % 8          # 4 waves per 256-thread block, blocks round-robin
+    out["loop_by_xcd_p50"] = [int(np.median(tot[xcd == x])) for x in range(8)]
+    out["loop_by_xcd_max"] = [int(tot[xcd == x].max()) for x in range(8)]
+    out["loop_pct"] = {q: int(np.percentile(tot, q)) for q in (1, 10, 50, 90, 99, 100)}
+    simd = np.arange(W) % 4
+    out["loop_by_wave_in_block_p50"] = [int(np.median(tot[simd == x])) for x in range(4)]
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
