@@ -68,21 +68,25 @@ constexpr int32_t kStartTick = 1;     // GameState.tick of a fresh game (worldge
 constexpr uint32_t kDeadSlot = 0xFFFFu;
 
 // Diagnostic builds only (-DORX_DIAG=bits; results are wrong): rollout_kernel
-// 1 no policy RNG, 2 no initiative RNG, 4 no move logic, 8 no reset, 16 no
-// trajectory.  Used by tools/ab_rollout.py to attribute time.
+// 16 writes no trajectory.  Used by tools/ab_rollout.py to attribute time.
 #ifndef ORX_DIAG
 #define ORX_DIAG 0
 #endif
 // -DORX_STAMPS (diagnostic builds): rollout_kernel lane 0 of each wave
 // records s_memtime at 8 points into g_stamps; orx_diag_stamps copies them out.
 #ifdef ORX_STAMPS
-__device__ uint64_t g_stamps[65536 * 8];
+__device__ uint64_t g_stamps[65536 * 16];
 #define ORX_STAMP(j)                                                               \
   if ((threadIdx.x & 63) == 0)                                                     \
-    g_stamps[(size_t)((blockIdx.x * blockDim.x + threadIdx.x) >> 6) * 8 + (j)] =   \
+    g_stamps[(size_t)((blockIdx.x * blockDim.x + threadIdx.x) >> 6) * 16 + (j)] =   \
         __builtin_amdgcn_s_memtime()
+// per-wave counts of rare-block entries (stamp slots 5..7): the block's first
+// active lane counts the entry; the lanes' counts are summed at the end
+#define ORX_COUNT(var)                                                                   \
+  var += (__lane_id() == (uint32_t)__builtin_ctzll(__builtin_amdgcn_read_exec())) ? 1u : 0u
 #else
 #define ORX_STAMP(j) ((void)0)
+#define ORX_COUNT(var) ((void)0)
 #endif
 #ifndef ORX_ROLLOUT_BLOCK
 #define ORX_ROLLOUT_BLOCK 256
@@ -200,6 +204,9 @@ struct Cfg {  // device copy of orx_cfg_t plus derived constants (all wave-unifo
 
 struct Deltas {  // counter / return increments, flushed once per launch
   int32_t combat, descend, dungeon, npc_death, ret, eps;
+#ifdef ORX_STAMPS
+  uint32_t n_rare = 0, n_ordered = 0, n_hits = 0, n_desc = 0, n_meet = 0;  // rare-block entries
+#endif
 };
 
 // Update-event sink (orx_step_events): records {type, iden, a, b} in the
@@ -310,6 +317,32 @@ struct Npcs {
     }
   }
 };
+
+// Both players' NPC occupancy tests in one pass over the slot registers
+// (the rollout's common path): with K = k1 | k2 << 16 and its half-swap Ks,
+// the packed 16-bit minimum over (slots ^ K) has a zero low half iff some
+// low slot holds k1 and a zero high half iff some high slot holds k2; over
+// (slots ^ Ks) the same for the other two pairings.
+template <int NCAP>
+__device__ __forceinline__ void npc_any2(const Npcs<NCAP>& npc, uint32_t k1, uint32_t k2,
+                                         bool& h1, bool& h2) {
+  if constexpr (NCAP == 0) {
+    h1 = h2 = false;
+  } else {
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    const uint32_t K = k1 | (k2 << 16), Ks = k2 | (k1 << 16);
+    u16x2 mx = __builtin_bit_cast(u16x2, npc.rd(0) ^ K);
+    u16x2 my = __builtin_bit_cast(u16x2, npc.rd(0) ^ Ks);
+#pragma unroll
+    for (int r = 1; r < Npcs<NCAP>::kRegs; ++r) {
+      mx = __builtin_elementwise_min(mx, __builtin_bit_cast(u16x2, npc.rd(r) ^ K));
+      my = __builtin_elementwise_min(my, __builtin_bit_cast(u16x2, npc.rd(r) ^ Ks));
+    }
+    const u16x2 z = __builtin_elementwise_min(mx, my.yx);
+    h1 = z.x == 0;
+    h2 = z.y == 0;
+  }
+}
 
 __device__ __forceinline__ uint32_t pack_xy(int32_t x, int32_t y) {
   return (uint32_t)(x & 0xFF) | ((uint32_t)(y & 0xFF) << 8);
@@ -1008,101 +1041,6 @@ __device__ __forceinline__ void tick_game(const Cfg& c, Key key, uint32_t game, 
                             dl, ev, sep_start);
 }
 
-// The rollout's tick: Updater.update (updater.py:76-162) with a straight
-// common path.  When neither player can meet the other this tick -- other
-// depth, or neither target is the other's cell nor the other's target --
-// the move order drawn by the initiative shuffle (:114) is unobservable: each
-// handle_move (:180-243) resolves against the other's unchanged cell, and NPCs
-// never move and are swept only after both moves (:136-145), so a hit does not
-// depend on the order either.  Such ticks (all but a few per thousand) skip the
-// shuffle decode and the ordered pair of moves.  The ordered path (tick_game)
-// takes the rest: a possible meeting, a step onto a staircase (descend draws
-// the SPAWN stream in move order), extension flags, and a tick whose shuffle
-// bits all reject (its stream fallback can stop the game).  Player health only
-// changes on the ordered path, so the common path's status is the max_ticks
-// test alone.  Invariants used: two players on one depth never share a cell,
-// and no player stands on its depth's staircase or on an NPC (spawns and moves
-// exclude them).  Counters: the ordered path counts the game's end itself.
-template <int NCAP, bool GRID, class M>
-__device__ __forceinline__ void tick_rollout(const Cfg& c, Key key, uint32_t game, uint32_t ep,
-                                             uint32_t pk_shf, Player& p1, Player& p2,
-                                             Npcs<NCAP>& npc, M& m, int32_t& tick,
-                                             int32_t& status, Deltas& dl, int32_t& sep) {
-  // effective targets: the player's own cell when staying or blocked
-  calc_pos(p1.x, p1.y, p1.move, p1.tx, p1.ty);
-  calc_pos(p2.x, p2.y, p2.move, p2.tx, p2.ty);
-  const bool b1 = blocked<GRID>(c, p1.lay, p1.tx, p1.ty);
-  const bool b2 = blocked<GRID>(c, p2.lay, p2.tx, p2.ty);
-  const int32_t t1x = b1 ? p1.x : p1.tx, t1y = b1 ? p1.y : p1.ty;
-  const int32_t t2x = b2 ? p2.x : p2.tx, t2y = b2 ? p2.y : p2.ty;
-  // meet: same depth and (target 1 == cell 2 or target 2 == cell 1 or
-  // target 1 == target 2), as one zero test over xor differences
-  const uint32_t e12 = (uint32_t)(t1x ^ p2.x) | (uint32_t)(t1y ^ p2.y);
-  const uint32_t e21 = (uint32_t)(t2x ^ p1.x) | (uint32_t)(t2y ^ p1.y);
-  const uint32_t e11 = (uint32_t)(t1x ^ t2x) | (uint32_t)(t1y ^ t2y);
-  const bool meet = ((uint32_t)(p1.d ^ p2.d) | min(e12, min(e21, e11))) == 0u;
-  const uint32_t k1 = pack_xy(t1x, t1y), k2 = pack_xy(t2x, t2y);  // NPC keys (W, H <= 256)
-  const bool hit1 = NCAP > 0 && ((p1.d == c.d1) & npc.any(k1));
-  const bool hit2 = NCAP > 0 && ((p2.d == c.d1) & npc.any(k2));
-  const bool st1 = stair_tile<GRID>(c, p1, t1x, t1y), st2 = stair_tile<GRID>(c, p2, t2x, t2y);
-  const bool shf_reject = (~(pk_shf >> 1) & 0x55555555u) == 0u;
-  // a descend into the other player's depth depends on the move order (the
-  // spawn cell's occupancy test, and the other's later move into the spawn cell)
-  const bool desc_meet = (st1 & (p2.d == p1.d + 1)) | (st2 & (p1.d == p2.d + 1));
-  const bool ordered = meet | (st1 & st2) | desc_meet | shf_reject | (c.ext != 0);
-  // The ordered lanes run first, in an if without else placed out of line;
-  // the common path below is gated by selects (an if/else would put a taken
-  // branch around one of the two bodies on every tick).  `fast` is laundered
-  // so the compiler cannot rebuild the if/else from the two conditions.
-  uint32_t fast = ordered ? 0u : 1u;
-  asm volatile("" : "+v"(fast));
-  if (ORX_UNLIKELY(ordered)) {
-    bool err = false;
-    const bool p1_first = first_from_packed(pk_shf, key, game, ep, tick, err);
-    Events<false> ev{nullptr, 0};
-    tick_game<NCAP, false, GRID>(c, key, game, ep, p1_first, p1, p2, npc, m, tick, status, err,
-                                 dl, ev, sep);
-  }
-  const bool f = fast != 0u;
-  const bool s1 = f & !hit1 & !st1, s2 = f & !hit2 & !st2;
-  p1.x = s1 ? t1x : p1.x;
-  p1.y = s1 ? t1y : p1.y;
-  p2.x = s2 ? t2x : p2.x;
-  p2.y = s2 ? t2y : p2.y;
-  if (NCAP > 0 && ORX_UNLIKELY(f & (hit1 | hit2))) {
-    Events<false> ev{nullptr, 0};
-    dl.combat += (hit1 ? 1 : 0) + (hit2 ? 1 : 0);
-    npc_hits(c, npc, m, hit1 ? npc.find(k1) : -1, hit2 ? npc.find(k2) : -1, dl, ev);
-  }
-  // One player steps onto its staircase (updater.py:205-208) and descends
-  // (handle_descend, :259-296) to a depth the other player is not on: then
-  // nothing in it depends on the move order (dungeon presence reads only the
-  // other's depths, the spawn cell's occupancy test never matches the other,
-  // NPCs are swept after both moves, and the SPAWN stream has one consumer).
-  const int32_t t0 = tick;
-  const int32_t ft = tick + 1;
-  const bool end = c.max_ticks && ft >= c.max_ticks;
-  tick = f ? ft : tick;
-  status = f ? (end ? ORX_TIE : ORX_IN_PROGRESS) : status;
-  dl.eps += (f & end) ? 1 : 0;
-  if (ORX_UNLIKELY(f & (st1 | st2))) {
-    PhiloxSrc src{key, game, ep};
-    auto spawn = src.spawn(t0);
-    Events<false> ev{nullptr, 0};
-    bool err = false;
-    Player S = pick(st1, p1, p2);
-    const Player O = pick(st1, p2, p1);
-    descend<NCAP, false, GRID>(c, key, src, S, O, st1 ? c.d2 : c.d1, npc, spawn, dl, err,
-                               st1 ? 1 : 2, ev);
-    p1 = pick(st1, S, p1);
-    p2 = pick(st1, p2, S);
-    if (err) {  // an exhausted spawn stream stops the game (never observed)
-      dl.eps -= end ? 1 : 0;
-      status = ORX_STATUS_RNG_EXHAUSTED;
-    }
-  }
-}
-
 // ---------------------------------------------------------------------------
 // SoA load / store helpers (32-bit lane index: B < 2^31)
 // ---------------------------------------------------------------------------
@@ -1335,6 +1273,223 @@ __global__ void __launch_bounds__(256) policy_kernel(orx_state_t st, int32_t pol
   out[i] = pack_actions(a1, a2);
 }
 
+// updater.py:150-162 over the max_ticks result the rollout's common path set,
+// after a combat or separation damage there (the ordered path has its own
+// chain; a double death is a Tie: ORX_EXT_RANDOM_DOUBLE_DEATH is ordered).
+__device__ __forceinline__ void deaths_over(const Player& p1, const Player& p2, bool end,
+                                            int32_t& status, Deltas& dl) {
+  const bool d1 = p1.hp <= 0, d2 = p2.hp <= 0;
+  if ((d1 | d2) && status != ORX_STATUS_RNG_EXHAUSTED) {
+    const int32_t s = d1 ? (d2 ? ORX_TIE : ORX_PLAYER2_WIN) : ORX_PLAYER1_WIN;
+    dl.eps += end ? 0 : 1;
+    dl.ret += (s == ORX_PLAYER1_WIN ? 1 : 0) - (s == ORX_PLAYER2_WIN ? 1 : 0);
+    status = s;
+  }
+}
+
+// One rollout tick of one game (the hot loop of server/main.py:110-113,
+// fused): the bots' moves (randombot.py:20-21, staircasebot.py:9-21), then
+// Updater.update (updater.py:76-162) -- or, for a finished game, the next
+// episode's setup (autoreset).
+//
+// Common path.  The initiative shuffle (updater.py:114) orders the two
+// handle_move calls (:133-134, :180-243), but the order is observable only
+// when the moves can interact: both players on one depth with a target equal
+// to the other's cell or to the other's target (a "meet").  Otherwise each
+// move resolves against the other's unchanged cell; NPCs never move and are
+// swept only after both moves (:136-145), so an NPC hit does not depend on
+// the order either; and a descend into a depth the other player is not on
+// reads nothing the other's move changes.  So the common path resolves both
+// moves independently from their effective targets (the own cell when
+// staying or blocked), and its status is the max_ticks test alone: health
+// changes only in combat.  Invariants used: two players on one depth never
+// share a cell; no player stands on its depth's staircase or on an NPC.
+//
+// Every rare case sits in ONE out-of-line block -- a lone wave per SIMD pays
+// ~40 cycles per branch instruction, taken or not, so a
+// common tick carries that block's branch and the loop's:
+//  * a finished game: the next episode's setup_game (autoreset);
+//  * the ordered tick, tick_game, the reference's sequence literally: a meet
+//    involving a staircase, both players descending (SPAWN stream order), a
+//    descend into the other's depth (the spawn cell's occupancy test, and the
+//    other's later move into it), extension flags other than separation
+//    damage, shuffle bits that all reject (their stream fallback can stop the
+//    game), bot draws beyond the tick block's two segments;
+//  * on the common path's tick: NPC hits (npc_hits), one player's descend
+//    (handle_descend, :259-296), and a meet without staircases -- the two
+//    moves in the drawn order, the first against the second's cell, the
+//    second against the first's new cell; an occupied target is a combat
+//    (every CombatFlag deals damage - armor: no Modifier exists) and the
+//    attacker stays; deaths override the status.
+template <int NCAP, bool GRID, class M>
+__device__ __forceinline__ void rollout_tick(const Cfg& c, const orx_state_t& st, uint32_t B,
+                                             uint32_t i, Key key, uint32_t game, uint32_t& ep,
+                                             int32_t pol1, int32_t pol2, Player& p1,
+                                             Player& p2, Npcs<NCAP>& npc, M& hp,
+                                             int32_t& tick, int32_t& status, Deltas& dl,
+                                             int32_t& sep, bool& restarted, int32_t& a1,
+                                             int32_t& a2) {
+  // one tick block: the bots' bits and the initiative bits (§4)
+  const W4 tb = tick_block(key, game, ep, tick);
+  const uint32_t pk_shf = tb.a;
+  // RandomBot draws: the first accepted 3-bit fields of bits 0-29 of word b,
+  // then of word c (moves_from_block, both segments at once, no branch)
+  const int need = (pol1 == ORX_POLICY_RANDOM ? 1 : 0) + (pol2 == ORX_POLICY_RANDOM ? 1 : 0);
+  const uint64_t w = (uint64_t)(tb.b & 0x3FFFFFFFu) | ((uint64_t)(tb.c & 0x3FFFFFFFu) << 30);
+  const uint64_t acc = (uint64_t)accepted3(tb.b) | ((uint64_t)accepted3(tb.c) << 30);
+  const uint64_t acc2 = acc & (acc - 1u);
+  const int32_t r0 = (int32_t)((w >> __builtin_ctzll(acc | (1ull << 63))) & 7u) + 1;
+  const int32_t r1 = (int32_t)((w >> __builtin_ctzll(acc2 | (1ull << 63))) & 7u) + 1;
+  const bool need_fb = need > (acc == 0 ? 0 : acc2 == 0 ? 1 : 2);
+  assign_moves(pol1, pol2, r0, r1, p1, p2, a1, a2);
+  p1.move = a1;
+  p2.move = a2;
+  const bool in_progress = status == ORX_IN_PROGRESS;
+
+  // effective targets: the player's own cell when staying or blocked
+  calc_pos(p1.x, p1.y, p1.move, p1.tx, p1.ty);
+  calc_pos(p2.x, p2.y, p2.move, p2.tx, p2.ty);
+  const bool b1 = blocked<GRID>(c, p1.lay, p1.tx, p1.ty);
+  const bool b2 = blocked<GRID>(c, p2.lay, p2.tx, p2.ty);
+  const int32_t t1x = b1 ? p1.x : p1.tx, t1y = b1 ? p1.y : p1.ty;
+  const int32_t t2x = b2 ? p2.x : p2.tx, t2y = b2 ? p2.y : p2.ty;
+  // meet: same depth and (target 1 == cell 2 or target 2 == cell 1 or
+  // target 1 == target 2), as one zero test over xor differences
+  const uint32_t e12 = (uint32_t)(t1x ^ p2.x) | (uint32_t)(t1y ^ p2.y);
+  const uint32_t e21 = (uint32_t)(t2x ^ p1.x) | (uint32_t)(t2y ^ p1.y);
+  const uint32_t e11 = (uint32_t)(t1x ^ t2x) | (uint32_t)(t1y ^ t2y);
+  const bool meet = ((uint32_t)(p1.d ^ p2.d) | min(e12, min(e21, e11))) == 0u;
+  // NPC keys x | y << 8 (W, H <= 256 with NPCs; effective targets are in the grid)
+  const uint32_t k1 = (uint32_t)t1x | ((uint32_t)t1y << 8);
+  const uint32_t k2 = (uint32_t)t2x | ((uint32_t)t2y << 8);
+  bool n1 = false, n2 = false;
+  npc_any2(npc, k1, k2, n1, n2);
+  const bool hit1 = NCAP > 0 && ((p1.d == c.d1) & n1);
+  const bool hit2 = NCAP > 0 && ((p2.d == c.d1) & n2);
+  const bool st1 = stair_tile<GRID>(c, p1, t1x, t1y), st2 = stair_tile<GRID>(c, p2, t2x, t2y);
+  const bool shf_reject = (~(pk_shf >> 1) & 0x55555555u) == 0u;
+  const bool desc_meet = (st1 & (p2.d == p1.d + 1)) | (st2 & (p1.d == p2.d + 1));
+  const bool full = need_fb | (meet & (st1 | st2)) | (st1 & st2) | desc_meet | shf_reject |
+                    ((c.ext & ~ORX_EXT_SEPARATION_DAMAGE) != 0);
+  const bool lean = meet & !full;
+  // base: the in-progress games whose tick the common path takes (a hit, a
+  // descend or a meet adjusted below); f: those whose moves resolve freely.
+  // Laundered, so the compiler cannot rebuild an if/else around the rare block.
+  uint32_t bv = (in_progress & !full) ? 1u : 0u, fv = (in_progress & !full & !lean) ? 1u : 0u;
+  asm volatile("" : "+v"(bv), "+v"(fv));
+  const bool base = bv != 0u, f = fv != 0u;
+  const bool s1 = f & !hit1 & !st1, s2 = f & !hit2 & !st2;
+  p1.x = s1 ? t1x : p1.x;
+  p1.y = s1 ? t1y : p1.y;
+  p2.x = s2 ? t2x : p2.x;
+  p2.y = s2 ? t2y : p2.y;
+  const int32_t t0 = tick, ft = tick + 1;
+  const bool end = c.max_ticks && ft >= c.max_ticks;
+  tick = base ? ft : tick;
+  status = base ? (end ? ORX_TIE : ORX_IN_PROGRESS) : status;
+  dl.eps += (base & end) ? 1 : 0;
+
+  if (ORX_UNLIKELY(!base | hit1 | hit2 | st1 | st2 | lean)) {
+#ifdef ORX_STAMPS
+    ORX_COUNT(dl.n_rare);
+#endif
+    if (!in_progress) {
+      if (need_fb)  // the recorded actions: draws beyond the tick block
+        policy_pair(key, game, ep, t0, pol1, pol2, tb, p1, p2, a1, a2);
+      if (c.autoreset) {  // the next episode (worldgen.py:77-87, 124-135)
+        ep += 1;
+        setup_game<NCAP, GRID>(c, key, game, ep, p1, p2, npc, tick, status);
+        if constexpr (NCAP > 0) {
+          store_new_npcs(st, c, B, i, npc, false);  // health: from hp at the end
+          hp.fill(c.npc_hp);
+        }
+        restarted = true;
+        sep = -1;
+      }
+    } else if (!base) {  // the ordered tick
+#ifdef ORX_STAMPS
+      ORX_COUNT(dl.n_ordered);
+#endif
+      if (need_fb) {  // draws beyond the tick block: word c, then the POLICY stream
+        policy_pair(key, game, ep, t0, pol1, pol2, tb, p1, p2, a1, a2);
+        p1.move = a1;
+        p2.move = a2;
+      }
+      bool err = false;
+      const bool p1_first = first_from_packed(pk_shf, key, game, ep, t0, err);
+      Events<false> ev{nullptr, 0};
+      tick_game<NCAP, false, GRID>(c, key, game, ep, p1_first, p1, p2, npc, hp, tick, status,
+                                   err, dl, ev, sep);
+    } else {
+      if (NCAP > 0 && (hit1 | hit2)) {  // NPCs are swept after both moves
+#ifdef ORX_STAMPS
+        ORX_COUNT(dl.n_hits);
+#endif
+        Events<false> ev{nullptr, 0};
+        dl.combat += (hit1 ? 1 : 0) + (hit2 ? 1 : 0);
+        npc_hits(c, npc, hp, hit1 ? npc.find(k1) : -1, hit2 ? npc.find(k2) : -1, dl, ev);
+      }
+      if (f & (st1 | st2)) {  // one player descends, not into the other's depth
+#ifdef ORX_STAMPS
+        ORX_COUNT(dl.n_desc);
+#endif
+        PhiloxSrc src{key, game, ep};
+        auto spawn = src.spawn(t0);
+        Events<false> ev{nullptr, 0};
+        bool err = false;
+        Player S = pick(st1, p1, p2);
+        const Player O = pick(st1, p2, p1);
+        descend<NCAP, false, GRID>(c, key, src, S, O, st1 ? c.d2 : c.d1, npc, spawn, dl, err,
+                                   st1 ? 1 : 2, ev);
+        p1 = pick(st1, S, p1);
+        p2 = pick(st1, p2, S);
+        if (err) {  // an exhausted spawn stream stops the game (never observed)
+          dl.eps -= end ? 1 : 0;
+          status = ORX_STATUS_RNG_EXHAUSTED;
+        }
+      }
+      if (lean) {  // a meet: the two moves in the drawn order
+#ifdef ORX_STAMPS
+        ORX_COUNT(dl.n_meet);
+#endif
+        const uint32_t sa = ~(pk_shf >> 1) & 0x55555555u;  // nonzero: all-reject is ordered
+        const bool p1_first = ((pk_shf >> __builtin_ctz(sa)) & 1u) != 0;
+        const int32_t ax = p1_first ? t1x : t2x, ay = p1_first ? t1y : t2y;
+        const int32_t bx = p1_first ? t2x : t1x, by = p1_first ? t2y : t1y;
+        const int32_t fx0 = p1_first ? p1.x : p2.x, fy0 = p1_first ? p1.y : p2.y;
+        const int32_t sx0 = p1_first ? p2.x : p1.x, sy0 = p1_first ? p2.y : p1.y;
+        const bool hf = p1_first ? hit1 : hit2, hs = p1_first ? hit2 : hit1;
+        const bool occf = (ax == sx0) & (ay == sy0);
+        const int32_t fx = (occf | hf) ? fx0 : ax, fy = (occf | hf) ? fy0 : ay;
+        const bool occs = (bx == fx) & (by == fy);
+        const int32_t sx = (occs | hs) ? sx0 : bx, sy = (occs | hs) ? sy0 : by;
+        const int32_t dmg = c.player_dmg_net > 0 ? c.player_dmg_net : 0;
+        p1.x = p1_first ? fx : sx;
+        p1.y = p1_first ? fy : sy;
+        p2.x = p1_first ? sx : fx;
+        p2.y = p1_first ? sy : fy;
+        p1.hp -= (p1_first ? occs : occf) ? dmg : 0;
+        p2.hp -= (p1_first ? occf : occs) ? dmg : 0;
+        dl.combat += (occf ? 1 : 0) + (occs ? 1 : 0);
+        deaths_over(p1, p2, end, status, dl);
+      }
+    }
+  }
+  if (c.ext & ORX_EXT_SEPARATION_DAMAGE) {  // build extension (readme.md:46-47), C5's ladder
+    if (base) {
+      if (p1.d != p2.d) {
+        if (sep < 0) sep = t0;
+        const int32_t k = t0 - sep + 1;
+        const int32_t dmg = (k + c.sep_period - 1) / c.sep_period;
+        if (p1.d < p2.d) p1.hp -= dmg; else p2.hp -= dmg;
+        deaths_over(p1, p2, end, status, dl);
+      } else {
+        sep = -1;
+      }
+    }
+  }
+}
+
 // Fused rollout: n_ticks x (policy, step); state and NPC positions stay in
 // registers; tick t's observation row is streamed out to obs/act.  At the
 // headline batch (65,536 games) this is ONE wave per SIMD, so the tick loop is
@@ -1440,43 +1595,16 @@ __global__ void __launch_bounds__(kRolloutBlock) rollout_kernel(orx_cfg_t hc, or
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
   ORX_STAMP(1);
-  for (int32_t t = 0; t < n_ticks; ++t) {
+  int32_t t = 0;
+  do {  // n_ticks >= 1: orx_rollout returns before launching 0 ticks
 #ifdef ORX_STAMPS
     if (t == 64) { ORX_STAMP(2); }
 #endif
-    // one tick block: the bots' bits and the initiative bits (drawn although
-    // only in-progress games use the latter)
-    W4 tb = tick_block(key, game, ep, tick);
-    if (ORX_DIAG & 1) tb.b = tb.c = ((uint32_t)tick * 0x9E3779B9u) ^ (game * 0x85EBCA6Bu);
-    const uint32_t pk_shf = (ORX_DIAG & 2) ? 0x55555555u : tb.a;
     int32_t a1 = ORX_MOVE_STAY, a2 = ORX_MOVE_STAY;
-    policy_pair(key, game, ep, tick, pol1, pol2, tb, p1, p2, a1, a2);
-    if (ORX_LIKELY(status == ORX_IN_PROGRESS)) {
-      p1.move = a1; p2.move = a2;
-      if (ORX_DIAG & 4) {
-        tick += 1;
-        p1.x ^= (int32_t)(pk_shf & 1u);
-        status = (c.max_ticks && tick >= c.max_ticks) ? ORX_TIE : ORX_IN_PROGRESS;
-      } else {
-        tick_rollout<NCAP, GRID>(c, key, game, ep, pk_shf, p1, p2, npc, hp, tick, status, dl, sep);
-      }
-    } else if (c.autoreset) {
-      ep += 1;
-      if (ORX_DIAG & 8) {
-        tick = kStartTick;
-        status = ORX_IN_PROGRESS;
-      } else {
-        setup_game<NCAP, GRID>(c, key, game, ep, p1, p2, npc, tick, status);
-        if constexpr (NCAP > 0) {
-          store_new_npcs(st, c, B, i, npc, false);  // health: from hp at the end
-          hp.fill(c.npc_hp);
-        }
-      }
-      restarted = true;
-      sep = -1;
-    }
+    rollout_tick<NCAP, GRID>(c, st, B, i, key, game, ep, pol1, pol2, p1, p2, npc, hp, tick,
+                             status, dl, sep, restarted, a1, a2);
     if (!(ORX_DIAG & 16)) traj.write(t, p1, p2, tick, status, a1, a2);
-  }
+  } while (++t < n_ticks);
   ORX_STAMP(3);
   store_players<GRID>(st, B, i, p1, p2, restarted || dl.descend != 0);
   st.tick[i] = tick;
@@ -1492,6 +1620,17 @@ __global__ void __launch_bounds__(kRolloutBlock) rollout_kernel(orx_cfg_t hc, or
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
   ORX_STAMP(4);
+#ifdef ORX_STAMPS
+  uint32_t r[5] = {dl.n_rare, dl.n_ordered, dl.n_hits, dl.n_desc, dl.n_meet};
+#pragma unroll
+  for (int j = 0; j < 5; ++j)
+    for (int o = 32; o > 0; o >>= 1) r[j] += __shfl_xor(r[j], o);
+  if ((threadIdx.x & 63) == 0) {
+    const size_t w = (size_t)((blockIdx.x * blockDim.x + threadIdx.x) >> 6) * 16;
+#pragma unroll
+    for (int j = 0; j < 5; ++j) g_stamps[w + 5 + j] = r[j];
+  }
+#endif
 }
 
 // Staircases of arbitrary (game, episode, depth, generation) dungeons, for

@@ -37,11 +37,11 @@ def main():
     f.record()
     torch.cuda.synchronize()
     W = B // 64
-    buf = np.zeros(W * 8, dtype=np.uint64)
+    buf = np.zeros(W * 16, dtype=np.uint64)
     dl = ctypes.CDLL(lib)
     dl.orx_diag_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int64]
-    assert dl.orx_diag_stamps(buf.ctypes.data, W * 8) == 0
-    st = buf.reshape(W, 8)[:, :5].astype(np.int64)
+    assert dl.orx_diag_stamps(buf.ctypes.data, W * 16) == 0
+    st = buf.reshape(W, 16)[:, :5].astype(np.int64)
     t0 = st[:, 0].min()
     st = st - t0
     # s_memtime counts the shader clock; report cycles and the event time
@@ -59,6 +59,12 @@ def main():
     out["loop_by_xcd_p50"] = [int(np.median(tot[xcd == x])) for x in range(8)]
     out["loop_by_xcd_max"] = [int(tot[xcd == x].max()) for x in range(8)]
     out["loop_pct"] = {q: int(np.percentile(tot, q)) for q in (1, 10, 50, 90, 99, 100)}
+    rare = buf.reshape(W, 16)[:, 5:10].astype(np.int64)
+    for j, n in enumerate(["rare_block", "ordered", "npc_hits", "descend", "meet"]):
+        out["ticks_with_" + n] = {"mean": float(rare[:, j].mean()), "max": int(rare[:, j].max())}
+    slow = np.argsort(tot)[-10:]
+    out["slowest10_rare"] = rare[slow].tolist()
+    out["slowest10_loop"] = tot[slow].tolist()
     simd = np.arange(W) % 4
     out["loop_by_wave_in_block_p50"] = [int(np.median(tot[simd == x])) for x in range(4)]
     print(json.dumps(out, indent=1))
