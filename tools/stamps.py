@@ -25,15 +25,17 @@ def main():
     _lib.LIB_PATH = lib
     from optimax_rogue_amd.engine import BatchedEngine
     dev = torch.device("cuda", 0)
-    e = BatchedEngine(EnvConfig.c3(), B, seed=1, device=dev)
+    cname = os.environ.get("STAMPS_CFG", "c3")   # c5: StaircaseBot on C5's dungeon
+    pol = 2 if cname == "c5" else 1
+    e = BatchedEngine(getattr(EnvConfig, cname)(), B, seed=1, device=dev)
     obs = torch.empty((T, 14, B), dtype=torch.int32, device=dev)
     act = torch.empty((T, B, 2), dtype=torch.int8, device=dev)
     for _ in range(4):
-        e.rollout(T, 1, 1, obs=obs, act=act)
+        e.rollout(T, pol, pol, obs=obs, act=act)
     torch.cuda.synchronize()
     s, f = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
-    e.rollout(T, 1, 1, obs=obs, act=act)
+    e.rollout(T, pol, pol, obs=obs, act=act)
     f.record()
     torch.cuda.synchronize()
     W = B // 64
