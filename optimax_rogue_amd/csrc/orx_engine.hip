@@ -1335,12 +1335,16 @@ __device__ __forceinline__ void rollout_tick(const Cfg& c, const orx_state_t& st
   // RandomBot draws: the first accepted 3-bit fields of bits 0-29 of word b,
   // then of word c (moves_from_block, both segments at once, no branch)
   const int need = (pol1 == ORX_POLICY_RANDOM ? 1 : 0) + (pol2 == ORX_POLICY_RANDOM ? 1 : 0);
-  const uint64_t w = (uint64_t)(tb.b & 0x3FFFFFFFu) | ((uint64_t)(tb.c & 0x3FFFFFFFu) << 30);
-  const uint64_t acc = (uint64_t)accepted3(tb.b) | ((uint64_t)accepted3(tb.c) << 30);
-  const uint64_t acc2 = acc & (acc - 1u);
-  const int32_t r0 = (int32_t)((w >> __builtin_ctzll(acc | (1ull << 63))) & 7u) + 1;
-  const int32_t r1 = (int32_t)((w >> __builtin_ctzll(acc2 | (1ull << 63))) & 7u) + 1;
-  const bool need_fb = need > (acc == 0 ? 0 : acc2 == 0 ? 1 : 2);
+  int32_t r0 = ORX_MOVE_STAY, r1 = ORX_MOVE_STAY;
+  bool need_fb = false;
+  if (need > 0) {  // uniform: skipped for StaircaseBot pairs (C5)
+    const uint64_t w = (uint64_t)(tb.b & 0x3FFFFFFFu) | ((uint64_t)(tb.c & 0x3FFFFFFFu) << 30);
+    const uint64_t acc = (uint64_t)accepted3(tb.b) | ((uint64_t)accepted3(tb.c) << 30);
+    const uint64_t acc2 = acc & (acc - 1u);
+    r0 = (int32_t)((w >> __builtin_ctzll(acc | (1ull << 63))) & 7u) + 1;
+    r1 = (int32_t)((w >> __builtin_ctzll(acc2 | (1ull << 63))) & 7u) + 1;
+    need_fb = need > (acc == 0 ? 0 : acc2 == 0 ? 1 : 2);
+  }
   assign_moves(pol1, pol2, r0, r1, p1, p2, a1, a2);
   p1.move = a1;
   p2.move = a2;
