@@ -1310,13 +1310,16 @@ __device__ __forceinline__ void deaths_over(const Player& p1, const Player& p2, 
 // common tick carries that block's branch and the loop's:
 //  * a finished game: the next episode's setup_game (autoreset);
 //  * the ordered tick, tick_game, the reference's sequence literally: a meet
-//    involving a staircase, both players descending (SPAWN stream order), a
-//    descend into the other's depth (the spawn cell's occupancy test, and the
-//    other's later move into it), extension flags other than separation
-//    damage, shuffle bits that all reject (their stream fallback can stop the
-//    game), bot draws beyond the tick block's two segments;
-//  * on the common path's tick: NPC hits (npc_hits), one player's descend
-//    (handle_descend, :259-296), and a meet without staircases -- the two
+//    involving a staircase, both players descending (SPAWN stream order),
+//    extension flags other than separation damage, shuffle bits that all
+//    reject (their stream fallback can stop the game), bot draws beyond the
+//    tick block's two segments;
+//  * on the common path's tick: one player's descend (handle_descend,
+//    :259-296) -- into the other's depth in the drawn order: descending
+//    first, the spawn cell is tested against the other's old cell and the
+//    other's move into it is a combat --; NPC hits (npc_hits), after the
+//    descend, whose spawn test sees every NPC alive; and a meet without
+//    staircases -- the two
 //    moves in the drawn order, the first against the second's cell, the
 //    second against the first's new cell; an occupied target is a combat
 //    (every CombatFlag deals damage - armor: no Modifier exists) and the
@@ -1373,7 +1376,7 @@ __device__ __forceinline__ void rollout_tick(const Cfg& c, const orx_state_t& st
   const bool st1 = stair_tile<GRID>(c, p1, t1x, t1y), st2 = stair_tile<GRID>(c, p2, t2x, t2y);
   const bool shf_reject = (~(pk_shf >> 1) & 0x55555555u) == 0u;
   const bool desc_meet = (st1 & (p2.d == p1.d + 1)) | (st2 & (p1.d == p2.d + 1));
-  const bool full = need_fb | (meet & (st1 | st2)) | (st1 & st2) | desc_meet | shf_reject |
+  const bool full = need_fb | (meet & (st1 | st2)) | (st1 & st2) | shf_reject |
                     ((c.ext & ~ORX_EXT_SEPARATION_DAMAGE) != 0);
   const bool lean = meet & !full;
   // base: the in-progress games whose tick the common path takes (a hit, a
@@ -1383,6 +1386,7 @@ __device__ __forceinline__ void rollout_tick(const Cfg& c, const orx_state_t& st
   asm volatile("" : "+v"(bv), "+v"(fv));
   const bool base = bv != 0u, f = fv != 0u;
   const bool s1 = f & !hit1 & !st1, s2 = f & !hit2 & !st2;
+  const int32_t x1o = p1.x, y1o = p1.y, x2o = p2.x, y2o = p2.y;  // for a descend-meet
   p1.x = s1 ? t1x : p1.x;
   p1.y = s1 ? t1y : p1.y;
   p2.x = s2 ? t2x : p2.x;
@@ -1425,15 +1429,7 @@ __device__ __forceinline__ void rollout_tick(const Cfg& c, const orx_state_t& st
       tick_game<NCAP, false, GRID>(c, key, game, ep, p1_first, p1, p2, npc, hp, tick, status,
                                    err, dl, ev, sep);
     } else {
-      if (NCAP > 0 && (hit1 | hit2)) {  // NPCs are swept after both moves
-#ifdef ORX_STAMPS
-        ORX_COUNT(dl.n_hits);
-#endif
-        Events<false> ev{nullptr, 0};
-        dl.combat += (hit1 ? 1 : 0) + (hit2 ? 1 : 0);
-        npc_hits(c, npc, hp, hit1 ? npc.find(k1) : -1, hit2 ? npc.find(k2) : -1, dl, ev);
-      }
-      if (f & (st1 | st2)) {  // one player descends, not into the other's depth
+      if (f & (st1 | st2)) {  // one player descends
 #ifdef ORX_STAMPS
         ORX_COUNT(dl.n_desc);
 #endif
@@ -1442,15 +1438,41 @@ __device__ __forceinline__ void rollout_tick(const Cfg& c, const orx_state_t& st
         Events<false> ev{nullptr, 0};
         bool err = false;
         Player S = pick(st1, p1, p2);
-        const Player O = pick(st1, p2, p1);
-        descend<NCAP, false, GRID>(c, key, src, S, O, st1 ? c.d2 : c.d1, npc, spawn, dl, err,
+        Player O = pick(st1, p2, p1);  // after its own move
+        // into the other's depth (desc_meet), the drawn order matters: moving
+        // first, the descender's spawn cell is tested against the other's
+        // cell before that player's move, which may then attack it
+        bool s_first = false;
+        if (desc_meet) {
+          const uint32_t sa = ~(pk_shf >> 1) & 0x55555555u;  // nonzero: all-reject is ordered
+          s_first = (((pk_shf >> __builtin_ctz(sa)) & 1u) != 0) == st1;
+        }
+        const int32_t ox0 = st1 ? x2o : x1o, oy0 = st1 ? y2o : y1o;
+        Player Ot = O;
+        Ot.x = s_first ? ox0 : O.x;
+        Ot.y = s_first ? oy0 : O.y;
+        descend<NCAP, false, GRID>(c, key, src, S, Ot, st1 ? c.d2 : c.d1, npc, spawn, dl, err,
                                    st1 ? 1 : 2, ev);
-        p1 = pick(st1, S, p1);
-        p2 = pick(st1, p2, S);
+        const bool clash = s_first & ((O.x != ox0) | (O.y != oy0)) & (O.x == S.x) & (O.y == S.y);
+        O.x = clash ? ox0 : O.x;
+        O.y = clash ? oy0 : O.y;
+        S.hp -= (clash && c.player_dmg_net > 0) ? c.player_dmg_net : 0;
+        dl.combat += clash ? 1 : 0;
+        p1 = pick(st1, S, O);
+        p2 = pick(st1, O, S);
         if (err) {  // an exhausted spawn stream stops the game (never observed)
           dl.eps -= end ? 1 : 0;
           status = ORX_STATUS_RNG_EXHAUSTED;
         }
+        if (clash) deaths_over(p1, p2, end, status, dl);
+      }
+      if (NCAP > 0 && (hit1 | hit2)) {  // NPCs are swept after both moves
+#ifdef ORX_STAMPS
+        ORX_COUNT(dl.n_hits);
+#endif
+        Events<false> ev{nullptr, 0};
+        dl.combat += (hit1 ? 1 : 0) + (hit2 ? 1 : 0);
+        npc_hits(c, npc, hp, hit1 ? npc.find(k1) : -1, hit2 ? npc.find(k2) : -1, dl, ev);
       }
       if (lean) {  // a meet: the two moves in the drawn order
 #ifdef ORX_STAMPS

@@ -126,6 +126,10 @@ ORACLE_CASES = {
     "bank_64_npc": (dict(width=64, height=64, n_npcs=8, max_ticks=300), (1, 1), 2048, 400, 15),
     "bank_stairs_unused": (dict(width=12, height=10, n_npcs=2, max_ticks=200, despawn=2), (2, 1),
                            2048, 400, 16),
+    # a StaircaseBot descending into a 5x4 depth a RandomBot walks: the
+    # rollout's descend-into-the-other's-depth path in both drawn orders
+    "desc_meet_5x4": (dict(width=5, height=4, start_mode=2, p1_depth=2, p2_depth=1,
+                           max_ticks=200), (1, 2), 2048, 200, 25),
     # build extensions (readme-only mechanics, parity unpinned: engine vs oracle)
     "ext_separation": (dict(width=9, height=9, start_mode=2, p1_depth=0, p2_depth=2, n_npcs=2,
                             max_ticks=300, flags=1, sep_period=4), (2, 1), 2048, 400, 17),
