@@ -6,20 +6,25 @@
 
 Workload (BASELINE.json configs[2], "C3"): 65,536 games per GPU on a 64x64
 grid with enemies (K = 8 NPCs per game), both players driven by RandomBot,
-Unreachable despawn, max_ticks 1000 with autoreset.  One "step" = one tick of
-every game in the batch; an env-step = one game advanced one tick.  Games
-shard across GPUs by global game id (weak scaling, no data-path collective);
-after the timed region the per-game episode returns are all-gathered over
-RCCL (the only collective).
+Unreachable despawn, max_ticks 1000 with autoreset.  An env-step = one game
+advanced one tick.  ONE BENCH STEP = one fused rollout launch of --chunk
+(default 128) ticks over every game: the trajectory horizon a learner
+consumes, the unit the hot path is called with.  `--steps K` times K such
+launches (K x 128 ticks of every game); `value` = games x ranks x ticks /
+time.  Games shard across GPUs by global game id (parallel.shard; weak
+scaling, no data-path collective); after the timed region the per-game
+episode returns are all-gathered over RCCL (the only collective).
 
-Timed path (headline): the fused rollout kernel, one launch per --chunk ticks;
-state stays in registers and EVERY tick's full observation (14 int32 fields:
-both players' x, y, depth, health, staircase, plus tick and status) and both
-actions are written to an HBM trajectory buffer -- nothing is skipped.
+Timed path: the fused rollout kernel; state stays in registers and EVERY
+tick's full observation (14 int32 fields: both players' x, y, depth, health,
+staircase, plus tick and status) and both actions are written to an HBM
+trajectory buffer -- nothing is skipped.  The launches are issued through a
+pre-bound launcher (one ctypes call each) with HIP events created beforehand,
+so the timed region is the kernels back to back.
 
 Extras (rank 0, 1 GPU): the unfused path (orx_policy + orx_step per tick,
-captured in a HIP graph) at the config batch, and both kernels at a large
-batch (2^21 games) where the chip is full.
+captured in a HIP graph) at the config batch, the per-tick kernels at 2^21
+games, C2 and C5.
 
 Rank 0 prints one JSON line.
 """
@@ -151,8 +156,11 @@ def timed_launches(torch, launch, n):
     return [a.elapsed_time(b) * 1e-3 for a, b in evs]
 
 
-def extras(torch, cfg, dev, B_cfg, K):
-    """Unfused path at the config batch (HIP graph) and both paths at 2^21 games."""
+def extras(torch, cfg, dev, B_cfg, K, large_rollout=False):
+    """Unfused path at the config batch (HIP graph), the per-tick kernels at
+    2^21 games (and, with `large_rollout`, the headline rollout kernel there:
+    off by default so that a profile of the bench command sees that kernel at
+    the headline shape only), C2 and C5."""
     from optimax_rogue_amd import OBS_FIELDS
     from optimax_rogue_amd.engine import BatchedEngine
     out = {}
@@ -190,15 +198,8 @@ def extras(torch, cfg, dev, B_cfg, K):
         eng.step(eng.policy(1, 1))
     step_s = timed_launches(torch, lambda: eng.step(), 30)
     pol_s = timed_launches(torch, lambda: eng.policy(1, 1), 30)
-    T = 20
-    obs = torch.empty((T, len(OBS_FIELDS), BL), dtype=torch.int32, device=dev)
-    act = torch.empty((T, BL, 2), dtype=torch.int8, device=dev)
-    eng.rollout(T, 1, 1, obs=obs, act=act)
-    roll_s = timed_launches(torch, lambda: eng.rollout(T, 1, 1, obs=obs, act=act), 5)
     med = lambda v: sorted(v)[len(v) // 2]
     sb = contract_bytes_per_env_step(K) * BL
-    rb = bytes_per_game("rollout", K, T) * BL
-    rc = contract_bytes_per_env_step(K) * BL * T
     out["large_batch"] = {
         "games": BL,
         "step_kernel": {"avg_us": med(step_s) * 1e6, "achieved_GBps": sb / med(step_s) / 1e9,
@@ -206,13 +207,21 @@ def extras(torch, cfg, dev, B_cfg, K):
                         "bytes_per_env_step": contract_bytes_per_env_step(K),
                         "moved_bytes_per_env_step": bytes_per_game("step", K)},
         "policy_kernel": {"avg_us": med(pol_s) * 1e6},
-        "rollout_kernel": {"avg_us": med(roll_s) * 1e6, "ticks": T,
-                           "env_steps_per_s": BL * T / med(roll_s),
-                           "achieved_GBps": rb / med(roll_s) / 1e9,
-                           "frac": rb / med(roll_s) / 1e9 / HBM_PEAK_GBS,
-                           "contract_frac": rc / med(roll_s) / 1e9 / HBM_PEAK_GBS},
     }
-    del eng, obs, act
+    if large_rollout:
+        T = 20
+        obs = torch.empty((T, len(OBS_FIELDS), BL), dtype=torch.int32, device=dev)
+        act = torch.empty((T, BL, 2), dtype=torch.int8, device=dev)
+        eng.rollout(T, 1, 1, obs=obs, act=act)
+        roll_s = timed_launches(torch, lambda: eng.rollout(T, 1, 1, obs=obs, act=act), 5)
+        rb = bytes_per_game("rollout", K, T) * BL
+        rc = contract_bytes_per_env_step(K) * BL * T
+        out["large_batch"]["rollout_kernel"] = {
+            "avg_us": med(roll_s) * 1e6, "ticks": T, "env_steps_per_s": BL * T / med(roll_s),
+            "achieved_GBps": rb / med(roll_s) / 1e9, "frac": rb / med(roll_s) / 1e9 / HBM_PEAK_GBS,
+            "contract_frac": rc / med(roll_s) / 1e9 / HBM_PEAK_GBS}
+        del obs, act
+    del eng
     torch.cuda.empty_cache()
     # (3) the other BASELINE.json GPU configs, fused rollout with trajectories:
     # C2 (4,096 games, 32x32, RandomBot) and C5 (128x128, StaircaseBot "ladder"
@@ -221,16 +230,18 @@ def extras(torch, cfg, dev, B_cfg, K):
     from optimax_rogue_amd import EnvConfig
     from optimax_rogue_amd.enums import EXT_SEPARATION_DAMAGE
 
-    def rollout_rate(c, games, pol, T=128, reps=4):
+    def rollout_rate(c, games, pol, T=128, reps=6):
         e = BatchedEngine(c, games, seed=5, device=dev)
         o = torch.empty((T, len(OBS_FIELDS), games), dtype=torch.int32, device=dev)
         a = torch.empty((T, games, 2), dtype=torch.int8, device=dev)
-        e.rollout(T, pol, pol, obs=o, act=a)
-        d = timed_launches(torch, lambda: e.rollout(T, pol, pol, obs=o, act=a), reps)
+        go = e.rollout_launcher(T, pol, pol, obs=o, act=a)
+        go()
+        d = timed_launches(torch, go, reps)
         us = sorted(d)[len(d) // 2]
-        del e, o, a
-        return {"games": games, "ticks_per_launch": T, "us_per_launch": us * 1e6,
-                "env_steps_per_s": games * T / us}
+        lanes = e.rollout_lanes()
+        del e, o, a, go
+        return {"games": games, "ticks_per_launch": T, "games_per_wave": lanes,
+                "us_per_launch": us * 1e6, "env_steps_per_s": games * T / us}
 
     out["c2"] = dict(rollout_rate(EnvConfig.c2(), 4096, 1), policy="2x RandomBot", grid="32x32")
     c5 = {}
@@ -250,26 +261,32 @@ def extras(torch, cfg, dev, B_cfg, K):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=2048, help="ticks in the timed region")
-    ap.add_argument("--warmup", type=int, default=256)
+    ap.add_argument("--steps", type=int, default=20,
+                    help="timed steps; one step = one --chunk-tick rollout launch of every game")
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=65536, help="games per GPU")
     ap.add_argument("--chunk", type=int, default=128,
-                    help="ticks per rollout launch (the trajectory horizon a learner consumes)")
+                    help="ticks per step (one rollout launch: the trajectory horizon a learner "
+                         "consumes)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
+    ap.add_argument("--large", action="store_true",
+                    help="extras also time the headline rollout kernel at 2^21 games")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, default) or gloo (multi-rank rehearsal on one GPU)")
     ap.add_argument("--same-device", action="store_true",
                     help="every rank uses cuda:0 (rehearsing N ranks on a 1-GPU box)")
     args = ap.parse_args()
+    if args.steps < 1 or args.chunk < 1 or args.warmup < 0:
+        raise SystemExit("--steps and --chunk must be >= 1, --warmup >= 0")
 
     import torch
     import torch.distributed as dist
 
-    from optimax_rogue_amd import EnvConfig, OBS_FIELDS
+    from optimax_rogue_amd import EnvConfig, OBS_FIELDS, _lib
     from optimax_rogue_amd.engine import BatchedEngine
-    from optimax_rogue_amd.parallel import env_rank, gather_returns, init
+    from optimax_rogue_amd.parallel import env_rank, gather_returns, init, shard
 
     rank, world, local = env_rank()
     if args.same_device:
@@ -280,34 +297,28 @@ def main():
     coll_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
 
     cfg = EnvConfig.c3()
-    B = args.batch
-    eng = BatchedEngine(cfg, B, seed=3, game_offset=rank * B, device=dev)
-    chunk = max(1, min(args.chunk, args.steps))
+    G = args.batch * world                    # weak scaling: --batch games per GPU
+    offset, B = shard(G, rank, world)
+    chunk = args.chunk
+    eng = BatchedEngine(cfg, B, seed=3, game_offset=offset, device=dev)
     obs = torch.empty((chunk, len(OBS_FIELDS), B), dtype=torch.int32, device=dev)
     act = torch.empty((chunk, B, 2), dtype=torch.int8, device=dev)
-
-    def run(n_ticks, events=None):
-        left = n_ticks
-        while left > 0:
-            t = min(chunk, left)
-            if events is not None:
-                e0 = torch.cuda.Event(enable_timing=True)
-                e1 = torch.cuda.Event(enable_timing=True)
-                e0.record()
-            eng.rollout(t, 1, 1, obs=obs, act=act)
-            if events is not None:
-                e1.record()
-                events.append((e0, e1, t))
-            left -= t
-
-    run(args.warmup)
+    launch = eng.rollout_launcher(chunk, 1, 1, obs=obs, act=act)
+    for _ in range(args.warmup):
+        launch()
+    # HIP events on the launch stream (torch's current stream, the one the
+    # engine launches on), created before the timed region, bracketing the K
+    # back-to-back launches
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    events = []
     t0 = time.perf_counter()
-    run(args.steps, events)
+    e0.record()
+    for _ in range(args.steps):
+        launch()
+    e1.record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -317,39 +328,39 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # dominant kernel: average duration of the full-chunk rollout launches.
+    # dominant kernel: average duration of the timed rollout launches.
     # roofline.achieved prices a launch with the bytes the fused kernel must
     # move (its trajectory rows + the state once per launch);
     # SURVEY s8(d)'s per-tick contract figure (106 B/env-step: state re-read
     # and re-written every tick) is reported beside it as contract_*.
-    durs = [(a.elapsed_time(b) * 1e-3, n) for a, b, n in events]
-    full = [d for d, n in durs if n == chunk]
-    avg_launch_s = sum(full) / max(1, len(full))
+    avg_launch_s = e0.elapsed_time(e1) * 1e-3 / args.steps
     materialized = bytes_per_game("rollout", cfg.n_npcs, chunk) * B
     achieved_gbs = materialized / avg_launch_s / 1e9
     contract_bytes = contract_bytes_per_env_step(cfg.n_npcs) * B * chunk
+    lanes = eng.rollout_lanes()
 
     # the only collective: all-gather of per-game episode returns (RCCL / xGMI)
     torch.cuda.synchronize()
     g0 = time.perf_counter()
-    allrets = gather_returns(eng.episode_returns(), B * world)
+    allrets = gather_returns(eng.episode_returns(), G)
     torch.cuda.synchronize()
     gather_ms = (time.perf_counter() - g0) * 1e3 if world > 1 else None
     episodes = int(allrets[1].sum().item())
     mean_ret = float(allrets[0].sum().item()) / max(1, episodes)
 
-    value = B * world * args.steps / elapsed
+    value = G * chunk * args.steps / elapsed
     if rank == 0:
         traffic = None
         if os.path.exists(TRAFFIC_FILE):
             tr = json.load(open(TRAFFIC_FILE)).get("rollout", {})
-            if tr.get("batch") == B and tr.get("ticks") == chunk:
+            if tr.get("batch") == B and tr.get("ticks") == chunk \
+                    and tr.get("build_id") == _lib.build_id():
                 traffic = tr.get("hbm_bytes_per_launch")
         extra = None
         if not args.no_extras and world == 1:
-            del obs, act
+            del obs, act, launch
             torch.cuda.empty_cache()
-            extra = extras(torch, cfg, dev, B, cfg.n_npcs)
+            extra = extras(torch, cfg, dev, B, cfg.n_npcs, args.large)
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(cfg.to_dict(), args.cpu_seconds)
@@ -368,11 +379,14 @@ def main():
             "data": "synthetic (Philox-seeded dungeons and RandomBot actions)",
             "config": {
                 "workload": "C3: 65536 games/GPU, 64x64 grid, 8 NPCs/game, 2x RandomBot, "
-                            "Unreachable despawn, max_ticks 1000, autoreset; every tick's "
+                            "Unreachable despawn, max_ticks 1000, autoreset; one step = one "
+                            f"{chunk}-tick rollout launch of every game, every tick's "
                             "observation + actions written to HBM",
-                "batch_per_gpu": B, "global_batch": B * world, "grid": "64x64",
-                "n_npcs": cfg.n_npcs, "ticks_per_launch": chunk,
+                "batch_per_gpu": B, "global_batch": G, "grid": "64x64",
+                "n_npcs": cfg.n_npcs, "ticks_per_step": chunk,
+                "env_steps_per_step": G * chunk, "games_per_wave": lanes,
                 "parallelism": f"games sharded by global id over {world} GPU(s)",
+                "build_id": _lib.build_id(),
             },
             "roofline": {
                 "bound": "hbm",
@@ -386,16 +400,17 @@ def main():
                 "bytes_per_env_step": materialized / (B * chunk),
                 "env_steps_per_launch": B * chunk,
                 "avg_launch_us": avg_launch_s * 1e6,
-                "launches": len(full),
+                "launches": args.steps,
                 "contract_bytes_per_env_step": contract_bytes_per_env_step(cfg.n_npcs),
                 "contract_bytes_per_launch": contract_bytes,
                 "contract_GBps": contract_bytes / avg_launch_s / 1e9,
                 "contract_frac": contract_bytes / avg_launch_s / 1e9 / HBM_PEAK_GBS,
                 "note": "achieved = the fused rollout's own algorithmic bytes (56 B observation "
                         "+ 2 B actions per env-step, state read and written once per launch); "
-                        "contract_* = SURVEY s8(d)'s per-tick 106 B/env-step, which counts a "
-                        "state re-read every tick that the fused kernel never makes, hence "
-                        "contract_frac can exceed 1",
+                        "traffic = PMC HBM bytes per launch of this command (profiles/"
+                        "traffic.json, same build id); contract_* = SURVEY s8(d)'s per-tick "
+                        "106 B/env-step, which counts a state re-read every tick that the "
+                        "fused kernel never makes, hence contract_frac can exceed 1",
             },
             "cpu_baseline": cpu,
             "episodes_finished": episodes,

@@ -222,6 +222,18 @@ typedef struct orx_state {
 /* ORX_ABI_VERSION of the loaded library. */
 int orx_abi_version(void);
 
+/* Source hash the library was built from: the first 16 hex digits of the
+ * SHA-256 of orx_engine.hip followed by include/orx.h (build.py), so a test
+ * can prove the loaded library is the tree's own kernel ("unknown" for a
+ * build made outside build.py).  No reference counterpart. */
+const char* orx_build_id(void);
+
+/* Games per wave orx_rollout launches for a batch of n_games (1..64, a power
+ * of two; < 64 when the batch is too small to give every SIMD of the current
+ * device a wave; env ORX_ROLLOUT_LANES overrides).  Results do not depend on
+ * it.  No reference counterpart (the reference runs one game per process). */
+int orx_rollout_lanes(int64_t n_games);
+
 /* Message for the last non-zero return on this thread ("" if none). */
 const char* orx_last_error(void);
 

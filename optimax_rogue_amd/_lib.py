@@ -35,7 +35,7 @@ _lib = None
 
 EXPORTS = ("orx_abi_version", "orx_last_error", "orx_validate_cfg", "orx_reset", "orx_step",
            "orx_step_events", "orx_policy", "orx_rollout", "orx_dungeon_stairs",
-           "orx_dungeon_spawn", "orx_seed_mt")
+           "orx_dungeon_spawn", "orx_seed_mt", "orx_build_id", "orx_rollout_lanes")
 
 
 def load() -> ctypes.CDLL:
@@ -74,6 +74,10 @@ def load() -> ctypes.CDLL:
                                     vp]
     L.orx_seed_mt.restype = ctypes.c_int
     L.orx_seed_mt.argtypes = [P(OrxCfg), P(OrxState), i64, u64, i64, vp]
+    L.orx_build_id.restype = ctypes.c_char_p
+    L.orx_build_id.argtypes = []
+    L.orx_rollout_lanes.restype = ctypes.c_int
+    L.orx_rollout_lanes.argtypes = [i64]
     v = L.orx_abi_version()
     if v != ABI_VERSION:
         raise RuntimeError(f"liborx.so ABI {v} != expected {ABI_VERSION}")
@@ -85,3 +89,8 @@ def check(fn: str, code: int) -> None:
     if code != 0:
         msg = load().orx_last_error().decode(errors="replace")
         raise OrxError(fn, code, msg)
+
+
+def build_id() -> str:
+    """orx_build_id() of the loaded library (build.source_id() of its sources)."""
+    return load().orx_build_id().decode()

@@ -4,6 +4,7 @@
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import subprocess
 import sys
@@ -23,12 +24,35 @@ def hipcc() -> str:
     return "hipcc"
 
 
+def built_id(path: str = OUT):
+    """orx_build_id() of the library at `path` (None if it cannot be loaded),
+    read in a child process so this one does not map a library that a later
+    build replaces."""
+    code = ("import ctypes,sys; L=ctypes.CDLL(sys.argv[1]); "
+            "L.orx_build_id.restype=ctypes.c_char_p; print(L.orx_build_id().decode())")
+    try:
+        out = subprocess.run([sys.executable, "-c", code, path], capture_output=True, text=True,
+                             timeout=60)
+    except (OSError, subprocess.SubprocessError):
+        return None
+    return out.stdout.strip() if out.returncode == 0 else None
+
+
+def source_id() -> str:
+    """First 16 hex digits of SHA-256(orx_engine.hip || orx.h): the id
+    orx_build_id() of a library built from these sources returns."""
+    h = hashlib.sha256()
+    for p in (SRC, HDR):
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
-    newest = max(os.path.getmtime(SRC), os.path.getmtime(HDR))
-    if not force and os.path.exists(OUT) and os.path.getmtime(OUT) >= newest:
+    if not force and os.path.exists(OUT) and built_id() == source_id():
         return OUT
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC",
-           "-Wall", "-o", OUT + ".tmp", SRC]
+           "-Wall", f'-DORX_BUILD_ID="{source_id()}"', "-o", OUT + ".tmp", SRC]
     if verbose:
         print(" ".join(cmd))
     subprocess.check_call(cmd)

@@ -43,6 +43,7 @@
 //     with a single Philox call site.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -92,13 +93,10 @@ __device__ uint64_t g_stamps[65536 * 16];
 #define ORX_ROLLOUT_BLOCK 256
 #endif
 constexpr int kRolloutBlock = ORX_ROLLOUT_BLOCK;  // rollout_kernel workgroup size
-#ifndef ORX_ROLLOUT_LANES
-#define ORX_ROLLOUT_LANES 64
-#endif
-// games per rollout wave (experiment: < 64 leaves lanes idle to put more waves
-// on each SIMD at a fixed batch)
-constexpr int kRolloutLanes = ORX_ROLLOUT_LANES;
-constexpr int kRolloutGamesPerBlock = kRolloutBlock / 64 * kRolloutLanes;
+// Games per rollout wave ("lanes", a power of two 1..64) is a launch
+// argument: below 64 the wave's upper lanes idle so that a small batch still
+// puts a wave on every SIMD (orx_rollout picks it from the batch and the CU
+// count, rollout_lanes()).
 
 struct Key {
   uint32_t k0, k1;
@@ -1591,13 +1589,13 @@ __global__ void __launch_bounds__(kRolloutBlock) rollout_kernel(orx_cfg_t hc, or
                                                       int32_t pol2_, int32_t n_ticks,
                                                       int32_t* __restrict__ obs,
                                                       int8_t* __restrict__ act, uint32_t B,
-                                                      Key key, uint32_t off) {
+                                                      Key key, uint32_t off, uint32_t lanes) {
   const int32_t pol1 = FAST ? (int32_t)ORX_POLICY_RANDOM : pol1_;
   const int32_t pol2 = FAST ? (int32_t)ORX_POLICY_RANDOM : pol2_;
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if constexpr (kRolloutLanes < 64) {
-    if ((threadIdx.x & 63u) >= (uint32_t)kRolloutLanes) return;
-    i = (i >> 6) * kRolloutLanes + (threadIdx.x & 63u);
+  if (lanes < 64u) {  // uniform: lanes >= `lanes` of every wave idle
+    if ((threadIdx.x & 63u) >= lanes) return;
+    i = (i >> 6) * lanes + (threadIdx.x & 63u);
   }
   if (i >= B) return;
   Cfg c = make_cfg(hc, st);
@@ -2029,11 +2027,63 @@ int check_sizes(int64_t B, int64_t off) {
 // NPC slot capacity of the kernel instance for K NPCs.
 inline int ncap_for(int K) { return K == 0 ? 0 : K <= 8 ? 8 : 16; }
 
+// Games per rollout wave.  A rollout lane runs its game's whole tick stream,
+// so a wave's time is set by its instruction stream, not by how many of its
+// lanes are busy: a batch too small to put a wave on every SIMD (4 per CU) is
+// spread over more, narrower waves, which also take the rare block on fewer
+// ticks (C5 at 16,384 games: 232 us per 128-tick launch at 64 games per wave,
+// 158 at 16).  Not below 16: narrower waves share each 128-B trajectory line
+// among four or more waves, and launches took twice as long (C2 at 4,096
+// games: 77 us at 16, 155 at 8).  Two half-full waves per SIMD lose to one
+// full one (C3: 101 us at 64, 130 at 32), so the rule is "at most one wave per
+// SIMD until the wave is full".  The environment variable ORX_ROLLOUT_LANES
+// (1..64, a power of two) overrides it for measurements.
+constexpr int kMaxDevices = 64;
+constexpr uint32_t kMinLanes = 16;
+std::atomic<int> g_cu_count[kMaxDevices];
+
+int device_simds() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return 1024;
+  int n = g_cu_count[dev].load(std::memory_order_relaxed);
+  if (n <= 0) {
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        n <= 0)
+      n = 256;
+    g_cu_count[dev].store(n, std::memory_order_relaxed);
+  }
+  return 4 * n;
+}
+
+int lanes_override() {  // read per launch, so a sweep can change it in-process
+  const char* e = getenv("ORX_ROLLOUT_LANES");
+  const int x = e ? atoi(e) : 0;
+  return (x >= 1 && x <= 64 && (x & (x - 1)) == 0) ? x : 0;
+}
+
+uint32_t rollout_lanes(uint32_t B) {
+  if (const int o = lanes_override()) return (uint32_t)o;
+  const uint64_t simds = (uint64_t)device_simds();
+  uint32_t L = 64;
+  while (L > kMinLanes && (uint64_t)B < simds * L) L >>= 1;
+  return L;
+}
+
 }  // namespace
 
 extern "C" {
 
 int orx_abi_version(void) { return ORX_ABI_VERSION; }
+
+#ifndef ORX_BUILD_ID
+#define ORX_BUILD_ID "unknown"
+#endif
+const char* orx_build_id(void) { return ORX_BUILD_ID; }
+
+int orx_rollout_lanes(int64_t n_games) {
+  if (n_games <= 0 || n_games > 0x7FFFFFFFLL) return fail(ORX_EINVAL, "bad n_games");
+  return (int)rollout_lanes((uint32_t)n_games);
+}
 
 const char* orx_last_error(void) { return g_err; }
 
@@ -2188,12 +2238,13 @@ int orx_rollout(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p1, 
   const bool rr = !grid && cfg->flags == 0 && policy_p1 == ORX_POLICY_RANDOM &&
                   policy_p2 == ORX_POLICY_RANDOM && obs && act &&
                   (uint64_t)B * ORX_OBS_FIELDS * 4u < (1ull << 31);
+  const uint32_t lanes = rollout_lanes(B);
+  const uint32_t per_block = (uint32_t)kRolloutBlock / 64u * lanes;
 #define ORX_ROLLOUT(N, R, G)                                                                    \
   if (nc == N && rr == R && grid == G)                                                          \
-    hipLaunchKernelGGL((rollout_kernel<N, R, G>),                                               \
-                       dim3((B + kRolloutGamesPerBlock - 1) / kRolloutGamesPerBlock),            \
+    hipLaunchKernelGGL((rollout_kernel<N, R, G>), dim3((B + per_block - 1) / per_block),        \
                        dim3(kRolloutBlock), 0, s, *cfg, *st,                                    \
-                       policy_p1, policy_p2, n_ticks, obs, act, B, k, off);
+                       policy_p1, policy_p2, n_ticks, obs, act, B, k, off, lanes);
   ORX_ROLLOUT(0, false, false) ORX_ROLLOUT(0, true, false) ORX_ROLLOUT(8, false, false)
   ORX_ROLLOUT(8, true, false) ORX_ROLLOUT(16, false, false) ORX_ROLLOUT(16, true, false)
   ORX_ROLLOUT(0, false, true) ORX_ROLLOUT(8, false, true) ORX_ROLLOUT(16, false, true)

@@ -97,6 +97,7 @@ class BatchedEngine:
             self.dstore = z(DSTORE, 2, B)
             ptrs.update({f: getattr(self, f).data_ptr() for f in ("mt_py", "mt_np", "dstore")})
         self._st = _lib.OrxState(**ptrs)
+        self._pcfg, self._pst = ctypes.byref(self._ccfg), ctypes.byref(self._st)
         if self.mt_py is not None:
             self.seed_rng()
         if reset:
@@ -107,9 +108,33 @@ class BatchedEngine:
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
     def _call(self, name, *args):
-        with torch.cuda.device(self.device):
-            code = getattr(self.lib, name)(ctypes.byref(self._ccfg), ctypes.byref(self._st), *args)
+        fn = getattr(self.lib, name)
+        if torch.cuda.current_device() == self.device.index:
+            code = fn(self._pcfg, self._pst, *args)
+        else:
+            with torch.cuda.device(self.device):
+                code = fn(self._pcfg, self._pst, *args)
         _lib.check(name, code)
+
+    def rollout_launcher(self, n_ticks: int, p1: int = Policy.Random, p2: int = Policy.Random,
+                         obs: Optional[torch.Tensor] = None, act: Optional[torch.Tensor] = None):
+        """A zero-argument callable that launches ``rollout(n_ticks, p1, p2, obs,
+        act)`` on the current stream of this moment, its C arguments bound once
+        (a timed loop then pays one ctypes call per launch, nothing else)."""
+        self._check_traj(n_ticks, obs, act)
+        fn, check = self.lib.orx_rollout, _lib.check
+        args = (self._pcfg, self._pst, int(p1), int(p2), int(n_ticks), _ptr(obs), _ptr(act),
+                self.B, self.seed, self.game_offset, self._stream())
+
+        def launch():
+            code = fn(*args)
+            if code:
+                check("orx_rollout", code)
+        return launch
+
+    def rollout_lanes(self) -> int:
+        """Games per wave of this batch's rollout launches (orx_rollout_lanes)."""
+        return int(self.lib.orx_rollout_lanes(self.B))
 
     # -- the C-ABI entry points -------------------------------------------
     def seed_rng(self, seed: Optional[int] = None) -> None:
@@ -174,13 +199,18 @@ class BatchedEngine:
         """n_ticks x (policy, step) fused in one launch.  ``obs`` (int32
         [n_ticks, len(OBS_FIELDS), n_games]) and ``act`` (int8 [n_ticks,
         n_games, 2]) receive every tick's observation and actions."""
-        if obs is not None and (obs.dtype != torch.int32 or obs.numel() <
-                                n_ticks * len(OBS_FIELDS) * self.B):
-            raise ValueError("obs must be int32 [n_ticks, 14, n_games]")
-        if act is not None and (act.dtype != torch.int8 or act.numel() < n_ticks * self.B * 2):
-            raise ValueError("act must be int8 [n_ticks, n_games, 2]")
+        self._check_traj(n_ticks, obs, act)
         self._call("orx_rollout", int(p1), int(p2), int(n_ticks), _ptr(obs), _ptr(act), self.B,
                    self.seed, self.game_offset, self._stream())
+
+    def _check_traj(self, n_ticks, obs, act):
+        for t, dt, n, what in ((obs, torch.int32, n_ticks * len(OBS_FIELDS) * self.B,
+                                "obs must be a contiguous int32 [n_ticks, 14, n_games] tensor"),
+                               (act, torch.int8, n_ticks * self.B * 2,
+                                "act must be a contiguous int8 [n_ticks, n_games, 2] tensor")):
+            if t is not None and (t.dtype != dt or t.numel() < n or not t.is_contiguous()
+                                  or t.device != self.device):
+                raise ValueError(f"{what} on {self.device}")
 
     # -- host views -----------------------------------------------------------
     def snapshot(self) -> dict:

@@ -38,7 +38,8 @@ def test_library_exports_every_declared_symbol(lib):
     decl = declared_functions()
     assert decl == sorted(["orx_abi_version", "orx_last_error", "orx_validate_cfg", "orx_reset",
                            "orx_step", "orx_step_events", "orx_policy", "orx_rollout",
-                           "orx_dungeon_stairs", "orx_dungeon_spawn", "orx_seed_mt"])
+                           "orx_dungeon_stairs", "orx_dungeon_spawn", "orx_seed_mt",
+                           "orx_build_id", "orx_rollout_lanes"])
     from optimax_rogue_amd import _lib
     assert sorted(_lib.EXPORTS) == decl
     for name in decl:
@@ -48,6 +49,12 @@ def test_library_exports_every_declared_symbol(lib):
                          capture_output=True, text=True, check=True).stdout
     exported = set(re.findall(r" T (orx_\w+)", out))
     assert set(decl) <= exported
+
+
+def test_library_is_built_from_the_tree(lib):
+    """orx_build_id() is the hash of the tree's own orx_engine.hip + orx.h."""
+    from optimax_rogue_amd import _lib, build
+    assert _lib.build_id() == build.source_id()
 
 
 def test_struct_layouts_match_header():

@@ -210,6 +210,50 @@ def test_sharding_invariance():
         assert np.array_equal(sf[k], np.concatenate([sa[k], sb[k]], axis=axis)), k
 
 
+def test_loaded_library_is_the_trees_kernel():
+    """The liborx.so these tests run was built from this tree's sources."""
+    from optimax_rogue_amd import _lib, build
+    _engine(dict(width=8, height=8), 1, 0)
+    assert _lib.build_id() == build.source_id()
+
+
+@pytest.mark.parametrize("which", ["c5_sep", "npc_dense", "c3"])
+def test_rollout_games_per_wave_invariance(which, monkeypatch):
+    """Results do not depend on how many games a rollout wave carries
+    (orx_rollout_lanes; ORX_ROLLOUT_LANES forces it), FAST and plain kernels,
+    with trajectories, across resets, descends and NPC hits."""
+    import torch
+    from optimax_rogue_amd import EnvConfig
+    from optimax_rogue_amd.enums import EXT_SEPARATION_DAMAGE, OBS_FIELDS
+    if which == "c5_sep":
+        cfg = dict(EnvConfig.c5().to_dict(), width=16, height=12, max_ticks=90,
+                   flags=EXT_SEPARATION_DAMAGE, sep_period=4)
+        pol, B, T = (2, 1), 3001, 300
+    elif which == "npc_dense":
+        cfg = dict(width=8, height=8, n_npcs=16, max_ticks=60)
+        pol, B, T = (1, 2), 2053, 200
+    else:
+        cfg = dict(EnvConfig.c3().to_dict(), max_ticks=100)
+        pol, B, T = (1, 1), 4099, 150
+    ref = None
+    for lanes in (64, 32, 8, 1):
+        monkeypatch.setenv("ORX_ROLLOUT_LANES", str(lanes))
+        e = _engine(cfg, B, 11, 7)
+        assert e.rollout_lanes() == lanes
+        obs = torch.zeros((T, len(OBS_FIELDS), B), dtype=torch.int32, device=e.device)
+        act = torch.zeros((T, B, 2), dtype=torch.int8, device=e.device)
+        e.rollout(T // 2, *pol, obs=obs, act=act)
+        e.rollout(T - T // 2, *pol, obs=obs[T // 2:], act=act[T // 2:])
+        got = (e.snapshot(), obs.cpu().numpy(), act.cpu().numpy())
+        if ref is None:
+            ref = got
+            continue
+        for k in STATE_KEYS:
+            assert np.array_equal(got[0][k], ref[0][k]), (lanes, k)
+        assert np.array_equal(got[1], ref[1]) and np.array_equal(got[2], ref[2]), lanes
+    assert ref[0]["ep_count"].sum() > 0
+
+
 def test_rollout_equals_step_c3():
     """C3 shape (B=65536, 64x64, K=8): fused rollout == per-tick policy+step."""
     from optimax_rogue_amd import EnvConfig

@@ -1,12 +1,14 @@
-"""Summarizes a rocprofv3 kernel_trace.csv: consecutive dispatches of the same
-kernel + grid size form a segment; prints each segment's count and median /
-mean duration (us), in launch order."""
+"""Summarizes a rocprofv3 kernel_trace.csv: dispatches are grouped by kernel
++ grid size (--segments: consecutive runs of the same kernel + grid, in launch
+order); prints each group's count and median / mean duration (us), ordered by
+total time."""
 import csv
 import statistics
 import sys
 
 
-def main(path, only=None):
+def main(path, only=None, segments=False):
+    groups = {}
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     segs = []
@@ -17,14 +19,20 @@ def main(path, only=None):
             continue
         key = (name, r["Grid_Size_X"] if "Grid_Size_X" in r else r.get("Grid_Size"))
         d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
-        if segs and segs[-1][0] == key:
-            segs[-1][1].append(d)
+        if segments:
+            if segs and segs[-1][0] == key:
+                segs[-1][1].append(d)
+            else:
+                segs.append((key, [d]))
         else:
-            segs.append((key, [d]))
+            groups.setdefault(key, []).append(d)
+    if not segments:
+        segs = sorted(groups.items(), key=lambda kv: -sum(kv[1]))
     for (name, grid), ds in segs:
         print(f"{name[:60]:60s} grid={grid:>9s} n={len(ds):4d} median={statistics.median(ds):10.2f}us "
               f"mean={statistics.mean(ds):10.2f}us")
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None)
+    args = [a for a in sys.argv[1:] if a != "--segments"]
+    main(args[0], args[1] if len(args) > 1 else None, "--segments" in sys.argv)

@@ -1,10 +1,15 @@
-"""Writes profiles/traffic.json from the two rocprofv3 PMC passes of
-tools/_gpu_final.sh (FETCH_SIZE and WRITE_SIZE over tools/prof_kernels.py).
+"""Writes profiles/traffic.json from two rocprofv3 PMC passes over the bench
+command itself (tools/gpu_profile.sh):
 
-    python tools/make_traffic.py gpurun_out/prof/fetch gpurun_out/prof/write
+    rocprofv3 --pmc FETCH_SIZE -d <fetch dir> ... -- python3 bench.py --gpus 1 --steps 20 --warmup 5
+    rocprofv3 --pmc WRITE_SIZE -d <write dir> ... -- python3 bench.py --gpus 1 --steps 20 --warmup 5
+    python tools/make_traffic.py <fetch dir> <write dir> [out.json]
 
 HBM bytes per launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024: FETCH_SIZE is
 doubled per MI355X_MICROARCH.md (gfx950 tallies 128-B read requests at 64 B).
+Only the dispatches of the headline kernel at the headline grid are averaged
+(bench.py launches that kernel at no other shape by default).  The entry is
+stamped with the library's build id: bench.py uses it only for that build.
 """
 import collections
 import csv
@@ -25,36 +30,38 @@ def load(d, counter):
             continue
         name = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "")
         agg[(name.split("(")[0], int(r["Grid_Size"]))].append(float(r["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in agg.items()}
+    return {k: (sum(v) / len(v), len(v)) for k, v in agg.items()}
 
 
-def main(fetch_dir, write_dir):
+def main(fetch_dir, write_dir, out_path=None, batch=65536, ticks=128):
     import bench
+    from optimax_rogue_amd import _lib
     fe, wr = load(fetch_dir, "FETCH_SIZE"), load(write_dir, "WRITE_SIZE")
-    out = {"_source": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over "
-                      "tools/prof_kernels.py (MI355X, ROCm 7.2), written by tools/make_traffic.py. "
-                      "hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024: FETCH_SIZE doubled per "
-                      "MI355X_MICROARCH.md (gfx950 tallies 128-B read requests at 64 B). Per "
-                      "launch, averaged over the profiled dispatches."}
-    # (key, kernel prefix, grid, batch, ticks, algorithmic bytes per launch)
     K = 8
-    rows = [("step_kernel", "step_kernel<8, false, false>", 1 << 21, 1 << 21, 1,
-             bench.bytes_per_game("step", K) * (1 << 21)),
-            ("rollout", "rollout_kernel<8, true, false>", 65536, 65536, 128,
-             bench.bytes_per_game("rollout", K, 128) * 65536),
-            ("rollout_large", "rollout_kernel<8, true, false>", 1 << 21, 1 << 21, 20,
-             bench.bytes_per_game("rollout", K, 20) * (1 << 21))]
-    for key, kname, grid, batch, ticks, alg in rows:
-        f, w = fe.get((kname, grid)), wr.get((kname, grid))
-        if f is None or w is None:
-            print("missing", key, kname, grid, file=sys.stderr)
-            continue
-        out[key] = {"kernel": kname, "batch": batch, "ticks": ticks, "fetch_kb": round(f, 1),
-                    "write_kb": round(w, 1), "hbm_bytes_per_launch": int((2 * f + w) * 1024),
-                    "algorithmic_bytes_per_launch": int(alg)}
-    json.dump(out, open(os.path.join(ROOT, "profiles", "traffic.json"), "w"), indent=1)
+    kname = bench.rollout_kernel_name(batch, K)
+    lanes = _lib.load().orx_rollout_lanes(batch)
+    grid = -(-batch // (4 * lanes)) * 256        # 256-thread blocks of 4 waves
+    out = {"_source": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over "
+                      "`python3 bench.py --gpus 1 --steps 20 --warmup 5` (MI355X, ROCm 7.2), "
+                      "written by tools/make_traffic.py. hbm_bytes = (2 * FETCH_SIZE + "
+                      "WRITE_SIZE) * 1024: FETCH_SIZE doubled per MI355X_MICROARCH.md (gfx950 "
+                      "tallies 128-B read requests at 64 B). Per launch, averaged over the "
+                      "profiled dispatches of the headline kernel at the headline grid."}
+    f, w = fe.get((kname, grid)), wr.get((kname, grid))
+    if f is None or w is None:
+        raise SystemExit(f"no dispatches of {kname} at grid {grid}: {sorted(fe)}")
+    alg = bench.bytes_per_game("rollout", K, ticks) * batch
+    out["rollout"] = {"kernel": kname, "batch": batch, "ticks": ticks, "grid": grid,
+                      "games_per_wave": lanes, "dispatches": [f[1], w[1]],
+                      "fetch_kb": round(f[0], 1), "write_kb": round(w[0], 1),
+                      "hbm_bytes_per_launch": int((2 * f[0] + w[0]) * 1024),
+                      "algorithmic_bytes_per_launch": int(alg),
+                      "ratio": round((2 * f[0] + w[0]) * 1024 / alg, 4),
+                      "build_id": _lib.build_id()}
+    out_path = out_path or os.path.join(ROOT, "profiles", "traffic.json")
+    json.dump(out, open(out_path, "w"), indent=1)
     print(json.dumps(out, indent=1))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(*sys.argv[1:4])
