@@ -562,6 +562,14 @@ CASES = {
                              ticks=260),
     # C3 shape: 64x64, K=8 NPCs, random
     "c3_npc_64": dict(cfg=dict(width=64, height=64, n_npcs=8), seed=3, games=6, ticks=300),
+    # C3 at full episode length: 64x64, K=8, max_ticks 1000, past the first
+    # autoreset (NPC hits and kills, descents, episode ends)
+    "c3_npc_64_long": dict(cfg=dict(width=64, height=64, n_npcs=8), seed=31, games=32,
+                           ticks=1100),
+    # C5 shape: 128x128, both StaircaseBot ("ladder"), Unreachable, past the
+    # first autoreset
+    "c5_stairs_128": dict(cfg=dict(width=128, height=128, policy=(2, 2)), seed=51, games=12,
+                          ticks=1100),
     # minimum board (W=H=4: staircase fixed at (1,1), no dungeon draws)
     "tiny_4": dict(cfg=dict(width=4, height=4, max_ticks=40, n_npcs=1, policy=(1, 2)), seed=9,
                    games=16, ticks=200),

@@ -63,6 +63,24 @@ def test_fixtures_cover_the_paths():
     assert npcs and unused_regen
 
 
+@pytest.mark.parametrize("name,shape,need", [
+    # BASELINE.json configs[2] (C3): 64x64, K=8, RandomBot, max_ticks 1000
+    ("c3_npc_64_long", (64, 64, 8), ("combat", "npc_death", "descend", "episode")),
+    # configs[4] (C5) without its build extension: 128x128, StaircaseBot pair
+    ("c5_stairs_128", (128, 128, 0), ("descend", "deep", "episode")),
+])
+def test_config_fixtures_cover_their_paths(name, shape, need):
+    """The reference fixtures at the headline shapes are not movement-only:
+    they hold combats, NPC deaths, descents and finished episodes."""
+    fx = Fixture(name)
+    assert (fx.cfg["width"], fx.cfg["height"], fx.K) == shape
+    c = fx.z["counters"][-1]
+    got = {"combat": c[0].sum() > 0, "descend": c[1].sum() > 0, "npc_death": c[3].sum() > 0,
+           "episode": fx.z["ep_count"][-1].sum() >= fx.G, "deep": fx.z["p_depth"].max() >= 5}
+    assert all(got[k] for k in need), got
+    assert fx.T >= 1100 and fx.cfg["max_ticks"] == 1000
+
+
 def test_oracle_sharding_invariance(oracle_lib):
     cfg = dict(width=9, height=7, n_npcs=3, max_ticks=60)
     full = oracle_lib.Oracle(cfg, 300, 5, 0)
