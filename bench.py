@@ -44,6 +44,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 OBS_BYTES = 14 * 4      # one tick record: 14 int32 fields
 ACT_BYTES = 2
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic.json")
+# the reference's own Python updater timed on the build container's cores
+# (tools/ref_cpu_baseline.py; the reference never travels to the GPU box)
+REF_CPU_FILE = os.path.join(ROOT, "profiles", "ref_cpu_c3.json")
 
 
 def contract_bytes_per_env_step(K: int) -> int:
@@ -90,7 +93,9 @@ def _cpu_model() -> str:
 
 
 def cpu_baseline(cfg_dict: dict, seconds: float) -> dict:
-    """The C oracle (scalar port of the reference updater) on the host cores,
+    """The C oracle (scalar port of the reference updater) on the host cores
+    (the reference's own Python updater, timed in the build container, rides
+    beside it as `reference_python`),
     same workload shape: one core for `seconds` * 0.4, then one thread per
     core of this job's CPU share (at most 16, the GPU box's share per GPU) for
     `seconds` * 1.5 / cores each -- about `seconds` * 2 of CPU work in all.
@@ -132,7 +137,20 @@ def cpu_baseline(cfg_dict: dict, seconds: float) -> dict:
         t.join()
     el = time.perf_counter() - t0
     total = sum(B * n for n, _ in res.values())
+    ref = None
+    if os.path.exists(REF_CPU_FILE):
+        r = json.load(open(REF_CPU_FILE))
+        full = r["full"]
+        ref = {"value": full["aggregate_env_steps_per_s"], "unit": "env-steps/s",
+               "cores": full["procs"], "per_core": full["per_core_env_steps_per_s"],
+               "single_core": full["single_core_env_steps_per_s"], "host": r["host"],
+               "where": "build container (the reference cannot run on the GPU box)",
+               "sample": f"{r['workload']}; the reference's RandomBot.move x2 + on_tick + "
+                         f"Updater.update, one process per core for "
+                         f"{full['seconds_per_proc']} s each ({full['env_steps']} env-steps); "
+                         "tools/ref_cpu_baseline.py -> profiles/ref_cpu_c3.json"}
     return {"value": total / el, "unit": "env-steps/s", "cores": cores, "kind": "port",
+            "reference_python": ref,
             "per_core": total / el / cores, "single_core": single,
             "sample": f"C oracle (scalar C restatement of Updater.update + RandomBot) on the "
                       f"same C3 workload: {cores} threads x 256 games for {el:.1f} s "
