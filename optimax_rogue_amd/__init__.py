@@ -10,14 +10,14 @@ from .enums import (CombatFlag, DungeonDespawningStrategy, Move, OBS_FIELDS, Pol
                     Tile, UpdateResult)
 
 __all__ = ["EnvConfig", "DungeonBank", "Move", "UpdateResult", "DungeonDespawningStrategy", "Tile", "CombatFlag",
-           "StartMode", "Policy", "OBS_FIELDS", "BatchedEngine", "BatchedUpdater"]
+           "StartMode", "Policy", "OBS_FIELDS", "BatchedEngine", "StreamShardedEngine", "BatchedUpdater"]
 
 
 def __getattr__(name):
     # lazy: importing the package must not require torch / the built library
-    if name == "BatchedEngine":
-        from .engine import BatchedEngine
-        return BatchedEngine
+    if name in ("BatchedEngine", "StreamShardedEngine"):
+        from . import engine
+        return getattr(engine, name)
     if name == "BatchedUpdater":
         from .updater import BatchedUpdater
         return BatchedUpdater

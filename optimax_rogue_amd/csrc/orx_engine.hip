@@ -728,6 +728,27 @@ __device__ __forceinline__ W4 tick_block(Key key, uint32_t game, uint32_t ep, in
   return philox(game, ep, (uint32_t)tick, tag(PUR_TICK, 0), key);
 }
 
+// v_med3_i32: x clamped to [lo, hi]
+__device__ __forceinline__ int32_t med3_i32(int32_t x, int32_t lo, int32_t hi) {
+  int32_t r;
+  asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(lo), "s"(hi));
+  return r;
+}
+
+// An empty asm that "changes" its operands: values derived from them after
+// this point are recomputed rather than kept live from before it.
+__device__ __forceinline__ void launder(int32_t& a, int32_t& b, int32_t& c, int32_t& d) {
+  asm volatile("" : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+}
+
+// v_ffbl_b32: index of the lowest set bit, 0xFFFFFFFF for 0 (an opaque asm
+// so the compiler neither adds a zero guard nor reasons from ctz(0) being UB)
+__device__ __forceinline__ uint32_t ffbl(uint32_t x) {
+  uint32_t r;
+  asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(x));
+  return r;
+}
+
 // bit 0 of each accepted three-bit field among a word's low ten
 __device__ __forceinline__ uint32_t accepted3(uint32_t w) {
   return ~((w >> 2) & (w | (w >> 1))) & 0x09249249u;
@@ -1333,31 +1354,42 @@ __device__ __forceinline__ void rollout_tick(const Cfg& c, const orx_state_t& st
   // one tick block: the bots' bits and the initiative bits (§4)
   const W4 tb = tick_block(key, game, ep, tick);
   const uint32_t pk_shf = tb.a;
-  // RandomBot draws: the first accepted 3-bit fields of bits 0-29 of word b,
-  // then of word c (moves_from_block, both segments at once, no branch)
+  // RandomBot draws: the first two accepted 3-bit fields of bits 0-29 of
+  // word b; the rare games whose word b holds fewer take word c and then the
+  // POLICY stream in a separate unlikely block (moves_from_block), so the
+  // common decode is 32-bit and loop-free
   const int need = (pol1 == ORX_POLICY_RANDOM ? 1 : 0) + (pol2 == ORX_POLICY_RANDOM ? 1 : 0);
   int32_t r0 = ORX_MOVE_STAY, r1 = ORX_MOVE_STAY;
-  bool need_fb = false;
   if (need > 0) {  // uniform: skipped for StaircaseBot pairs (C5)
-    const uint64_t w = (uint64_t)(tb.b & 0x3FFFFFFFu) | ((uint64_t)(tb.c & 0x3FFFFFFFu) << 30);
-    const uint64_t acc = (uint64_t)accepted3(tb.b) | ((uint64_t)accepted3(tb.c) << 30);
-    const uint64_t acc2 = acc & (acc - 1u);
-    r0 = (int32_t)((w >> __builtin_ctzll(acc | (1ull << 63))) & 7u) + 1;
-    r1 = (int32_t)((w >> __builtin_ctzll(acc2 | (1ull << 63))) & 7u) + 1;
-    need_fb = need > (acc == 0 ? 0 : acc2 == 0 ? 1 : 2);
+    const uint32_t acc = accepted3(tb.b);
+    const uint32_t acc2 = acc & (acc - 1u);
+    r0 = (int32_t)((tb.b >> (ffbl(acc) & 31u)) & 7u) + 1;
+    r1 = (int32_t)((tb.b >> (ffbl(acc2) & 31u)) & 7u) + 1;
+    if (ORX_UNLIKELY((need > 1 ? acc2 : acc) == 0u)) {
+      bool err = false;  // (the rollout, like orx_policy's fused form, ignores exhaustion)
+      moves_from_block(tb, need, key, game, ep, tick, r0, r1, err);
+    }
   }
   assign_moves(pol1, pol2, r0, r1, p1, p2, a1, a2);
   p1.move = a1;
   p2.move = a2;
   const bool in_progress = status == ORX_IN_PROGRESS;
 
-  // effective targets: the player's own cell when staying or blocked
+  // effective targets: the player's own cell when staying or blocked.  Empty
+  // dungeons: a move changes one coordinate by one, so a blocked target is
+  // the border and clamping it to the interior gives back the own cell
   calc_pos(p1.x, p1.y, p1.move, p1.tx, p1.ty);
   calc_pos(p2.x, p2.y, p2.move, p2.tx, p2.ty);
-  const bool b1 = blocked<GRID>(c, p1.lay, p1.tx, p1.ty);
-  const bool b2 = blocked<GRID>(c, p2.lay, p2.tx, p2.ty);
-  const int32_t t1x = b1 ? p1.x : p1.tx, t1y = b1 ? p1.y : p1.ty;
-  const int32_t t2x = b2 ? p2.x : p2.tx, t2y = b2 ? p2.y : p2.ty;
+  int32_t t1x, t1y, t2x, t2y;
+  if constexpr (GRID) {
+    const bool b1 = blocked<GRID>(c, p1.lay, p1.tx, p1.ty);
+    const bool b2 = blocked<GRID>(c, p2.lay, p2.tx, p2.ty);
+    t1x = b1 ? p1.x : p1.tx; t1y = b1 ? p1.y : p1.ty;
+    t2x = b2 ? p2.x : p2.tx; t2y = b2 ? p2.y : p2.ty;
+  } else {
+    t1x = med3_i32(p1.tx, 1, c.W - 2); t1y = med3_i32(p1.ty, 1, c.H - 2);
+    t2x = med3_i32(p2.tx, 1, c.W - 2); t2y = med3_i32(p2.ty, 1, c.H - 2);
+  }
   // meet: same depth and (target 1 == cell 2 or target 2 == cell 1 or
   // target 1 == target 2), as one zero test over xor differences
   const uint32_t e12 = (uint32_t)(t1x ^ p2.x) | (uint32_t)(t1y ^ p2.y);
@@ -1372,36 +1404,45 @@ __device__ __forceinline__ void rollout_tick(const Cfg& c, const orx_state_t& st
   const bool hit1 = NCAP > 0 && ((p1.d == c.d1) & n1);
   const bool hit2 = NCAP > 0 && ((p2.d == c.d1) & n2);
   const bool st1 = stair_tile<GRID>(c, p1, t1x, t1y), st2 = stair_tile<GRID>(c, p2, t2x, t2y);
-  const bool shf_reject = (~(pk_shf >> 1) & 0x55555555u) == 0u;
-  const bool desc_meet = (st1 & (p2.d == p1.d + 1)) | (st2 & (p1.d == p2.d + 1));
-  const bool full = need_fb | (meet & (st1 | st2)) | (st1 & st2) | shf_reject |
-                    ((c.ext & ~ORX_EXT_SEPARATION_DAMAGE) != 0);
-  const bool lean = meet & !full;
-  // base: the in-progress games whose tick the common path takes (a hit, a
-  // descend or a meet adjusted below); f: those whose moves resolve freely.
-  // Laundered, so the compiler cannot rebuild an if/else around the rare block.
-  uint32_t bv = (in_progress & !full) ? 1u : 0u, fv = (in_progress & !full & !lean) ? 1u : 0u;
-  asm volatile("" : "+v"(bv), "+v"(fv));
-  const bool base = bv != 0u, f = fv != 0u;
-  const bool s1 = f & !hit1 & !st1, s2 = f & !hit2 & !st2;
-  const int32_t x1o = p1.x, y1o = p1.y, x2o = p2.x, y2o = p2.y;  // for a descend-meet
-  p1.x = s1 ? t1x : p1.x;
-  p1.y = s1 ? t1y : p1.y;
-  p2.x = s2 ? t2x : p2.x;
-  p2.y = s2 ? t2y : p2.y;
-  const int32_t t0 = tick, ft = tick + 1;
+  // all sixteen 2-bit shuffle fields rejected (high bits all set)
+  const bool shf_reject = (pk_shf | 0x55555555u) == 0xFFFFFFFFu;
+  const bool ext_ordered = (c.ext & ~ORX_EXT_SEPARATION_DAMAGE) != 0;  // uniform
+  // The rare games: finished, or a meet, an NPC hit, a staircase, an
+  // all-reject shuffle word, an extension that needs the literal sequence.
+  // Only this union is formed here; the rare block re-derives its parts
+  // (from laundered inputs, so they are not kept live across the common
+  // path as 0/1 values).
+  const bool rare = !in_progress | meet | hit1 | hit2 | st1 | st2 | shf_reject | ext_ordered;
+  const int32_t ft = tick + 1;
   const bool end = c.max_ticks && ft >= c.max_ticks;
-  tick = base ? ft : tick;
-  status = base ? (end ? ORX_TIE : ORX_IN_PROGRESS) : status;
-  dl.eps += (base & end) ? 1 : 0;
 
-  if (ORX_UNLIKELY(!base | hit1 | hit2 | st1 | st2 | lean)) {
+  // The rare block runs first, from the pre-tick state, and finishes its
+  // games in place; the common tick's update follows as selects over the same
+  // registers (applied after the block, the old and new values of a field
+  // are never live together, so the loop carries no register copies).
+  if (ORX_UNLIKELY(rare)) {
 #ifdef ORX_STAMPS
     ORX_COUNT(dl.n_rare);
 #endif
+    launder(t1x, t1y, t2x, t2y);
+    launder(p1.x, p1.y, p2.x, p2.y);
+    launder(p1.d, p2.d, p1.sx, p1.sy);
+    launder(p2.sx, p2.sy, status, tick);
+    const bool in_progress = status == ORX_IN_PROGRESS;
+    const bool meet = ((uint32_t)(p1.d ^ p2.d) |
+                       min((uint32_t)(t1x ^ p2.x) | (uint32_t)(t1y ^ p2.y),
+                           min((uint32_t)(t2x ^ p1.x) | (uint32_t)(t2y ^ p1.y),
+                               (uint32_t)(t1x ^ t2x) | (uint32_t)(t1y ^ t2y)))) == 0u;
+    const uint32_t k1 = (uint32_t)t1x | ((uint32_t)t1y << 8);
+    const uint32_t k2 = (uint32_t)t2x | ((uint32_t)t2y << 8);
+    const bool hit1 = NCAP > 0 && (p1.d == c.d1) && npc.any(k1);
+    const bool hit2 = NCAP > 0 && (p2.d == c.d1) && npc.any(k2);
+    const bool st1 = stair_tile<GRID>(c, p1, t1x, t1y), st2 = stair_tile<GRID>(c, p2, t2x, t2y);
+    const bool shf_reject = (pk_shf | 0x55555555u) == 0xFFFFFFFFu;
+    const bool full = (meet & (st1 | st2)) | (st1 & st2) | shf_reject | ext_ordered;
+    const int32_t t0 = tick, ft = tick + 1;
+    const bool end = c.max_ticks && ft >= c.max_ticks;
     if (!in_progress) {
-      if (need_fb)  // the recorded actions: draws beyond the tick block
-        policy_pair(key, game, ep, t0, pol1, pol2, tb, p1, p2, a1, a2);
       if (c.autoreset) {  // the next episode (worldgen.py:77-87, 124-135)
         ep += 1;
         setup_game<NCAP, GRID>(c, key, game, ep, p1, p2, npc, tick, status);
@@ -1412,25 +1453,33 @@ __device__ __forceinline__ void rollout_tick(const Cfg& c, const orx_state_t& st
         restarted = true;
         sep = -1;
       }
-    } else if (!base) {  // the ordered tick
+    } else if (full) {  // the ordered tick
 #ifdef ORX_STAMPS
       ORX_COUNT(dl.n_ordered);
 #endif
-      if (need_fb) {  // draws beyond the tick block: word c, then the POLICY stream
-        policy_pair(key, game, ep, t0, pol1, pol2, tb, p1, p2, a1, a2);
-        p1.move = a1;
-        p2.move = a2;
-      }
       bool err = false;
       const bool p1_first = first_from_packed(pk_shf, key, game, ep, t0, err);
       Events<false> ev{nullptr, 0};
       tick_game<NCAP, false, GRID>(c, key, game, ep, p1_first, p1, p2, npc, hp, tick, status,
                                    err, dl, ev, sep);
     } else {
-      if (f & (st1 | st2)) {  // one player descends
+      // the common path's rules, then the one-sided events: a player that
+      // hits an NPC, descends or meets the other does not move freely
+      const bool lean = meet;
+      const bool s1 = !lean & !hit1 & !st1, s2 = !lean & !hit2 & !st2;
+      const int32_t x1o = p1.x, y1o = p1.y, x2o = p2.x, y2o = p2.y;  // for a descend-meet
+      p1.x = s1 ? t1x : p1.x;
+      p1.y = s1 ? t1y : p1.y;
+      p2.x = s2 ? t2x : p2.x;
+      p2.y = s2 ? t2y : p2.y;
+      tick = ft;
+      status = end ? ORX_TIE : ORX_IN_PROGRESS;
+      dl.eps += end ? 1 : 0;
+      if (!lean & (st1 | st2)) {  // one player descends
 #ifdef ORX_STAMPS
         ORX_COUNT(dl.n_desc);
 #endif
+        const bool desc_meet = (st1 & (p2.d == p1.d + 1)) | (st2 & (p1.d == p2.d + 1));
         PhiloxSrc src{key, game, ep};
         auto spawn = src.spawn(t0);
         Events<false> ev{nullptr, 0};
@@ -1499,7 +1548,20 @@ __device__ __forceinline__ void rollout_tick(const Cfg& c, const orx_state_t& st
       }
     }
   }
+  // the common tick: both players move to their effective targets
+  p1.x = rare ? p1.x : t1x;
+  p1.y = rare ? p1.y : t1y;
+  p2.x = rare ? p2.x : t2x;
+  p2.y = rare ? p2.y : t2y;
+  dl.eps += (!rare & end) ? 1 : 0;
+  status = rare ? status : (end ? ORX_TIE : ORX_IN_PROGRESS);
+  tick = rare ? tick : ft;
+  const int32_t t0 = ft - 1;  // the pre-tick tick of every game
   if (c.ext & ORX_EXT_SEPARATION_DAMAGE) {  // build extension (readme.md:46-47), C5's ladder
+    // base: the in-progress games whose tick took the common path's rules
+    // (free moves, or a hit, a descend or a meet in the rare block)
+    const bool base =
+        in_progress & !((meet & (st1 | st2)) | (st1 & st2) | shf_reject | ext_ordered);
     if (base) {
       if (p1.d != p2.d) {
         if (sep < 0) sep = t0;

@@ -327,3 +327,92 @@ class BatchedEngine:
     def episode_returns(self) -> torch.Tensor:
         """(ret_sum, ep_count) stacked as int32 [2, n_games] (device)."""
         return torch.stack([self.ret_sum, self.ep_count])
+
+
+class StreamShardedEngine:
+    """One GPU's batch as ``n_streams`` shards, each a BatchedEngine on its
+    own HIP stream (contiguous global game ids, ``parallel.shard``).
+
+    The fused rollout is HBM-write-bound inside its tick loop, so what a
+    launch loses is its ramp (state loads) and its tail (waves that took more
+    rare ticks finish last, with too few waves left to keep HBM busy).  Launches
+    on different streams run concurrently, so one shard's ramp and tail overlap
+    the other shards' steady state.  A game's trajectory depends on its
+    global id only (the Philox key), so the shards compute exactly what one
+    engine over the whole batch computes (tests/test_gpu_parity.py).  This is
+    the multi-GPU sharding of parallel.py applied within one device.
+    """
+
+    def __init__(self, cfg: EnvConfig, n_games: int, seed: int = 0, game_offset: int = 0,
+                 device: Optional[torch.device] = None, n_streams: int = 2):
+        from .parallel import shard
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        self.device = torch.device(device)
+        self.B = int(n_games)
+        n_streams = max(1, min(int(n_streams), self.B))
+        self.streams = [torch.cuda.Stream(device=self.device) for _ in range(n_streams)]
+        self.parts = []
+        cur = torch.cuda.current_stream(self.device)
+        for k, s in enumerate(self.streams):
+            off, cnt = shard(self.B, k, n_streams)
+            s.wait_stream(cur)
+            with torch.cuda.stream(s):
+                self.parts.append(BatchedEngine(cfg, cnt, seed=seed, game_offset=game_offset + off,
+                                                device=self.device))
+        for s in self.streams:
+            cur.wait_stream(s)
+
+    def trajectory_buffers(self, n_ticks: int):
+        """Per-shard obs int32 [n_ticks, 14, count] and act int8 [n_ticks, count, 2]."""
+        return ([torch.empty((n_ticks, len(OBS_FIELDS), e.B), dtype=torch.int32,
+                             device=self.device) for e in self.parts],
+                [torch.empty((n_ticks, e.B, 2), dtype=torch.int8, device=self.device)
+                 for e in self.parts])
+
+    def rollout_launcher(self, n_ticks: int, p1: int = Policy.Random, p2: int = Policy.Random,
+                         obs=None, act=None):
+        """A zero-argument callable launching every shard's rollout on its own
+        stream (``obs``/``act``: per-shard lists, or None).  Ordering against
+        the caller's stream is explicit: ``fork()`` before (the shards wait for
+        the caller's work so far), ``join()`` after (the caller waits for the
+        shards) -- a fork per launch would put a cross-queue barrier between
+        consecutive launches of a shard."""
+        obs = obs or [None] * len(self.parts)
+        act = act or [None] * len(self.parts)
+        go = []
+        for e, s, o, a in zip(self.parts, self.streams, obs, act):
+            with torch.cuda.stream(s):
+                go.append(e.rollout_launcher(n_ticks, p1, p2, obs=o, act=a))
+
+        def launch():
+            for g in go:
+                g()
+        return launch
+
+    def fork(self) -> None:
+        """Every shard's stream waits for the caller's current stream's work so far."""
+        cur = torch.cuda.current_stream(self.device)
+        for s in self.streams:
+            s.wait_stream(cur)
+
+    def join(self) -> None:
+        """The caller's current stream waits for every shard's work so far."""
+        cur = torch.cuda.current_stream(self.device)
+        for s in self.streams:
+            cur.wait_stream(s)
+
+    def rollout_lanes(self) -> int:
+        return self.parts[0].rollout_lanes()
+
+    def episode_returns(self) -> torch.Tensor:
+        """(ret_sum, ep_count) int32 [2, n_games] in global id order (device)."""
+        self.join()
+        return torch.cat([e.episode_returns() for e in self.parts], dim=1)
+
+    def snapshot(self) -> dict:
+        """The whole batch's SoA state, shards concatenated along the game axis."""
+        self.join()
+        snaps = [e.snapshot() for e in self.parts]
+        return {k: np.concatenate([s[k] for s in snaps], axis=snaps[0][k].ndim - 1)
+                for k in snaps[0]}

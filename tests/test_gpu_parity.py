@@ -254,6 +254,35 @@ def test_rollout_games_per_wave_invariance(which, monkeypatch):
     assert ref[0]["ep_count"].sum() > 0
 
 
+@pytest.mark.parametrize("n_streams", [2, 3])
+def test_stream_shards_equal_one_engine(n_streams):
+    """StreamShardedEngine (the bench's per-stream shards) computes exactly
+    what one BatchedEngine over the whole batch does: state and trajectory."""
+    import torch
+    from optimax_rogue_amd import EnvConfig
+    from optimax_rogue_amd.engine import StreamShardedEngine
+    from optimax_rogue_amd.enums import OBS_FIELDS
+    cfg = dict(EnvConfig.c3().to_dict(), max_ticks=100)
+    B, T = 5001, 130
+    one = _engine(cfg, B, 3, 11)
+    obs = torch.zeros((T, len(OBS_FIELDS), B), dtype=torch.int32, device=one.device)
+    act = torch.zeros((T, B, 2), dtype=torch.int8, device=one.device)
+    one.rollout(T, 1, 1, obs=obs, act=act)
+    sh = StreamShardedEngine(EnvConfig.from_dict(cfg), B, seed=3, game_offset=11,
+                             device=one.device, n_streams=n_streams)
+    so, sa = sh.trajectory_buffers(T)
+    go = sh.rollout_launcher(T, 1, 1, obs=so, act=sa)
+    sh.fork()
+    go()
+    sh.join()
+    a, b = one.snapshot(), sh.snapshot()
+    for k in STATE_KEYS:
+        assert np.array_equal(a[k], b[k]), k
+    assert np.array_equal(obs.cpu().numpy(), torch.cat(so, dim=2).cpu().numpy())
+    assert np.array_equal(act.cpu().numpy(), torch.cat(sa, dim=1).cpu().numpy())
+    assert a["ep_count"].sum() >= B
+
+
 def test_rollout_equals_step_c3():
     """C3 shape (B=65536, 64x64, K=8): fused rollout == per-tick policy+step."""
     from optimax_rogue_amd import EnvConfig

@@ -8,7 +8,8 @@ command itself (tools/gpu_profile.sh):
 HBM bytes per launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024: FETCH_SIZE is
 doubled per MI355X_MICROARCH.md (gfx950 tallies 128-B read requests at 64 B).
 Only the dispatches of the headline kernel at the headline grid are averaged
-(bench.py launches that kernel at no other shape by default).  The entry is
+(bench.py launches that kernel at no other shape by default); a bench step is
+one dispatch per stream shard, so bytes per step = shards x the average.  The entry is
 stamped with the library's build id: bench.py uses it only for that build.
 """
 import collections
@@ -33,14 +34,15 @@ def load(d, counter):
     return {k: (sum(v) / len(v), len(v)) for k, v in agg.items()}
 
 
-def main(fetch_dir, write_dir, out_path=None, batch=65536, ticks=128):
+def main(fetch_dir, write_dir, out_path=None, batch=65536, ticks=128, streams=2):
     import bench
     from optimax_rogue_amd import _lib
     fe, wr = load(fetch_dir, "FETCH_SIZE"), load(write_dir, "WRITE_SIZE")
     K = 8
     kname = bench.rollout_kernel_name(batch, K)
-    lanes = _lib.load().orx_rollout_lanes(batch)
-    grid = -(-batch // (4 * lanes)) * 256        # 256-thread blocks of 4 waves
+    part = batch // streams                      # bench.py's stream shards (equal here)
+    lanes = _lib.load().orx_rollout_lanes(part)
+    grid = -(-part // (4 * lanes)) * 256         # 256-thread blocks of 4 waves
     out = {"_source": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over "
                       "`python3 bench.py --gpus 1 --steps 20 --warmup 5` (MI355X, ROCm 7.2), "
                       "written by tools/make_traffic.py. hbm_bytes = (2 * FETCH_SIZE + "
@@ -51,12 +53,14 @@ def main(fetch_dir, write_dir, out_path=None, batch=65536, ticks=128):
     if f is None or w is None:
         raise SystemExit(f"no dispatches of {kname} at grid {grid}: {sorted(fe)}")
     alg = bench.bytes_per_game("rollout", K, ticks) * batch
-    out["rollout"] = {"kernel": kname, "batch": batch, "ticks": ticks, "grid": grid,
-                      "games_per_wave": lanes, "dispatches": [f[1], w[1]],
-                      "fetch_kb": round(f[0], 1), "write_kb": round(w[0], 1),
-                      "hbm_bytes_per_launch": int((2 * f[0] + w[0]) * 1024),
-                      "algorithmic_bytes_per_launch": int(alg),
-                      "ratio": round((2 * f[0] + w[0]) * 1024 / alg, 4),
+    per_step = streams * (2 * f[0] + w[0]) * 1024
+    out["rollout"] = {"kernel": kname, "batch": batch, "ticks": ticks, "streams": streams,
+                      "grid": grid, "games_per_wave": lanes, "dispatches": [f[1], w[1]],
+                      "fetch_kb_per_dispatch": round(f[0], 1),
+                      "write_kb_per_dispatch": round(w[0], 1),
+                      "hbm_bytes_per_step": int(per_step),
+                      "algorithmic_bytes_per_step": int(alg),
+                      "ratio": round(per_step / alg, 4),
                       "build_id": _lib.build_id()}
     out_path = out_path or os.path.join(ROOT, "profiles", "traffic.json")
     json.dump(out, open(out_path, "w"), indent=1)
