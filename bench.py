@@ -77,9 +77,9 @@ def bytes_per_game(kernel: str, K: int, ticks: int = 1) -> int:
 
 def rollout_kernel_name(B: int, K: int) -> str:
     """The kernel orx_rollout launches for this workload: rollout_kernel with
-    the RandomBot + trajectory specialization (FAST=1), NPC capacity 0/8/16."""
+    the RandomBot + trajectory specialization (PM=1), NPC capacity 0/8/16."""
     ncap = 0 if K == 0 else 8 if K <= 8 else 16
-    return f"rollout_kernel<{ncap}, true, false>"
+    return f"rollout_kernel<{ncap}, 1, false>"
 
 
 def _cpu_model() -> str:

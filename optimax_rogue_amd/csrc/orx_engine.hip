@@ -44,6 +44,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <type_traits>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -189,6 +190,10 @@ struct Cfg {  // device copy of orx_cfg_t plus derived constants (all wave-unifo
   int32_t npc_hp, player_hp, player_dmg_net, autoreset;
   int32_t ext, sep_period;  // ORX_EXT_* build extensions (0 in FAST kernels)
   int32_t ih;        // H - 2 (interior column height)
+  // ceil(2^32 / d) for d = ih and d = H: n / d == umulhi(n, magic) for every
+  // n < 2^16 (error < n / 2^32 <= 1/d), so set only when the dividends
+  // (interior / grid cell indices) stay below 2^16; 0 = divide
+  uint32_t ih_magic, h_magic;
   NpBound ground;    // randint(n_ground), n_ground = (W-2)(H-2) - 1
   NpBound stair_x;   // randint(1, W-2)
   NpBound stair_y;   // randint(1, H-2)
@@ -404,14 +409,14 @@ __device__ __forceinline__ void ground_cell(const Cfg& c, uint32_t ch, int32_t l
                                             int32_t sy, int32_t& x, int32_t& y) {
   if constexpr (GRID) {
     const uint32_t flat = c.gground[(size_t)lay * (uint32_t)(c.W * c.H) + ch];
-    const uint32_t q = flat / (uint32_t)c.H;
+    const uint32_t q = c.h_magic ? __umulhi(flat, c.h_magic) : flat / (uint32_t)c.H;
     x = (int32_t)q;
     y = (int32_t)(flat - q * (uint32_t)c.H);
     return;
   }
   const uint32_t s_idx = (uint32_t)((sx - 1) * c.ih + (sy - 1));
   const uint32_t ci = ch + (ch >= s_idx ? 1u : 0u);
-  const uint32_t q = ci / (uint32_t)c.ih;
+  const uint32_t q = c.ih_magic ? __umulhi(ci, c.ih_magic) : ci / (uint32_t)c.ih;
   x = 1 + (int32_t)q;
   y = 1 + (int32_t)(ci - q * (uint32_t)c.ih);
 }
@@ -452,6 +457,26 @@ __device__ __forceinline__ void dungeon_draw(const Cfg& c, S& s, Key key, int32_
   if (n < 2) err = true;
   sx = 1 + v0;
   sy = 1 + v1;
+}
+
+// EmptyDungeonGenerator.spawn_dungeon from the first block of its keyed
+// stream: randint(1, W-2) takes the first accepted of words a, b, c and
+// randint(1, H-2) the first accepted word after it.  False when the block
+// holds no such pair (p ~ 1e-5 at 128x128) or a bound consumes no word
+// (W or H = 4); the caller then runs dungeon_draw, which reads the same words.
+__device__ __forceinline__ bool stair_from_block(const Cfg& c, const W4& w, int32_t& sx,
+                                                 int32_t& sy) {
+  const NpBound bx = c.stair_x, by = c.stair_y;
+  if (bx.rng == 0u || by.rng == 0u) return false;
+  const uint32_t x0 = w.a & bx.mask, x1 = w.b & bx.mask, x2 = w.c & bx.mask;
+  const uint32_t y1 = w.b & by.mask, y2 = w.c & by.mask, y3 = w.d & by.mask;
+  const bool ax0 = x0 <= bx.rng, ax1 = x1 <= bx.rng, ax2 = x2 <= bx.rng;
+  const bool ay1 = y1 <= by.rng, ay2 = y2 <= by.rng, ay3 = y3 <= by.rng;
+  const uint32_t y_after1 = ay2 ? y2 : y3;               // y after x at word b
+  const uint32_t y_after0 = ay1 ? y1 : y_after1;         // y after x at word a
+  sx = 1 + (int32_t)(ax0 ? x0 : ax1 ? x1 : x2);
+  sy = 1 + (int32_t)(ax0 ? y_after0 : ax1 ? y_after1 : y3);
+  return ax0 ? (ay1 | ay2 | ay3) : ax1 ? (ay2 | ay3) : (ax2 & ay3);
 }
 
 // The keyed form: words from (episode, depth, generation).
@@ -678,7 +703,13 @@ __device__ __forceinline__ void descend(const Cfg& c, Key key, Src& src, Player&
     // keyed: regenerate (present or not); stock-seed: a present dungeon must
     // be in the ring (a gap beyond ORX_DSTORE stops the game), else draw it
     if (Src::kMt && present) err = true;
-    src.template dungeon<GRID>(c, nd, gen, sx, sy, lay, err);
+    bool drawn = false;
+    if constexpr (!Src::kMt && !GRID) {  // straight from the stream's first block
+      lay = -1;
+      drawn = stair_from_block(c, philox(src.game, src.ep, (uint32_t)nd, tag(PUR_DUNGEON, gen),
+                                         key), sx, sy);
+    }
+    if (!drawn) src.template dungeon<GRID>(c, nd, gen, sx, sy, lay, err);
   }
   src.remember(nd, sx, sy, lay);
   if (!present) {
@@ -689,6 +720,24 @@ __device__ __forceinline__ void descend(const Cfg& c, Key key, Src& src, Player&
   int32_t x = 0, y = 0;
   bool done = false;
   const NpBound gb = ground_bound<GRID>(c, lay);
+  if constexpr (std::is_same<S, Stream>::value && !GRID) {
+    // the common spawn: the first word of a fresh SPAWN stream accepted and
+    // the cell free; otherwise the loop below replays the stream from there
+    if (spawn.idx == 0u && gb.rng != 0u) {
+      const W4 w = philox(spawn.c0, spawn.c1, spawn.c2, spawn.c3, key);
+      const uint32_t v = w.a & gb.mask;
+      if (v <= gb.rng) {
+        ground_cell<GRID>(c, v, lay, sx, sy, x, y);
+        bool occ = other.d == nd && other.x == x && other.y == y;
+        if (npc_depth) occ = occ || npc.find(pack_xy(x, y)) >= 0;
+        done = !occ;
+        if (done) {  // the stream now stands after its first word
+          spawn.w = w;
+          spawn.idx = 1u;
+        }
+      }
+    }
+  }
   for (uint32_t t = 0; t < kWordCap && !done; ++t) {
     uint32_t v = 0;
     if (gb.rng != 0) {
@@ -1162,6 +1211,10 @@ __device__ __forceinline__ Cfg make_cfg(const orx_cfg_t& h, const orx_state_t& s
   c.ext = h.flags;
   c.sep_period = h.sep_period > 0 ? h.sep_period : 1;
   c.ih = h.height - 2;
+  c.ih_magic = (int64_t)(h.width - 2) * (h.height - 2) <= 65536
+                   ? (uint32_t)(0xFFFFFFFFu / (uint32_t)c.ih + 1u) : 0u;
+  c.h_magic = (int64_t)h.width * h.height <= 65536
+                  ? (uint32_t)(0xFFFFFFFFu / (uint32_t)h.height + 1u) : 0u;
   c.ground.set((h.width - 2) * (h.height - 2) - 1);
   c.stair_x.set(h.width - 3);
   c.stair_y.set(h.height - 3);
@@ -1351,14 +1404,16 @@ __device__ __forceinline__ void rollout_tick(const Cfg& c, const orx_state_t& st
                                              int32_t& tick, int32_t& status, Deltas& dl,
                                              int32_t& sep, bool& restarted, int32_t& a1,
                                              int32_t& a2) {
-  // one tick block: the bots' bits and the initiative bits (§4)
-  const W4 tb = tick_block(key, game, ep, tick);
-  const uint32_t pk_shf = tb.a;
+  // one tick block: the bots' bits and the initiative bits (§4).  Without a
+  // RandomBot the block's only reader is the initiative order, which matters
+  // only to rare games: the rare block draws it then (C5's StaircaseBots).
+  const int need = (pol1 == ORX_POLICY_RANDOM ? 1 : 0) + (pol2 == ORX_POLICY_RANDOM ? 1 : 0);
+  W4 tb = {0u, 0u, 0u, 0u};
+  if (need > 0) tb = tick_block(key, game, ep, tick);  // uniform
   // RandomBot draws: the first two accepted 3-bit fields of bits 0-29 of
   // word b; the rare games whose word b holds fewer take word c and then the
   // POLICY stream in a separate unlikely block (moves_from_block), so the
   // common decode is 32-bit and loop-free
-  const int need = (pol1 == ORX_POLICY_RANDOM ? 1 : 0) + (pol2 == ORX_POLICY_RANDOM ? 1 : 0);
   int32_t r0 = ORX_MOVE_STAY, r1 = ORX_MOVE_STAY;
   if (need > 0) {  // uniform: skipped for StaircaseBot pairs (C5)
     const uint32_t acc = accepted3(tb.b);
@@ -1404,15 +1459,16 @@ __device__ __forceinline__ void rollout_tick(const Cfg& c, const orx_state_t& st
   const bool hit1 = NCAP > 0 && ((p1.d == c.d1) & n1);
   const bool hit2 = NCAP > 0 && ((p2.d == c.d1) & n2);
   const bool st1 = stair_tile<GRID>(c, p1, t1x, t1y), st2 = stair_tile<GRID>(c, p2, t2x, t2y);
-  // all sixteen 2-bit shuffle fields rejected (high bits all set)
-  const bool shf_reject = (pk_shf | 0x55555555u) == 0xFFFFFFFFu;
   const bool ext_ordered = (c.ext & ~ORX_EXT_SEPARATION_DAMAGE) != 0;  // uniform
   // The rare games: finished, or a meet, an NPC hit, a staircase, an
-  // all-reject shuffle word, an extension that needs the literal sequence.
-  // Only this union is formed here; the rare block re-derives its parts
-  // (from laundered inputs, so they are not kept live across the common
-  // path as 0/1 values).
-  const bool rare = !in_progress | meet | hit1 | hit2 | st1 | st2 | shf_reject | ext_ordered;
+  // extension that needs the literal sequence.  Only this union is formed
+  // here; the rare block re-derives its parts (from laundered inputs, so they
+  // are not kept live across the common path as 0/1 values).  The initiative
+  // order is unobservable in a common tick, so its draw -- and the SHUFFLE
+  // stream fallback of an all-reject word, whose 4,096-word cap is the only
+  // way it could matter there (p < 2^-4000) -- is consulted by the rare
+  // block only, where the order is used.
+  const bool rare = !in_progress | meet | hit1 | hit2 | st1 | st2 | ext_ordered;
   const int32_t ft = tick + 1;
   const bool end = c.max_ticks && ft >= c.max_ticks;
 
@@ -1420,6 +1476,7 @@ __device__ __forceinline__ void rollout_tick(const Cfg& c, const orx_state_t& st
   // games in place; the common tick's update follows as selects over the same
   // registers (applied after the block, the old and new values of a field
   // are never live together, so the loop carries no register copies).
+  bool took_ordered = false;  // the ordered tick ran (it applies its own extensions)
   if (ORX_UNLIKELY(rare)) {
 #ifdef ORX_STAMPS
     ORX_COUNT(dl.n_rare);
@@ -1438,8 +1495,18 @@ __device__ __forceinline__ void rollout_tick(const Cfg& c, const orx_state_t& st
     const bool hit1 = NCAP > 0 && (p1.d == c.d1) && npc.any(k1);
     const bool hit2 = NCAP > 0 && (p2.d == c.d1) && npc.any(k2);
     const bool st1 = stair_tile<GRID>(c, p1, t1x, t1y), st2 = stair_tile<GRID>(c, p2, t2x, t2y);
-    const bool shf_reject = (pk_shf | 0x55555555u) == 0xFFFFFFFFu;
-    const bool full = (meet & (st1 | st2)) | (st1 & st2) | shf_reject | ext_ordered;
+    const bool full0 = (meet & (st1 | st2)) | (st1 & st2) | ext_ordered;
+    const bool desc_meet = (st1 & (p2.d == p1.d + 1)) | (st2 & (p1.d == p2.d + 1));
+    // the games that use the initiative order: the ordered tick, a meet, a
+    // descend into the other's depth
+    const bool ordered_use = in_progress & (full0 | meet | desc_meet);
+    uint32_t pk_shf = tb.a;
+    if (need == 0 && ordered_use) pk_shf = tick_block(key, game, ep, tick).a;
+    // all sixteen 2-bit shuffle fields rejected (high bits all set): the
+    // SHUFFLE stream fallback and its cap, in the ordered tick
+    const bool shf_reject = ordered_use & ((pk_shf | 0x55555555u) == 0xFFFFFFFFu);
+    const bool full = full0 | shf_reject;
+    took_ordered = in_progress & full;
     const int32_t t0 = tick, ft = tick + 1;
     const bool end = c.max_ticks && ft >= c.max_ticks;
     if (!in_progress) {
@@ -1479,7 +1546,6 @@ __device__ __forceinline__ void rollout_tick(const Cfg& c, const orx_state_t& st
 #ifdef ORX_STAMPS
         ORX_COUNT(dl.n_desc);
 #endif
-        const bool desc_meet = (st1 & (p2.d == p1.d + 1)) | (st2 & (p1.d == p2.d + 1));
         PhiloxSrc src{key, game, ep};
         auto spawn = src.spawn(t0);
         Events<false> ev{nullptr, 0};
@@ -1560,8 +1626,7 @@ __device__ __forceinline__ void rollout_tick(const Cfg& c, const orx_state_t& st
   if (c.ext & ORX_EXT_SEPARATION_DAMAGE) {  // build extension (readme.md:46-47), C5's ladder
     // base: the in-progress games whose tick took the common path's rules
     // (free moves, or a hit, a descend or a meet in the rare block)
-    const bool base =
-        in_progress & !((meet & (st1 | st2)) | (st1 & st2) | shf_reject | ext_ordered);
+    const bool base = in_progress & !took_ordered;
     if (base) {
       if (p1.d != p2.d) {
         if (sep < 0) sep = t0;
@@ -1643,17 +1708,23 @@ struct TrajWriter {
   }
 };
 
-// FAST: both players are RandomBots and obs/act are both given (compile-time,
-// the common case: no per-tick uniform branches on policy codes or pointers).
-template <int NCAP, bool FAST, bool GRID>
+// PM (policy mode, compile-time): 0 generic; 1 both players RandomBot, obs
+// and act given, no extension flags (the headline C3/C2 form); 2 both
+// StaircaseBot, obs and act given, at most separation damage (C5).  The
+// specialized forms carry no per-tick uniform branches on policy codes or
+// pointers and write the trajectory with buffer stores.
+template <int NCAP, int PM, bool GRID>
 __global__ void __launch_bounds__(kRolloutBlock) rollout_kernel(orx_cfg_t hc, orx_state_t st,
                                                                 int32_t pol1_,
                                                       int32_t pol2_, int32_t n_ticks,
                                                       int32_t* __restrict__ obs,
                                                       int8_t* __restrict__ act, uint32_t B,
                                                       Key key, uint32_t off, uint32_t lanes) {
-  const int32_t pol1 = FAST ? (int32_t)ORX_POLICY_RANDOM : pol1_;
-  const int32_t pol2 = FAST ? (int32_t)ORX_POLICY_RANDOM : pol2_;
+  constexpr bool kTraj = PM != 0;
+  const int32_t pol1 = PM == 1 ? (int32_t)ORX_POLICY_RANDOM
+                               : PM == 2 ? (int32_t)ORX_POLICY_STAIRCASE : pol1_;
+  const int32_t pol2 = PM == 1 ? (int32_t)ORX_POLICY_RANDOM
+                               : PM == 2 ? (int32_t)ORX_POLICY_STAIRCASE : pol2_;
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (lanes < 64u) {  // uniform: lanes >= `lanes` of every wave idle
     if ((threadIdx.x & 63u) >= lanes) return;
@@ -1661,7 +1732,8 @@ __global__ void __launch_bounds__(kRolloutBlock) rollout_kernel(orx_cfg_t hc, or
   }
   if (i >= B) return;
   Cfg c = make_cfg(hc, st);
-  if (FAST) c.ext = 0;  // FAST launches require flags == 0
+  if (PM == 1) c.ext = 0;                           // launched only with flags == 0
+  if (PM == 2) c.ext &= ORX_EXT_SEPARATION_DAMAGE;  // launched only with flags <= that
   const uint32_t game = off + i;
   ORX_STAMP(0);
   Player p1, p2;
@@ -1676,7 +1748,7 @@ __global__ void __launch_bounds__(kRolloutBlock) rollout_kernel(orx_cfg_t hc, or
   Deltas dl = {0, 0, 0, 0, 0, 0};
   int32_t sep = (c.ext & ORX_EXT_SEPARATION_DAMAGE) ? st.sep_start[i] : -1;
   bool restarted = false;
-  TrajWriter<FAST> traj(obs, act, B, i);
+  TrajWriter<kTraj> traj(obs, act, B, i);
 #ifdef ORX_STAMPS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
@@ -2297,19 +2369,24 @@ int orx_rollout(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p1, 
 #undef ORX_ROLLOUT
     return launch_status("orx_rollout");
   }
-  const bool rr = !grid && cfg->flags == 0 && policy_p1 == ORX_POLICY_RANDOM &&
-                  policy_p2 == ORX_POLICY_RANDOM && obs && act &&
-                  (uint64_t)B * ORX_OBS_FIELDS * 4u < (1ull << 31);
+  const bool traj_fast = !grid && obs && act && (uint64_t)B * ORX_OBS_FIELDS * 4u < (1ull << 31);
+  const int pm = !traj_fast ? 0
+                 : (cfg->flags == 0 && policy_p1 == ORX_POLICY_RANDOM &&
+                    policy_p2 == ORX_POLICY_RANDOM) ? 1
+                 : ((cfg->flags & ~ORX_EXT_SEPARATION_DAMAGE) == 0 &&
+                    policy_p1 == ORX_POLICY_STAIRCASE && policy_p2 == ORX_POLICY_STAIRCASE) ? 2
+                 : 0;
   const uint32_t lanes = rollout_lanes(B);
   const uint32_t per_block = (uint32_t)kRolloutBlock / 64u * lanes;
-#define ORX_ROLLOUT(N, R, G)                                                                    \
-  if (nc == N && rr == R && grid == G)                                                          \
-    hipLaunchKernelGGL((rollout_kernel<N, R, G>), dim3((B + per_block - 1) / per_block),        \
+#define ORX_ROLLOUT(N, P, G)                                                                    \
+  if (nc == N && pm == P && grid == G)                                                          \
+    hipLaunchKernelGGL((rollout_kernel<N, P, G>), dim3((B + per_block - 1) / per_block),        \
                        dim3(kRolloutBlock), 0, s, *cfg, *st,                                    \
                        policy_p1, policy_p2, n_ticks, obs, act, B, k, off, lanes);
-  ORX_ROLLOUT(0, false, false) ORX_ROLLOUT(0, true, false) ORX_ROLLOUT(8, false, false)
-  ORX_ROLLOUT(8, true, false) ORX_ROLLOUT(16, false, false) ORX_ROLLOUT(16, true, false)
-  ORX_ROLLOUT(0, false, true) ORX_ROLLOUT(8, false, true) ORX_ROLLOUT(16, false, true)
+  ORX_ROLLOUT(0, 0, false) ORX_ROLLOUT(0, 1, false) ORX_ROLLOUT(0, 2, false)
+  ORX_ROLLOUT(8, 0, false) ORX_ROLLOUT(8, 1, false) ORX_ROLLOUT(8, 2, false)
+  ORX_ROLLOUT(16, 0, false) ORX_ROLLOUT(16, 1, false) ORX_ROLLOUT(16, 2, false)
+  ORX_ROLLOUT(0, 0, true) ORX_ROLLOUT(8, 0, true) ORX_ROLLOUT(16, 0, true)
 #undef ORX_ROLLOUT
   return launch_status("orx_rollout");
 }
