@@ -262,6 +262,14 @@ def extras(torch, cfg, dev, B_cfg, K, large_rollout=False):
                 "us_per_launch": us * 1e6, "env_steps_per_s": games * T / us}
 
     out["c2"] = dict(rollout_rate(EnvConfig.c2(), 4096, 1), policy="2x RandomBot", grid="32x32")
+    # the explicit-grid generator (dungeon bank): C3's shape on 16 random
+    # 64x64 layouts, tiles staged in LDS by the rollout
+    from optimax_rogue_amd import DungeonBank
+    bank = DungeonBank.random(64, 64, 16, seed=7)
+    out["bank"] = dict(rollout_rate(EnvConfig(width=64, height=64, n_npcs=8, layouts=bank.layouts),
+                                    65536, 1),
+                       policy="2x RandomBot", grid="64x64, 16 layouts (15% walls)",
+                       note="tiles staged in LDS (64 KiB)")
     c5 = {}
     for flag in (0, EXT_SEPARATION_DAMAGE):
         c = EnvConfig.c5()

@@ -203,7 +203,15 @@ struct Cfg {  // device copy of orx_cfg_t plus derived constants (all wave-unifo
   const uint8_t* tiles;
   const uint16_t* gground;
   const int32_t* gmeta;
+  bool lds_tiles;    // the bank's tiles are staged in orx_lds_tiles (rollout)
 };
+
+// The dungeon bank's tiles in LDS (the rollout stages them once per block
+// when they fit, kMaxLdsTiles; every tile test of the tick then reads LDS
+// instead of waiting out an L2 round trip -- at one wave per SIMD nothing
+// hides that latency).
+extern __shared__ uint8_t orx_lds_tiles[];
+constexpr uint32_t kMaxLdsTiles = 64 * 1024;
 
 struct Deltas {  // counter / return increments, flushed once per launch
   int32_t combat, descend, dungeon, npc_death, ret, eps;
@@ -364,7 +372,8 @@ __device__ __forceinline__ void calc_pos(int32_t x, int32_t y, int32_t m, int32_
 
 // Dungeon.tiles[x, y] of bank layout `lay` (x, y inside the grid).
 __device__ __forceinline__ uint32_t bank_tile(const Cfg& c, int32_t lay, int32_t x, int32_t y) {
-  return c.tiles[(size_t)lay * (uint32_t)(c.W * c.H) + (uint32_t)(x * c.H + y)];
+  const uint32_t idx = (uint32_t)lay * (uint32_t)(c.W * c.H) + (uint32_t)(x * c.H + y);
+  return c.lds_tiles ? orx_lds_tiles[idx] : c.tiles[idx];
 }
 
 // Dungeon.is_blocked (world.py:41-46).  GRID = dungeon bank: outside the grid
@@ -1223,6 +1232,7 @@ __device__ __forceinline__ Cfg make_cfg(const orx_cfg_t& h, const orx_state_t& s
   c.tiles = st.bank_tiles;
   c.gground = st.bank_ground;
   c.gmeta = st.bank_meta;
+  c.lds_tiles = false;
   return c;
 }
 
@@ -1436,9 +1446,17 @@ __device__ __forceinline__ void rollout_tick(const Cfg& c, const orx_state_t& st
   calc_pos(p1.x, p1.y, p1.move, p1.tx, p1.ty);
   calc_pos(p2.x, p2.y, p2.move, p2.tx, p2.ty);
   int32_t t1x, t1y, t2x, t2y;
+  bool g_st1 = false, g_st2 = false;  // bank: the target tile is a staircase
   if constexpr (GRID) {
-    const bool b1 = blocked<GRID>(c, p1.lay, p1.tx, p1.ty);
-    const bool b2 = blocked<GRID>(c, p2.lay, p2.tx, p2.ty);
+    // one tile read per player: a Wall blocks, a staircase descends (a
+    // blocked player's own cell is never a staircase)
+    const bool in1 = (uint32_t)p1.tx < (uint32_t)c.W && (uint32_t)p1.ty < (uint32_t)c.H;
+    const bool in2 = (uint32_t)p2.tx < (uint32_t)c.W && (uint32_t)p2.ty < (uint32_t)c.H;
+    const uint32_t tile1 = bank_tile(c, p1.lay, in1 ? p1.tx : p1.x, in1 ? p1.ty : p1.y);
+    const uint32_t tile2 = bank_tile(c, p2.lay, in2 ? p2.tx : p2.x, in2 ? p2.ty : p2.y);
+    const bool b1 = !in1 || tile1 == ORX_TILE_WALL, b2 = !in2 || tile2 == ORX_TILE_WALL;
+    g_st1 = !b1 && tile1 == ORX_TILE_STAIRCASE_DOWN;
+    g_st2 = !b2 && tile2 == ORX_TILE_STAIRCASE_DOWN;
     t1x = b1 ? p1.x : p1.tx; t1y = b1 ? p1.y : p1.ty;
     t2x = b2 ? p2.x : p2.tx; t2y = b2 ? p2.y : p2.ty;
   } else {
@@ -1458,7 +1476,8 @@ __device__ __forceinline__ void rollout_tick(const Cfg& c, const orx_state_t& st
   npc_any2(npc, k1, k2, n1, n2);
   const bool hit1 = NCAP > 0 && ((p1.d == c.d1) & n1);
   const bool hit2 = NCAP > 0 && ((p2.d == c.d1) & n2);
-  const bool st1 = stair_tile<GRID>(c, p1, t1x, t1y), st2 = stair_tile<GRID>(c, p2, t2x, t2y);
+  const bool st1 = GRID ? g_st1 : stair_tile<GRID>(c, p1, t1x, t1y);
+  const bool st2 = GRID ? g_st2 : stair_tile<GRID>(c, p2, t2x, t2y);
   const bool ext_ordered = (c.ext & ~ORX_EXT_SEPARATION_DAMAGE) != 0;  // uniform
   // The rare games: finished, or a meet, an NPC hit, a staircase, an
   // extension that needs the literal sequence.  Only this union is formed
@@ -1719,12 +1738,31 @@ __global__ void __launch_bounds__(kRolloutBlock) rollout_kernel(orx_cfg_t hc, or
                                                       int32_t pol2_, int32_t n_ticks,
                                                       int32_t* __restrict__ obs,
                                                       int8_t* __restrict__ act, uint32_t B,
-                                                      Key key, uint32_t off, uint32_t lanes) {
+                                                      Key key, uint32_t off, uint32_t lanes,
+                                                      uint32_t lds_n) {
   constexpr bool kTraj = PM != 0;
   const int32_t pol1 = PM == 1 ? (int32_t)ORX_POLICY_RANDOM
                                : PM == 2 ? (int32_t)ORX_POLICY_STAIRCASE : pol1_;
   const int32_t pol2 = PM == 1 ? (int32_t)ORX_POLICY_RANDOM
                                : PM == 2 ? (int32_t)ORX_POLICY_STAIRCASE : pol2_;
+  bool lds_tiles = false;
+  if constexpr (GRID) {  // stage the bank's tiles in LDS (the whole block, before any exit)
+    const uint32_t n = lds_n;  // the bank's bytes, or 0: not staged (too large, or disabled)
+    if (n > 0u) {
+      const uint8_t* src = st.bank_tiles;
+      for (uint32_t k = threadIdx.x * 4u; k < n; k += blockDim.x * 4u) {
+        if (k + 4u <= n) {
+          uint32_t v;
+          __builtin_memcpy(&v, src + k, 4);
+          __builtin_memcpy(orx_lds_tiles + k, &v, 4);
+        } else {
+          for (uint32_t j = k; j < n; ++j) orx_lds_tiles[j] = src[j];
+        }
+      }
+      __syncthreads();
+      lds_tiles = true;
+    }
+  }
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (lanes < 64u) {  // uniform: lanes >= `lanes` of every wave idle
     if ((threadIdx.x & 63u) >= lanes) return;
@@ -1732,6 +1770,7 @@ __global__ void __launch_bounds__(kRolloutBlock) rollout_kernel(orx_cfg_t hc, or
   }
   if (i >= B) return;
   Cfg c = make_cfg(hc, st);
+  c.lds_tiles = lds_tiles;
   if (PM == 1) c.ext = 0;                           // launched only with flags == 0
   if (PM == 2) c.ext &= ORX_EXT_SEPARATION_DAMAGE;  // launched only with flags <= that
   const uint32_t game = off + i;
@@ -2355,8 +2394,7 @@ int orx_rollout(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p1, 
   const uint32_t B = (uint32_t)n_games, off = (uint32_t)game_offset;
   const hipStream_t s = (hipStream_t)stream;
   const Key k = make_key(seed);
-  // the buffer-addressed fast path needs one tick's obs rows below 2 GiB; a
-  // dungeon bank runs the generic plain kernel (tile lookups)
+  // the buffer-addressed trajectory forms need one tick's obs rows below 2 GiB
   const bool grid = cfg->n_layouts > 0;
   const int nc = ncap_for(cfg->n_npcs);
   if (cfg->rng == ORX_RNG_MT19937) {
@@ -2369,7 +2407,7 @@ int orx_rollout(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p1, 
 #undef ORX_ROLLOUT
     return launch_status("orx_rollout");
   }
-  const bool traj_fast = !grid && obs && act && (uint64_t)B * ORX_OBS_FIELDS * 4u < (1ull << 31);
+  const bool traj_fast = obs && act && (uint64_t)B * ORX_OBS_FIELDS * 4u < (1ull << 31);
   const int pm = !traj_fast ? 0
                  : (cfg->flags == 0 && policy_p1 == ORX_POLICY_RANDOM &&
                     policy_p2 == ORX_POLICY_RANDOM) ? 1
@@ -2378,15 +2416,22 @@ int orx_rollout(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p1, 
                  : 0;
   const uint32_t lanes = rollout_lanes(B);
   const uint32_t per_block = (uint32_t)kRolloutBlock / 64u * lanes;
+  // dynamic LDS: the bank's tiles when they fit (rollout_kernel stages them)
+  const uint64_t tiles = grid ? (uint64_t)cfg->n_layouts * (uint64_t)(cfg->width * cfg->height) : 0;
+  const bool use_lds = tiles && tiles <= kMaxLdsTiles && !getenv("ORX_NO_LDS_TILES");
+  const uint32_t lds_n = use_lds ? (uint32_t)tiles : 0u;
+  const uint32_t lds = use_lds ? (uint32_t)((tiles + 15u) & ~15ull) : 0u;
 #define ORX_ROLLOUT(N, P, G)                                                                    \
   if (nc == N && pm == P && grid == G)                                                          \
     hipLaunchKernelGGL((rollout_kernel<N, P, G>), dim3((B + per_block - 1) / per_block),        \
-                       dim3(kRolloutBlock), 0, s, *cfg, *st,                                    \
-                       policy_p1, policy_p2, n_ticks, obs, act, B, k, off, lanes);
+                       dim3(kRolloutBlock), lds, s, *cfg, *st,                                  \
+                       policy_p1, policy_p2, n_ticks, obs, act, B, k, off, lanes, lds_n);
   ORX_ROLLOUT(0, 0, false) ORX_ROLLOUT(0, 1, false) ORX_ROLLOUT(0, 2, false)
   ORX_ROLLOUT(8, 0, false) ORX_ROLLOUT(8, 1, false) ORX_ROLLOUT(8, 2, false)
   ORX_ROLLOUT(16, 0, false) ORX_ROLLOUT(16, 1, false) ORX_ROLLOUT(16, 2, false)
-  ORX_ROLLOUT(0, 0, true) ORX_ROLLOUT(8, 0, true) ORX_ROLLOUT(16, 0, true)
+  ORX_ROLLOUT(0, 0, true) ORX_ROLLOUT(0, 1, true) ORX_ROLLOUT(0, 2, true)
+  ORX_ROLLOUT(8, 0, true) ORX_ROLLOUT(8, 1, true) ORX_ROLLOUT(8, 2, true)
+  ORX_ROLLOUT(16, 0, true) ORX_ROLLOUT(16, 1, true) ORX_ROLLOUT(16, 2, true)
 #undef ORX_ROLLOUT
   return launch_status("orx_rollout");
 }

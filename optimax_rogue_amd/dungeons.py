@@ -51,6 +51,28 @@ class DungeonBank:
             self.ground[li, :len(g)] = g
             self.meta[li] = (len(g), st[0] // H, st[0] % H, 0)
 
+    @classmethod
+    def random(cls, width: int, height: int, n_layouts: int, seed: int = 0,
+               wall_p: float = 0.15, n_stairs: int = 1) -> "DungeonBank":
+        """A synthetic bank: border walls, interior walls with probability
+        ``wall_p``, ``n_stairs`` staircases on Ground tiles (numpy
+        RandomState(seed); connectivity is not required by the updater)."""
+        rs = np.random.RandomState(seed)
+        out = []
+        for _ in range(int(n_layouts)):
+            t = np.full((width, height), Tile.Ground, np.uint8)
+            t[[0, -1], :] = Tile.Wall
+            t[:, [0, -1]] = Tile.Wall
+            inner = rs.rand(width, height) < wall_p
+            inner[[0, -1], :] = False
+            inner[:, [0, -1]] = False
+            t[inner] = Tile.Wall
+            ground = np.argwhere(t == Tile.Ground)
+            for j in rs.choice(len(ground), n_stairs, replace=False):
+                t[tuple(ground[j])] = Tile.StaircaseDown
+            out.append(t)
+        return cls(np.stack(out))
+
     def __len__(self) -> int:
         return len(self.layouts)
 

@@ -126,6 +126,11 @@ ORACLE_CASES = {
     "bank_64_npc": (dict(width=64, height=64, n_npcs=8, max_ticks=300), (1, 1), 2048, 400, 15),
     "bank_stairs_unused": (dict(width=12, height=10, n_npcs=2, max_ticks=200, despawn=2), (2, 1),
                            2048, 400, 16),
+    # a bank too large for the rollout's LDS staging (64 x 36 x 36 tiles =
+    # 81 KiB > 64 KiB): the rollout reads the tiles from global memory
+    # (bank_64_npc, exactly 64 KiB, is staged)
+    "bank_big_global": (dict(width=36, height=36, n_npcs=4, max_ticks=200), (2, 1), 2048, 300,
+                        26),
     # a StaircaseBot descending into a 5x4 depth a RandomBot walks: the
     # rollout's descend-into-the-other's-depth path in both drawn orders
     "desc_meet_5x4": (dict(width=5, height=4, start_mode=2, p1_depth=2, p2_depth=1,
@@ -145,6 +150,7 @@ ORACLE_CASES = {
                        rng=1), (1, 1), 2048, 200, 23),
 }
 ORACLE_BANKS = {"bank_64_npc": (64, 64, 16, 21, (1,)), "bank_stairs_unused": (12, 10, 5, 22, (1, 3)),
+                "bank_big_global": (36, 36, 64, 27, (1, 2)),
                 "stock_bank_separated": (12, 10, 7, 24, (1, 2))}
 
 
@@ -281,6 +287,36 @@ def test_stream_shards_equal_one_engine(n_streams):
     assert np.array_equal(obs.cpu().numpy(), torch.cat(so, dim=2).cpu().numpy())
     assert np.array_equal(act.cpu().numpy(), torch.cat(sa, dim=1).cpu().numpy())
     assert a["ep_count"].sum() >= B
+
+
+@pytest.mark.parametrize("pol", [(1, 1), (2, 2)])
+def test_bank_rollout_forms_agree(pol, monkeypatch):
+    """A dungeon bank through the trajectory-specialized rollout (obs and act:
+    buffer stores, LDS-staged tiles), the generic one (act only) and with the
+    LDS staging disabled: identical states and observation rows."""
+    import torch
+    from optimax_rogue_amd import DungeonBank
+    from optimax_rogue_amd.enums import OBS_FIELDS
+    bank = DungeonBank.random(40, 30, 12, seed=5, n_stairs=2)
+    cfg = dict(width=40, height=30, n_npcs=4, max_ticks=150)
+    B, T = 3001, 200
+    res = []
+    for no_lds, with_obs in (("", True), ("", False), ("1", True)):
+        if no_lds:
+            monkeypatch.setenv("ORX_NO_LDS_TILES", "1")
+        else:
+            monkeypatch.delenv("ORX_NO_LDS_TILES", raising=False)
+        e = _engine(cfg, B, 9, layouts=bank.layouts)
+        obs = torch.zeros((T, len(OBS_FIELDS), B), dtype=torch.int32, device=e.device)
+        act = torch.zeros((T, B, 2), dtype=torch.int8, device=e.device)
+        e.rollout(T, *pol, obs=obs if with_obs else None, act=act)
+        res.append((e.snapshot(), obs.cpu().numpy() if with_obs else None, act.cpu().numpy()))
+    for got in res[1:]:
+        for k in STATE_KEYS:
+            assert np.array_equal(got[0][k], res[0][0][k]), k
+        assert np.array_equal(got[2], res[0][2])
+    assert np.array_equal(res[2][1], res[0][1])
+    assert res[0][0]["ep_count"].sum() > 0 and res[0][0]["counters"][1].sum() > 0
 
 
 def test_rollout_equals_step_c3():

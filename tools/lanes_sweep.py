@@ -45,6 +45,13 @@ def point(cfg, B, pol, lanes, T=128, warm=3, reps=10):
             "env_steps_per_s": B * T / us * 1e6}
 
 
+def bank_cfg():
+    """C3 on a dungeon bank: 16 random 64x64 layouts, K = 8, RandomBots."""
+    from optimax_rogue_amd import DungeonBank
+    bank = DungeonBank.random(64, 64, 16, seed=7)
+    return EnvConfig(width=64, height=64, n_npcs=8, layouts=bank.layouts)
+
+
 def main():
     which = sys.argv[1:] or ["c3", "c5", "c2"]
     c5sep = EnvConfig.c5()
@@ -53,9 +60,21 @@ def main():
             "c5": [(EnvConfig.c5(), 16384, 2), (EnvConfig.c5(), 131072, 2)],
             "c5sep": [(c5sep, 16384, 2), (c5sep, 131072, 2)],
             "c2": [(EnvConfig.c2(), 4096, 1)],
-            "large": [(EnvConfig.c3(), 1 << 20, 1)]}
+            "large": [(EnvConfig.c3(), 1 << 20, 1)],
+            "bank": [(bank_cfg(), 65536, 1), (bank_cfg(), 16384, 1)]}
     for w in which:
         for cfg, B, pol in work[w]:
+            if w == "bank":  # LDS-staged tiles against L2-resident global reads
+                for no_lds in ("", "1"):
+                    if no_lds:
+                        os.environ["ORX_NO_LDS_TILES"] = "1"
+                    else:
+                        os.environ.pop("ORX_NO_LDS_TILES", None)
+                    r = point(cfg, B, pol, 0)
+                    r.update(workload=w, lds_tiles=not no_lds)
+                    print(json.dumps(r), flush=True)
+                os.environ.pop("ORX_NO_LDS_TILES", None)
+                continue
             for lanes in (0, 64, 32, 16, 8, 4, 2):
                 if lanes and B // lanes > (1 << 16):
                     continue
