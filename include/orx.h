@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define ORX_ABI_VERSION 2
+#define ORX_ABI_VERSION 3
 
 /* ---- error codes -------------------------------------------------------- */
 #define ORX_OK 0
@@ -52,7 +52,8 @@ extern "C" {
 #define ORX_PLAYER2_WIN 3
 #define ORX_TIE 4
 /* build-only per-game status codes (>= 16): the game is stopped            */
-#define ORX_STATUS_BAD_ACTION 16   /* an action outside 1..5 (reference would
+#define ORX_STATUS_BAD_ACTION 16   /* an action outside 1..5 (1..6 with
+                                      ORX_EXT_HEAL; the reference would
                                       attack itself, updater.py:229-234)     */
 #define ORX_STATUS_RNG_EXHAUSTED 17 /* a rejection loop ran past its word cap
                                       (probability < 1e-180; never observed) */
@@ -102,6 +103,45 @@ extern "C" {
 #define ORX_EXT_RANDOM_DOUBLE_DEATH 2 /* "If both agents die during the same
    tick then one wins at random": one word of stream purpose 6 (c2 = tick)
    instead of Tie; top bit 0 = Player1Win                                  */
+/* The readme's character mechanics (readme.md:44, 72, 74).  Every free
+ * parameter is an orx_cfg_t field; the player attributes live in
+ * orx_state_t.p_rpg, items in item_pos / item_mask.       */
+#define ORX_EXT_MANA 4 /* "if A has mana then up to 1/3 the manabar is
+   converted into damage and spent": players start with mana_max mana; each
+   attack (handle_combat with a player attacker, vs a player or an NPC)
+   spends s = min(mana, mana_max / 3) rounded down to a multiple of
+   mana_per_point and deals s / mana_per_point extra damage; at the end of
+   every tick each player regains mana_regen, capped at mana_max          */
+#define ORX_EXT_HEAL 8 /* "A player may heal by spending up to 1/3 their
+   manabar and converting it to health.  They cannot move while healing":
+   action ORX_MOVE_HEAL (6) is a Stay (a Block for attackers) that, at the
+   player's turn in the initiative order and if it is alive, converts up to
+   min(mana, mana_max / 3) mana into health at mana_per_point per point,
+   never above its max health; reported as EntityHealthUpdate (+amount).
+   Needs ORX_EXT_MANA                                                      */
+#define ORX_EXT_LEVELING 16 /* "Enemies ... may be killed for experience.
+   Leveling refills health and mana": the player whose hit takes an NPC to
+   health <= 0 gains xp_per_kill; each time its xp crosses a multiple of
+   xp_per_level a living player's health is set to its max health and its
+   mana to mana_max (after the death sweep)                               */
+#define ORX_EXT_ITEMS 32 /* "Enemies may drop items, which provide flat
+   attribute bonuses if picked up.  There are a finite number of item
+   spots": an NPC removed by the death sweep drops an item on its cell with
+   probability item_drop_pct / 100 (Philox purpose 8, c2 = tick, block =
+   NPC slot: word a * 100 >> 32 < item_drop_pct; word b bit 0 = kind:
+   0 damage, 1 max health); a player whose move steps onto an item's cell
+   takes it if it holds fewer than item_slots items: damage or max health
+   (and health) += item_bonus                                              */
+#define ORX_EXT_RPG (ORX_EXT_MANA | ORX_EXT_HEAL | ORX_EXT_LEVELING | ORX_EXT_ITEMS)
+
+/* player attributes of the character mechanics: rows of orx_state_t.p_rpg  */
+#define ORX_RPG_MANA 0
+#define ORX_RPG_XP 1
+#define ORX_RPG_DAMAGE 2      /* Entity.damage (base + damage items)         */
+#define ORX_RPG_MAX_HEALTH 3  /* Entity.max_health (base + health items)     */
+#define ORX_RPG_ITEMS 4       /* items held                                  */
+#define ORX_RPG_FIELDS 5
+#define ORX_MOVE_HEAL 6       /* ORX_EXT_HEAL only                           */
 
 /* per-game event counters (rows of orx_state_t.counters)                    */
 #define ORX_CNT_COMBAT 0        /* handle_combat calls       updater.py:298  */
@@ -121,7 +161,8 @@ extern "C" {
 #define ORX_EV_POSITION 3
 #define ORX_EV_DUNGEON 4
 #define ORX_EV_HEALTH 5  /* {5, iden, amount, 0}  EntityHealthUpdate updates.py:222-253
-                            (separation damage, ORX_EXT_SEPARATION_DAMAGE)   */
+                            (separation damage -dmg, ORX_EXT_SEPARATION_DAMAGE;
+                            a heal +amount, ORX_EXT_HEAL)                   */
 #define ORX_MAX_EVENTS 8 /* per game per tick (at most 6 occur)            */
 
 #define ORX_MAX_NPCS 16 /* NPCs per game (alive mask is 32-bit; registers)  */
@@ -174,6 +215,15 @@ typedef struct orx_cfg {
                              grid DungeonGenerator plugin, worldgen.py:9-26) */
   int32_t sep_period;     /* ORX_EXT_SEPARATION_DAMAGE: ticks per +1 damage   */
   int32_t rng;            /* ORX_RNG_*                                       */
+  /* character mechanics (ORX_EXT_MANA / HEAL / LEVELING / ITEMS)            */
+  int32_t mana_max;       /* manabar size (>= 3 with MANA)                   */
+  int32_t mana_regen;     /* mana regained per tick                          */
+  int32_t mana_per_point; /* mana per point of damage or health (>= 1)       */
+  int32_t xp_per_kill;    /* experience per NPC kill                         */
+  int32_t xp_per_level;   /* experience per level (>= 1 with LEVELING)       */
+  int32_t item_drop_pct;  /* 0..100: chance a dying NPC drops an item        */
+  int32_t item_bonus;     /* flat attribute bonus of an item                 */
+  int32_t item_slots;     /* items a player can hold                         */
 } orx_cfg_t;
 
 /* ---- batch state (SoA, batch axis contiguous; all device pointers) ------- */
@@ -215,6 +265,13 @@ typedef struct orx_state {
                                    (layout + 1) << 16} of entered dungeons,
                                    slot depth % ORX_DSTORE (the staircases a
                                    keyed stream would regenerate)            */
+  /* character mechanics (any ORX_EXT_RPG flag; NULL otherwise)              */
+  int32_t* p_rpg;               /* [ORX_RPG_FIELDS][2][B] player attributes   */
+  uint16_t* item_pos;           /* [K][B] ORX_EXT_ITEMS: item dropped by NPC
+                                   slot k, x | y << 8 (on the NPCs' depth)    */
+  uint32_t* item_mask;          /* [2][B] ORX_EXT_ITEMS: row 0 bit k = item k
+                                   lies on the floor, row 1 bit k = its kind
+                                   (0 damage, 1 max health)                  */
 } orx_state_t;
 
 /* ---- entry points --------------------------------------------------------- */
@@ -259,7 +316,8 @@ int orx_reset(const orx_cfg_t* cfg, const orx_state_t* st, const uint8_t* mask,
               int64_t n_games, uint64_t seed, int64_t game_offset, void* stream);
 
 /* Advances every game one tick with actions[b][0] (player 1) and
- * actions[b][1] (player 2), values Move 1..5.  Replaces
+ * actions[b][1] (player 2), values Move 1..5 (and ORX_MOVE_HEAL with
+ * ORX_EXT_HEAL).  Replaces
  * Updater.update(game_state, player1_move, player2_move)  updater.py:76-162
  * (with GameState.on_tick, state.py:46-51, folded in).  A game whose status
  * is not ORX_IN_PROGRESS is reset to its next episode when cfg->autoreset,

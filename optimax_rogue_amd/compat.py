@@ -285,11 +285,13 @@ def game_state(snap: dict, i: int, cfg, extra_stairs: Optional[Dict[int, tuple]]
             return DungeonView(W, H, sx, sy, tiles=bank.tiles(int(lay)))
         return DungeonView(W, H, sx, sy)
 
+    rpg = snap.get("p_rpg")  # the character mechanics: items raise the base stats
     for p in range(2):
         d = int(snap["p_depth"][p][i])
+        mhp, dmg = ((rpg[3][p][i], rpg[2][p][i]) if rpg is not None
+                    else (cfg.player_health, cfg.player_damage))
         ents.append(EntityView(1 + p, d, snap["p_x"][p][i], snap["p_y"][p][i],
-                               snap["p_health"][p][i], cfg.player_health, cfg.player_damage,
-                               cfg.player_armor))
+                               snap["p_health"][p][i], mhp, dmg, cfg.player_armor))
         lay = int(snap["p_layout"][p][i]) if bank is not None else -1
         cur.setdefault(d, (int(snap["st_x"][p][i]), int(snap["st_y"][p][i]), lay))
     if extra_stairs is None:

@@ -23,7 +23,8 @@ from .enums import DungeonDespawningStrategy, StartMode
 CFG_FIELDS = ("width", "height", "despawn", "max_ticks", "start_mode", "p1_depth", "p2_depth",
               "n_npcs", "npc_health", "npc_damage", "npc_armor", "player_health",
               "player_damage", "player_armor", "autoreset", "flags", "n_layouts", "sep_period",
-              "rng")
+              "rng", "mana_max", "mana_regen", "mana_per_point", "xp_per_kill", "xp_per_level",
+              "item_drop_pct", "item_bonus", "item_slots")
 
 
 class OrxCfg(ctypes.Structure):
@@ -54,6 +55,17 @@ class EnvConfig:
     # RNG_MT19937 (stock seeding: each game's own random / np.random state
     # seeded with seed + game id, consumed in the reference's call order)
     rng: int = 0
+    # the readme's character mechanics (flags EXT_MANA / EXT_HEAL /
+    # EXT_LEVELING / EXT_ITEMS; readme.md:44, 72, 74).  The readme names no
+    # numbers, so every one is a parameter; these defaults are the build's.
+    mana_max: int = 9               # manabar; an attack or a heal spends up to a third
+    mana_regen: int = 1             # mana regained per tick
+    mana_per_point: int = 1         # mana per point of damage / health
+    xp_per_kill: int = 1            # experience per NPC kill
+    xp_per_level: int = 3           # experience per level (a level refills health, mana)
+    item_drop_pct: int = 50         # chance (%) that a dying NPC drops an item
+    item_bonus: int = 1             # flat bonus of an item (damage or max health)
+    item_slots: int = 3             # items a player can hold
     # explicit-grid dungeon generator: [L, W, H] Tile codes (None =
     # EmptyDungeonGenerator).  spawn_dungeon(depth) returns layout randint(L).
     layouts: Optional[np.ndarray] = dataclasses.field(default=None, repr=False, compare=False)

@@ -60,7 +60,8 @@ namespace {
 enum : uint32_t {
   PUR_INIT = 1, PUR_DUNGEON = 2, PUR_SHUFFLE = 3, PUR_SPAWN = 4, PUR_POLICY = 5,
   PUR_RESOLVE = 6,  // ORX_EXT_RANDOM_DOUBLE_DEATH
-  PUR_TICK = 7      // the tick's CPython-random bit reservoir (bots, shuffles)
+  PUR_TICK = 7,     // the tick's CPython-random bit reservoir (bots, shuffles)
+  PUR_ITEM = 8      // ORX_EXT_ITEMS: an NPC's drop (c2 = tick, block = NPC slot)
 };
 #define ORX_LIKELY(x) __builtin_expect(!!(x), 1)
 #define ORX_UNLIKELY(x) __builtin_expect(!!(x), 0)
@@ -166,6 +167,11 @@ struct Player {
   int32_t lay;    // bank layout of the player's depth (dungeon bank only)
   int32_t move;   // validated move for this tick
   int32_t tx, ty; // target cell of `move` from the pre-tick position
+  // character mechanics (ORX_EXT_RPG; never touched by the kernels that are
+  // compiled with those flags known off)
+  int32_t mana, xp, dmg, mhp, nitems;
+  int32_t heal;   // this tick's move is ORX_MOVE_HEAL (a Stay)
+  int32_t hd;     // damage of this tick's hit on an NPC
 };
 
 // Field-wise select: a conditional copy of the whole struct would be lowered
@@ -182,6 +188,13 @@ __device__ __forceinline__ Player pick(bool c, const Player& a, const Player& b)
   r.move = c ? a.move : b.move;
   r.tx = c ? a.tx : b.tx;
   r.ty = c ? a.ty : b.ty;
+  r.mana = c ? a.mana : b.mana;
+  r.xp = c ? a.xp : b.xp;
+  r.dmg = c ? a.dmg : b.dmg;
+  r.mhp = c ? a.mhp : b.mhp;
+  r.nitems = c ? a.nitems : b.nitems;
+  r.heal = c ? a.heal : b.heal;
+  r.hd = c ? a.hd : b.hd;
   return r;
 }
 
@@ -189,6 +202,9 @@ struct Cfg {  // device copy of orx_cfg_t plus derived constants (all wave-unifo
   int32_t W, H, despawn, max_ticks, start_mode, d1, d2, K;
   int32_t npc_hp, player_hp, player_dmg_net, autoreset;
   int32_t ext, sep_period;  // ORX_EXT_* build extensions (0 in FAST kernels)
+  // character mechanics (ORX_EXT_RPG)
+  int32_t player_dmg, player_armor, mana_max, mana_third, mana_regen, mana_pp;
+  int32_t xp_kill, xp_level, drop_pct, item_bonus, item_slots;
   int32_t ih;        // H - 2 (interior column height)
   // ceil(2^32 / d) for d = ih and d = H: n / d == umulhi(n, magic) for every
   // n < 2^16 (error < n / 2^32 <= 1/d), so set only when the dividends
@@ -670,6 +686,12 @@ __device__ __forceinline__ void setup_game(const Cfg& c, Key key, Src& src, Play
   if (placed < total) err = true;
   p1.hp = c.player_hp;
   p2.hp = c.player_hp;
+  // character mechanics (ORX_EXT_RPG): a fresh character's attributes
+  p1.mana = p2.mana = c.mana_max;
+  p1.xp = p2.xp = 0;
+  p1.dmg = p2.dmg = c.player_dmg;
+  p1.mhp = p2.mhp = c.player_hp;
+  p1.nitems = p2.nitems = 0;
   tick = kStartTick;
   status = err ? ORX_STATUS_RNG_EXHAUSTED : ORX_IN_PROGRESS;
 }
@@ -967,15 +989,96 @@ struct NpcHpRegs {
   }
 };
 
+// ---------------------------------------------------------------------------
+// Character mechanics (ORX_EXT_MANA / HEAL / LEVELING / ITEMS; readme.md:44,
+// 72, 74 -- no reference code, parameters in orx_cfg_t, include/orx.h)
+// ---------------------------------------------------------------------------
+// Items on the floor of the NPCs' depth: slot k holds the item NPC k dropped,
+// packed like the NPC slots (dead = 0xFFFF), kind bit k: 1 = max health.
+template <int NCAP>
+struct Items {
+  Npcs<NCAP> pos;
+  uint32_t kind;
+  __device__ __forceinline__ void clear() { pos.clear(); kind = 0; }
+};
+
+// Whole points from up to a third of the manabar, at most `cap` of them.
+__device__ __forceinline__ int32_t mana_points(const Cfg& c, int32_t mana, int32_t cap) {
+  const int32_t p = min(mana, c.mana_third) / c.mana_pp;
+  return min(p, cap);
+}
+
+// handle_combat's damage for a player attacker (updater.py:313, 331):
+// og_dmg = damage - armor; with ORX_EXT_MANA plus the mana spent on it.
+__device__ __forceinline__ int32_t rpg_attack(const Cfg& c, Player& self) {
+  int32_t d = self.dmg - c.player_armor;
+  if (c.ext & ORX_EXT_MANA) {
+    const int32_t pts = mana_points(c, self.mana, 0x7FFFFFFF);
+    self.mana -= pts * c.mana_pp;
+    d += pts;
+  }
+  return d > 0 ? d : 0;
+}
+
+// ORX_EXT_LEVELING: a kill's experience; crossing a level refills a living
+// player's health and mana.
+__device__ __forceinline__ void gain_xp(const Cfg& c, Player& p) {
+  const int32_t before = p.xp / c.xp_level;
+  p.xp += c.xp_kill;
+  if (p.xp / c.xp_level > before && p.hp > 0) {
+    p.hp = p.mhp;
+    if (c.ext & ORX_EXT_MANA) p.mana = c.mana_max;
+  }
+}
+
+// ORX_EXT_ITEMS: NPC k, swept at cell key `cell` in tick `tick`, may drop
+// its item (one Philox block of purpose ITEM, block index = slot).
+template <int NCAP>
+__device__ __forceinline__ void drop_item(const Cfg& c, Key key, uint32_t game, uint32_t ep,
+                                          int32_t tick, int k, uint32_t cell, Items<NCAP>& it) {
+  const W4 w = philox(game, ep, (uint32_t)tick, tag(PUR_ITEM, 0) | (uint32_t)k, key);
+  if ((int32_t)__umulhi(w.a, 100u) < c.drop_pct) {
+    it.pos.set(k, cell);
+    it.pos.alive |= 1u << k;
+    it.kind = (it.kind & ~(1u << k)) | ((w.b & 1u) << k);
+  }
+}
+
+// ORX_EXT_ITEMS: a player that stepped onto an item's cell takes it when it
+// has a free item spot.
+template <int NCAP>
+__device__ __forceinline__ void pick_up(const Cfg& c, Player& self, Items<NCAP>& it) {
+  const int k = it.pos.find(pack_xy(self.x, self.y));
+  if (k >= 0 && self.nitems < c.item_slots) {
+    const bool health_item = (it.kind >> k) & 1u;
+    it.pos.alive &= ~(1u << k);
+    it.pos.kill(k);
+    it.kind &= ~(1u << k);
+    self.nitems += 1;
+    if (health_item) {
+      self.mhp += c.item_bonus;
+      self.hp += c.item_bonus;
+    } else {
+      self.dmg += c.item_bonus;
+    }
+  }
+}
+
 // handle_move for `self` (updater.py:180-243), branch-free except for the
 // rare descend.  Returns true if the target cell holds an NPC (the slot is
 // resolved in npc_hits); combat against the other player is applied here.
 template <int NCAP, bool EV, bool GRID, class Src, class S>
 __device__ __forceinline__ bool handle_move(const Cfg& c, Key key, Src& src, Player& self,
                                             Player& other, int32_t other_start,
-                                            const Npcs<NCAP>& npc, S& spawn, Deltas& dl,
-                                            bool& err, int32_t self_iden, bool self_first,
-                                            Events<EV>& ev) {
+                                            const Npcs<NCAP>& npc, Items<NCAP>& items,
+                                            S& spawn, Deltas& dl, bool& err, int32_t self_iden,
+                                            bool self_first, Events<EV>& ev) {
+  if ((c.ext & ORX_EXT_HEAL) && self.heal && self.hp > 0) {  // readme.md:74
+    const int32_t pts = mana_points(c, self.mana, max(self.mhp - self.hp, 0));
+    self.mana -= pts * c.mana_pp;
+    self.hp += pts;
+    if (pts > 0) ev.emit(ORX_EV_HEALTH, self_iden, pts, 0);
+  }
   const bool moving = self.move != ORX_MOVE_STAY;
   const int32_t tx = self.tx, ty = self.ty;
   const bool occ_other = moving && other.d == self.d && other.x == tx && other.y == ty;
@@ -990,7 +1093,11 @@ __device__ __forceinline__ bool handle_move(const Cfg& c, Key key, Src& src, Pla
   // Block / Parry / Ambush / Flee (updater.py:222-243): without a Modifier
   // subclass every flag deals og_dmg = attacker.damage - attacker.armor.
   dl.combat += (occ_other || hit_npc) ? 1 : 0;
-  other.hp -= (occ_other && c.player_dmg_net > 0) ? c.player_dmg_net : 0;
+  int32_t dmg = c.player_dmg_net > 0 ? c.player_dmg_net : 0;
+  if (c.ext & ORX_EXT_RPG) dmg = (occ_other || hit_npc) ? rpg_attack(c, self) : 0;
+  other.hp -= occ_other ? dmg : 0;
+  self.hd = dmg;  // an NPC hit's damage, applied by npc_hits after both moves
+  if (NCAP > 0 && (c.ext & ORX_EXT_ITEMS) && step && self.d == c.d1) pick_up(c, self, items);
   if constexpr (EV) {
     if (occ_other) {
       int32_t ox, oy;
@@ -1010,17 +1117,23 @@ __device__ __forceinline__ bool handle_move(const Cfg& c, Key key, Src& src, Pla
   return hit_npc;
 }
 
-// handle_combat on NPC defenders, then the death sweep (updater.py:136-145):
-// only NPCs hit this tick can reach health <= 0.
+// handle_combat on NPC defenders (hits of d0 then d1 damage, in the attackers'
+// order), then the death sweep (updater.py:136-145): only NPCs hit this tick
+// can reach health <= 0.  kill0 / kill1: attacker 0's / 1's hit took its NPC
+// to health <= 0 (ORX_EXT_LEVELING's kill credit).
 template <int NCAP, bool EV, class M>
 __device__ __forceinline__ void npc_hits(const Cfg& c, Npcs<NCAP>& npc, M& m, int h0, int h1,
-                                         Deltas& dl, Events<EV>& ev) {
-  const int dmg = c.player_dmg_net > 0 ? c.player_dmg_net : 0;
+                                         int d0, int d1, Deltas& dl, Events<EV>& ev,
+                                         bool& kill0, bool& kill1) {
   int v0 = m.get(h0 >= 0 ? h0 : h1), v1 = m.get(h1 >= 0 ? h1 : h0);
-  if (h0 >= 0) v0 -= dmg;
-  if (h1 >= 0) { v1 = (h1 == h0) ? v0 - dmg : v1 - dmg; if (h1 == h0) v0 = v1; }
-  if (h0 >= 0) m.put(h0, v0);
-  if (h1 >= 0 && h1 != h0) m.put(h1, v1);
+  if (h0 >= 0) v0 -= d0;
+  const int v0a = v0;
+  if (h1 >= 0) { v1 = (h1 == h0) ? v0 - d1 : v1 - d1; if (h1 == h0) v0 = v1; }
+  kill0 = h0 >= 0 && v0a <= 0;
+  kill1 = h1 >= 0 && v1 <= 0 && !(h1 == h0 && v0a <= 0);
+  // the int8 rows keep health above -128 (a death is decided on the int)
+  if (h0 >= 0) m.put(h0, max(v0, -128));
+  if (h1 >= 0 && h1 != h0) m.put(h1, max(v1, -128));
   // the sweep walks GameState.entities backwards: higher slot first
   const bool swap = h1 > h0;
   const int ks[2] = {swap ? h1 : h0, swap ? h0 : h1};
@@ -1028,7 +1141,7 @@ __device__ __forceinline__ void npc_hits(const Cfg& c, Npcs<NCAP>& npc, M& m, in
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int k = ks[j];
-    if (k >= 0 && (int8_t)vs[j] <= 0 && ((npc.alive >> k) & 1u)) {
+    if (k >= 0 && vs[j] <= 0 && ((npc.alive >> k) & 1u)) {
       npc.alive &= ~(1u << k);
       npc.kill(k);
       dl.npc_death += 1;
@@ -1041,9 +1154,17 @@ __device__ __forceinline__ void npc_hits(const Cfg& c, Npcs<NCAP>& npc, M& m, in
 template <int NCAP, bool EV, bool GRID, class Src, class M>
 __device__ __forceinline__ void tick_game(const Cfg& c, Key key, Src& src, uint32_t game,
                                           uint32_t ep, bool p1_first, Player& p1, Player& p2,
-                                          Npcs<NCAP>& npc, M& m, int32_t& tick, int32_t& status,
-                                          bool& err, Deltas& dl, Events<EV>& ev,
-                                          int32_t& sep_start) {
+                                          Npcs<NCAP>& npc, Items<NCAP>& items, M& m,
+                                          int32_t& tick, int32_t& status, bool& err, Deltas& dl,
+                                          Events<EV>& ev, int32_t& sep_start) {
+  if (c.ext & ORX_EXT_HEAL) {  // a heal is a Stay that converts mana (readme.md:74)
+    p1.heal = p1.move == ORX_MOVE_HEAL;
+    p2.heal = p2.move == ORX_MOVE_HEAL;
+    p1.move = p1.heal ? ORX_MOVE_STAY : p1.move;
+    p2.move = p2.heal ? ORX_MOVE_STAY : p2.move;
+  } else {
+    p1.heal = p2.heal = 0;
+  }
   calc_pos(p1.x, p1.y, p1.move, p1.tx, p1.ty);         // updater.py:89-98
   if (blocked<GRID>(c, p1.lay, p1.tx, p1.ty)) p1.move = ORX_MOVE_STAY;
   calc_pos(p2.x, p2.y, p2.move, p2.tx, p2.ty);
@@ -1058,19 +1179,32 @@ __device__ __forceinline__ void tick_game(const Cfg& c, Key key, Src& src, uint3
   const int32_t a_start = p1_first ? c.d1 : c.d2;
   const int32_t b_start = p1_first ? c.d2 : c.d1;
   const int32_t a_iden = p1_first ? 1 : 2;
-  const bool hA = handle_move<NCAP, EV, GRID>(c, key, src, A, Bp, b_start, npc, spawn, dl, err,
-                                              a_iden, true, ev);
-  const bool hB = handle_move<NCAP, EV, GRID>(c, key, src, Bp, A, a_start, npc, spawn, dl, err,
-                                              3 - a_iden, false, ev);
+  const bool hA = handle_move<NCAP, EV, GRID>(c, key, src, A, Bp, b_start, npc, items, spawn,
+                                              dl, err, a_iden, true, ev);
+  const bool hB = handle_move<NCAP, EV, GRID>(c, key, src, Bp, A, a_start, npc, items, spawn,
+                                              dl, err, 3 - a_iden, false, ev);
   if (NCAP > 0 && ORX_UNLIKELY(hA || hB)) {
     // NPCs never move and are swept only after both moves: the slots found at
     // the targets now are the ones that were attacked.
     const int h0 = hA ? npc.find(pack_xy(A.tx, A.ty)) : -1;
     const int h1 = hB ? npc.find(pack_xy(Bp.tx, Bp.ty)) : -1;
-    npc_hits(c, npc, m, h0, h1, dl, ev);
+    bool kA = false, kB = false;
+    npc_hits(c, npc, m, h0, h1, A.hd, Bp.hd, dl, ev, kA, kB);
+    if (c.ext & (ORX_EXT_LEVELING | ORX_EXT_ITEMS)) {  // readme.md:44
+      if ((c.ext & ORX_EXT_LEVELING) && kA) gain_xp(c, A);
+      if ((c.ext & ORX_EXT_LEVELING) && kB) gain_xp(c, Bp);
+      if ((c.ext & ORX_EXT_ITEMS) && kA)
+        drop_item(c, key, game, ep, tick, h0, pack_xy(A.tx, A.ty), items);
+      if ((c.ext & ORX_EXT_ITEMS) && kB)
+        drop_item(c, key, game, ep, tick, h1, pack_xy(Bp.tx, Bp.ty), items);
+    }
   }
   p1 = pick(p1_first, A, Bp);
   p2 = pick(p1_first, Bp, A);
+  if (c.ext & ORX_EXT_MANA) {  // the end of the tick: mana regeneration
+    p1.mana = min(p1.mana + c.mana_regen, c.mana_max);
+    p2.mana = min(p2.mana + c.mana_regen, c.mana_max);
+  }
 
   if (c.ext & ORX_EXT_SEPARATION_DAMAGE) {  // build extension (readme.md:46-47)
     if (p1.d != p2.d) {
@@ -1110,12 +1244,66 @@ __device__ __forceinline__ void tick_game(const Cfg& c, Key key, Src& src, uint3
 template <int NCAP, bool EV, bool GRID = false, class M>
 __device__ __forceinline__ void tick_game(const Cfg& c, Key key, uint32_t game, uint32_t ep,
                                           bool p1_first, Player& p1, Player& p2,
-                                          Npcs<NCAP>& npc, M& m, int32_t& tick,
-                                          int32_t& status, bool& err, Deltas& dl,
+                                          Npcs<NCAP>& npc, Items<NCAP>& items, M& m,
+                                          int32_t& tick, int32_t& status, bool& err, Deltas& dl,
                                           Events<EV>& ev, int32_t& sep_start) {
   PhiloxSrc src{key, game, ep};
-  tick_game<NCAP, EV, GRID>(c, key, src, game, ep, p1_first, p1, p2, npc, m, tick, status, err,
-                            dl, ev, sep_start);
+  tick_game<NCAP, EV, GRID>(c, key, src, game, ep, p1_first, p1, p2, npc, items, m, tick, status,
+                            err, dl, ev, sep_start);
+}
+
+// The character mechanics' state (ORX_EXT_RPG): p_rpg rows and the items.
+// Without those flags only the register copies are zeroed (dead code in the
+// kernels that know the flags are off).
+template <int NCAP>
+__device__ __forceinline__ void load_rpg(const orx_state_t& st, const Cfg& c, uint32_t B,
+                                         uint32_t i, Player& p1, Player& p2, Items<NCAP>& it) {
+  it.clear();
+  p1.heal = p2.heal = 0;
+  p1.hd = p2.hd = 0;
+  if (!(c.ext & ORX_EXT_RPG)) {
+    p1.mana = p2.mana = p1.xp = p2.xp = p1.nitems = p2.nitems = 0;
+    p1.dmg = p2.dmg = c.player_dmg;
+    p1.mhp = p2.mhp = c.player_hp;
+    return;
+  }
+  const int32_t* r = st.p_rpg + i;
+  const size_t f = 2 * (size_t)B;
+  p1.mana = r[ORX_RPG_MANA * f];           p2.mana = r[ORX_RPG_MANA * f + B];
+  p1.xp = r[ORX_RPG_XP * f];               p2.xp = r[ORX_RPG_XP * f + B];
+  p1.dmg = r[ORX_RPG_DAMAGE * f];          p2.dmg = r[ORX_RPG_DAMAGE * f + B];
+  p1.mhp = r[ORX_RPG_MAX_HEALTH * f];      p2.mhp = r[ORX_RPG_MAX_HEALTH * f + B];
+  p1.nitems = r[ORX_RPG_ITEMS * f];        p2.nitems = r[ORX_RPG_ITEMS * f + B];
+  if constexpr (NCAP > 0) {
+    if (c.ext & ORX_EXT_ITEMS) {
+      it.pos.alive = st.item_mask[i];
+      it.kind = st.item_mask[B + i];
+      for (int k = 0; k < c.K; ++k)
+        if ((it.pos.alive >> k) & 1u) it.pos.set(k, st.item_pos[(size_t)k * B + i]);
+    }
+  }
+}
+
+template <int NCAP>
+__device__ __forceinline__ void store_rpg(const orx_state_t& st, const Cfg& c, uint32_t B,
+                                          uint32_t i, const Player& p1, const Player& p2,
+                                          const Items<NCAP>& it) {
+  if (!(c.ext & ORX_EXT_RPG)) return;
+  int32_t* r = st.p_rpg + i;
+  const size_t f = 2 * (size_t)B;
+  r[ORX_RPG_MANA * f] = p1.mana;           r[ORX_RPG_MANA * f + B] = p2.mana;
+  r[ORX_RPG_XP * f] = p1.xp;               r[ORX_RPG_XP * f + B] = p2.xp;
+  r[ORX_RPG_DAMAGE * f] = p1.dmg;          r[ORX_RPG_DAMAGE * f + B] = p2.dmg;
+  r[ORX_RPG_MAX_HEALTH * f] = p1.mhp;      r[ORX_RPG_MAX_HEALTH * f + B] = p2.mhp;
+  r[ORX_RPG_ITEMS * f] = p1.nitems;        r[ORX_RPG_ITEMS * f + B] = p2.nitems;
+  if constexpr (NCAP > 0) {
+    if (c.ext & ORX_EXT_ITEMS) {
+      st.item_mask[i] = it.pos.alive;
+      st.item_mask[B + i] = it.kind;
+      for (int k = 0; k < c.K; ++k)
+        if ((it.pos.alive >> k) & 1u) st.item_pos[(size_t)k * B + i] = (uint16_t)it.pos.get(k);
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1219,6 +1407,11 @@ __device__ __forceinline__ Cfg make_cfg(const orx_cfg_t& h, const orx_state_t& s
   c.autoreset = h.autoreset;
   c.ext = h.flags;
   c.sep_period = h.sep_period > 0 ? h.sep_period : 1;
+  c.player_dmg = h.player_damage; c.player_armor = h.player_armor;
+  c.mana_max = h.mana_max; c.mana_third = h.mana_max / 3; c.mana_regen = h.mana_regen;
+  c.mana_pp = h.mana_per_point > 0 ? h.mana_per_point : 1;
+  c.xp_kill = h.xp_per_kill; c.xp_level = h.xp_per_level > 0 ? h.xp_per_level : 1;
+  c.drop_pct = h.item_drop_pct; c.item_bonus = h.item_bonus; c.item_slots = h.item_slots;
   c.ih = h.height - 2;
   c.ih_magic = (int64_t)(h.width - 2) * (h.height - 2) <= 65536
                    ? (uint32_t)(0xFFFFFFFFu / (uint32_t)c.ih + 1u) : 0u;
@@ -1236,8 +1429,8 @@ __device__ __forceinline__ Cfg make_cfg(const orx_cfg_t& h, const orx_state_t& s
   return c;
 }
 
-__device__ __forceinline__ bool valid_move(int32_t m) {
-  return m >= ORX_MOVE_UP && m <= ORX_MOVE_STAY;
+__device__ __forceinline__ bool valid_move(const Cfg& c, int32_t m) {
+  return m >= ORX_MOVE_UP && m <= ((c.ext & ORX_EXT_HEAL) ? ORX_MOVE_HEAL : ORX_MOVE_STAY);
 }
 
 __device__ __forceinline__ uint16_t pack_actions(int32_t a1, int32_t a2) {
@@ -1260,6 +1453,9 @@ __global__ void __launch_bounds__(256) reset_kernel(orx_cfg_t hc, orx_state_t st
   int32_t tick, status;
   setup_game<NCAP, GRID>(c, key, off + i, (uint32_t)st.episode[i], p1, p2, npc, tick, status);
   store_players<GRID>(st, B, i, p1, p2, true);
+  Items<NCAP> items;
+  items.clear();
+  store_rpg(st, c, B, i, p1, p2, items);
   st.tick[i] = tick;
   st.status[i] = status;
   if (c.ext & ORX_EXT_SEPARATION_DAMAGE) st.sep_start[i] = -1;
@@ -1289,6 +1485,9 @@ __global__ void __launch_bounds__(256) step_kernel(orx_cfg_t hc, orx_state_t st,
     int32_t tick;
     setup_game<NCAP, GRID>(c, key, game, ep, p1, p2, npc, tick, status);
     store_players<GRID>(st, B, i, p1, p2, true);
+    Items<NCAP> items;
+    items.clear();
+    store_rpg(st, c, B, i, p1, p2, items);
     st.tick[i] = tick;
     st.status[i] = status;
     st.episode[i] = (int32_t)ep;
@@ -1302,7 +1501,7 @@ __global__ void __launch_bounds__(256) step_kernel(orx_cfg_t hc, orx_state_t st,
   const uint16_t a = reinterpret_cast<const uint16_t*>(actions)[i];
   p1.move = (int8_t)(a & 0xFF);
   p2.move = (int8_t)(a >> 8);
-  if (!valid_move(p1.move) || !valid_move(p2.move)) {
+  if (!valid_move(c, p1.move) || !valid_move(c, p2.move)) {
     st.status[i] = ORX_STATUS_BAD_ACTION;
     if (EV) n_events[i] = 0;
     return;
@@ -1311,15 +1510,18 @@ __global__ void __launch_bounds__(256) step_kernel(orx_cfg_t hc, orx_state_t st,
   int32_t tick = st.tick[i];
   load_players<GRID>(st, B, i, p1, p2);
   load_npcs(st, c, B, i, npc);
+  Items<NCAP> items;
+  load_rpg(st, c, B, i, p1, p2, items);
   NpcMem m{st.npc_pos, st.npc_health, B, i};
   Deltas dl = {0, 0, 0, 0, 0, 0};
   Events<EV> ev{EV ? events + (size_t)i * ORX_MAX_EVENTS * 4 : nullptr, 0};
   bool err = false;
   const bool p1_first = p1_first_draw(key, game, ep, tick, err);
   int32_t sep = (c.ext & ORX_EXT_SEPARATION_DAMAGE) ? st.sep_start[i] : -1;
-  tick_game<NCAP, EV, GRID>(c, key, game, ep, p1_first, p1, p2, npc, m, tick, status, err,
+  tick_game<NCAP, EV, GRID>(c, key, game, ep, p1_first, p1, p2, npc, items, m, tick, status, err,
                             dl, ev, sep);
   if (c.ext & ORX_EXT_SEPARATION_DAMAGE) st.sep_start[i] = sep;
+  store_rpg(st, c, B, i, p1, p2, items);
   store_players<GRID>(st, B, i, p1, p2, dl.descend != 0);
   st.tick[i] = tick;
   st.status[i] = status;
@@ -1410,8 +1612,8 @@ template <int NCAP, bool GRID, class M>
 __device__ __forceinline__ void rollout_tick(const Cfg& c, const orx_state_t& st, uint32_t B,
                                              uint32_t i, Key key, uint32_t game, uint32_t& ep,
                                              int32_t pol1, int32_t pol2, Player& p1,
-                                             Player& p2, Npcs<NCAP>& npc, M& hp,
-                                             int32_t& tick, int32_t& status, Deltas& dl,
+                                             Player& p2, Npcs<NCAP>& npc, Items<NCAP>& items,
+                                             M& hp, int32_t& tick, int32_t& status, Deltas& dl,
                                              int32_t& sep, bool& restarted, int32_t& a1,
                                              int32_t& a2) {
   // one tick block: the bots' bits and the initiative bits (§4).  Without a
@@ -1532,6 +1734,7 @@ __device__ __forceinline__ void rollout_tick(const Cfg& c, const orx_state_t& st
       if (c.autoreset) {  // the next episode (worldgen.py:77-87, 124-135)
         ep += 1;
         setup_game<NCAP, GRID>(c, key, game, ep, p1, p2, npc, tick, status);
+        items.clear();
         if constexpr (NCAP > 0) {
           store_new_npcs(st, c, B, i, npc, false);  // health: from hp at the end
           hp.fill(c.npc_hp);
@@ -1546,8 +1749,8 @@ __device__ __forceinline__ void rollout_tick(const Cfg& c, const orx_state_t& st
       bool err = false;
       const bool p1_first = first_from_packed(pk_shf, key, game, ep, t0, err);
       Events<false> ev{nullptr, 0};
-      tick_game<NCAP, false, GRID>(c, key, game, ep, p1_first, p1, p2, npc, hp, tick, status,
-                                   err, dl, ev, sep);
+      tick_game<NCAP, false, GRID>(c, key, game, ep, p1_first, p1, p2, npc, items, hp, tick,
+                                   status, err, dl, ev, sep);
     } else {
       // the common path's rules, then the one-sided events: a player that
       // hits an NPC, descends or meets the other does not move freely
@@ -1604,7 +1807,10 @@ __device__ __forceinline__ void rollout_tick(const Cfg& c, const orx_state_t& st
 #endif
         Events<false> ev{nullptr, 0};
         dl.combat += (hit1 ? 1 : 0) + (hit2 ? 1 : 0);
-        npc_hits(c, npc, hp, hit1 ? npc.find(k1) : -1, hit2 ? npc.find(k2) : -1, dl, ev);
+        const int32_t dmg = c.player_dmg_net > 0 ? c.player_dmg_net : 0;
+        bool kc0, kc1;  // (kill credit: the character mechanics take the ordered tick)
+        npc_hits(c, npc, hp, hit1 ? npc.find(k1) : -1, hit2 ? npc.find(k2) : -1, dmg, dmg, dl,
+                 ev, kc0, kc1);
       }
       if (lean) {  // a meet: the two moves in the drawn order
 #ifdef ORX_STAMPS
@@ -1784,6 +1990,8 @@ __global__ void __launch_bounds__(kRolloutBlock) rollout_kernel(orx_cfg_t hc, or
   load_npcs(st, c, B, i, npc);
   NpcHpRegs<NCAP> hp;
   if constexpr (NCAP > 0) hp.load(st.npc_health, c.K, B, i);
+  Items<NCAP> items;
+  load_rpg(st, c, B, i, p1, p2, items);
   Deltas dl = {0, 0, 0, 0, 0, 0};
   int32_t sep = (c.ext & ORX_EXT_SEPARATION_DAMAGE) ? st.sep_start[i] : -1;
   bool restarted = false;
@@ -1798,12 +2006,13 @@ __global__ void __launch_bounds__(kRolloutBlock) rollout_kernel(orx_cfg_t hc, or
     if (t == 64) { ORX_STAMP(2); }
 #endif
     int32_t a1 = ORX_MOVE_STAY, a2 = ORX_MOVE_STAY;
-    rollout_tick<NCAP, GRID>(c, st, B, i, key, game, ep, pol1, pol2, p1, p2, npc, hp, tick,
-                             status, dl, sep, restarted, a1, a2);
+    rollout_tick<NCAP, GRID>(c, st, B, i, key, game, ep, pol1, pol2, p1, p2, npc, items, hp,
+                             tick, status, dl, sep, restarted, a1, a2);
     if (!(ORX_DIAG & 16)) traj.write(t, p1, p2, tick, status, a1, a2);
   } while (++t < n_ticks);
   ORX_STAMP(3);
   store_players<GRID>(st, B, i, p1, p2, restarted || dl.descend != 0);
+  store_rpg(st, c, B, i, p1, p2, items);
   st.tick[i] = tick;
   st.status[i] = status;
   st.episode[i] = (int32_t)ep;
@@ -1920,6 +2129,9 @@ __global__ void __launch_bounds__(256) mt_reset_kernel(orx_cfg_t hc, orx_state_t
   setup_game<NCAP, GRID>(c, Key{0, 0}, src, p1, p2, npc, tick, status);
   src.close();
   store_players<GRID>(st, B, i, p1, p2, true);
+  Items<NCAP> items;
+  items.clear();
+  store_rpg(st, c, B, i, p1, p2, items);
   st.tick[i] = tick;
   st.status[i] = status;
   if (c.ext & ORX_EXT_SEPARATION_DAMAGE) st.sep_start[i] = -1;
@@ -1978,6 +2190,9 @@ __global__ void __launch_bounds__(256) mt_step_kernel(orx_cfg_t hc, orx_state_t 
     setup_game<NCAP, GRID>(c, key, src, p1, p2, npc, tick, status);
     src.close();
     store_players<GRID>(st, B, i, p1, p2, true);
+    Items<NCAP> items;
+    items.clear();
+    store_rpg(st, c, B, i, p1, p2, items);
     st.tick[i] = tick;
     st.status[i] = status;
     st.episode[i] = (int32_t)ep;
@@ -1991,7 +2206,7 @@ __global__ void __launch_bounds__(256) mt_step_kernel(orx_cfg_t hc, orx_state_t 
   const uint16_t a = reinterpret_cast<const uint16_t*>(actions)[i];
   p1.move = (int8_t)(a & 0xFF);
   p2.move = (int8_t)(a >> 8);
-  if (!valid_move(p1.move) || !valid_move(p2.move)) {
+  if (!valid_move(c, p1.move) || !valid_move(c, p2.move)) {
     st.status[i] = ORX_STATUS_BAD_ACTION;
     if (EV) n_events[i] = 0;
     return;
@@ -2000,6 +2215,8 @@ __global__ void __launch_bounds__(256) mt_step_kernel(orx_cfg_t hc, orx_state_t 
   int32_t tick = st.tick[i];
   load_players<GRID>(st, B, i, p1, p2);
   load_npcs(st, c, B, i, npc);
+  Items<NCAP> items;
+  load_rpg(st, c, B, i, p1, p2, items);
   NpcMem m{st.npc_pos, st.npc_health, B, i};
   Deltas dl = {0, 0, 0, 0, 0, 0};
   Events<EV> ev{EV ? events + (size_t)i * ORX_MAX_EVENTS * 4 : nullptr, 0};
@@ -2008,9 +2225,10 @@ __global__ void __launch_bounds__(256) mt_step_kernel(orx_cfg_t hc, orx_state_t 
   src.open(st, B, i);
   const bool p1_first = mt_shuffles(src.py, npc, err);
   int32_t sep = (c.ext & ORX_EXT_SEPARATION_DAMAGE) ? st.sep_start[i] : -1;
-  tick_game<NCAP, EV, GRID>(c, key, src, game, ep, p1_first, p1, p2, npc, m, tick, status,
+  tick_game<NCAP, EV, GRID>(c, key, src, game, ep, p1_first, p1, p2, npc, items, m, tick, status,
                             err, dl, ev, sep);
   src.close();
+  store_rpg(st, c, B, i, p1, p2, items);
   if (c.ext & ORX_EXT_SEPARATION_DAMAGE) st.sep_start[i] = sep;
   store_players<GRID>(st, B, i, p1, p2, dl.descend != 0);
   st.tick[i] = tick;
@@ -2039,6 +2257,8 @@ __global__ void __launch_bounds__(256) mt_rollout_kernel(orx_cfg_t hc, orx_state
   Npcs<NCAP> npc;
   load_npcs(st, c, B, i, npc);
   NpcMem m{st.npc_pos, st.npc_health, B, i};
+  Items<NCAP> items;
+  load_rpg(st, c, B, i, p1, p2, items);
   Deltas dl = {0, 0, 0, 0, 0, 0};
   int32_t sep = (c.ext & ORX_EXT_SEPARATION_DAMAGE) ? st.sep_start[i] : -1;
   bool stairs_dirty = false, npc_dirty = false;
@@ -2054,12 +2274,13 @@ __global__ void __launch_bounds__(256) mt_rollout_kernel(orx_cfg_t hc, orx_state
       const int32_t descents = dl.descend;
       const bool p1_first = mt_shuffles(src.py, npc, err);
       Events<false> ev{nullptr, 0};
-      tick_game<NCAP, false, GRID>(c, key, src, game, ep, p1_first, p1, p2, npc, m, tick,
+      tick_game<NCAP, false, GRID>(c, key, src, game, ep, p1_first, p1, p2, npc, items, m, tick,
                                    status, err, dl, ev, sep);
       stairs_dirty |= dl.descend != descents;
     } else if (c.autoreset) {
       ep += 1;
       setup_game<NCAP, GRID>(c, key, src, p1, p2, npc, tick, status);
+      items.clear();
       if constexpr (NCAP > 0) store_new_npcs(st, c, B, i, npc);
       stairs_dirty = true;
       npc_dirty = true;
@@ -2069,6 +2290,7 @@ __global__ void __launch_bounds__(256) mt_rollout_kernel(orx_cfg_t hc, orx_state
   }
   src.close();
   store_players<GRID>(st, B, i, p1, p2, stairs_dirty);
+  store_rpg(st, c, B, i, p1, p2, items);
   st.tick[i] = tick;
   st.status[i] = status;
   st.episode[i] = (int32_t)ep;
@@ -2139,8 +2361,19 @@ int check_cfg(const orx_cfg_t* c) {
     return fail(ORX_EINVAL, "board too small for the players and NPCs");
   if (c->player_health < 1) return fail(ORX_EINVAL, "player_health must be >= 1");
   if (c->autoreset != 0 && c->autoreset != 1) return fail(ORX_EINVAL, "autoreset must be 0 or 1");
-  if (c->flags & ~(ORX_EXT_SEPARATION_DAMAGE | ORX_EXT_RANDOM_DOUBLE_DEATH))
+  if (c->flags & ~(ORX_EXT_SEPARATION_DAMAGE | ORX_EXT_RANDOM_DOUBLE_DEATH | ORX_EXT_RPG))
     return fail(ORX_EINVAL, "unknown extension flag");
+  if ((c->flags & ORX_EXT_HEAL) && !(c->flags & ORX_EXT_MANA))
+    return fail(ORX_EINVAL, "ORX_EXT_HEAL needs ORX_EXT_MANA");
+  if ((c->flags & ORX_EXT_MANA) &&
+      (c->mana_max < 3 || c->mana_regen < 0 || c->mana_per_point < 1))
+    return fail(ORX_EINVAL, "mana needs mana_max >= 3, mana_regen >= 0, mana_per_point >= 1");
+  if ((c->flags & ORX_EXT_LEVELING) && (c->xp_per_kill < 0 || c->xp_per_level < 1))
+    return fail(ORX_EINVAL, "leveling needs xp_per_kill >= 0, xp_per_level >= 1");
+  if ((c->flags & ORX_EXT_ITEMS) && (c->item_drop_pct < 0 || c->item_drop_pct > 100 ||
+                                     c->item_bonus < 0 || c->item_slots < 0))
+    return fail(ORX_EINVAL, "items need item_drop_pct in [0, 100], item_bonus >= 0, "
+                            "item_slots >= 0");
   if ((c->flags & ORX_EXT_SEPARATION_DAMAGE) && c->sep_period < 1)
     return fail(ORX_EINVAL, "separation damage needs sep_period >= 1");
   if (c->rng != ORX_RNG_PHILOX && c->rng != ORX_RNG_MT19937)
@@ -2165,6 +2398,10 @@ int check_state(const orx_cfg_t* c, const orx_state_t* s, bool full) {
     return fail(ORX_EINVAL, "separation damage needs sep_start");
   if (c->rng == ORX_RNG_MT19937 && (!s->mt_py || !s->mt_np || !s->dstore))
     return fail(ORX_EINVAL, "stock-seed mode needs mt_py, mt_np and dstore");
+  if ((c->flags & ORX_EXT_RPG) && !s->p_rpg)
+    return fail(ORX_EINVAL, "the character mechanics need p_rpg");
+  if ((c->flags & ORX_EXT_ITEMS) && c->n_npcs > 0 && (!s->item_pos || !s->item_mask))
+    return fail(ORX_EINVAL, "ORX_EXT_ITEMS needs item_pos and item_mask");
   return ORX_OK;
 }
 

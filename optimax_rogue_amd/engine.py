@@ -17,7 +17,8 @@ import torch
 
 from . import _lib
 from .config import EnvConfig
-from .enums import DSTORE, EXT_SEPARATION_DAMAGE, MAX_EVENTS, RNG_MT19937, N_COUNTERS, OBS_FIELDS, Policy
+from .enums import (DSTORE, EXT_ITEMS, EXT_RPG, EXT_SEPARATION_DAMAGE, MAX_EVENTS, N_COUNTERS,
+                    OBS_FIELDS, RNG_MT19937, RPG_FIELDS, Policy)
 
 STATE_FIELDS = ("p_x", "p_y", "p_depth", "p_health", "st_x", "st_y", "tick", "status", "episode",
                 "ret_sum", "ep_count", "counters", "npc_pos", "npc_health", "npc_alive")
@@ -96,6 +97,17 @@ class BatchedEngine:
             self.mt_py, self.mt_np = z(625, B), z(625, B)
             self.dstore = z(DSTORE, 2, B)
             ptrs.update({f: getattr(self, f).data_ptr() for f in ("mt_py", "mt_np", "dstore")})
+        # the readme's character mechanics (EXT_RPG flags): player attributes
+        # [RPG_FIELDS][2][B]; with EXT_ITEMS and NPCs the items each NPC slot
+        # dropped (x | y << 8) and their on-floor / kind bit masks
+        self.p_rpg = self.item_pos = self.item_mask = None
+        if int(cfg.flags) & EXT_RPG:
+            self.p_rpg = z(len(RPG_FIELDS), 2, B)
+            ptrs["p_rpg"] = self.p_rpg.data_ptr()
+            if int(cfg.flags) & EXT_ITEMS and K > 0:
+                self.item_pos = z(K, B, dt=torch.int16)
+                self.item_mask = z(2, B)
+                ptrs.update(item_pos=self.item_pos.data_ptr(), item_mask=self.item_mask.data_ptr())
         self._st = _lib.OrxState(**ptrs)
         self._pcfg, self._pst = ctypes.byref(self._ccfg), ctypes.byref(self._st)
         if self.mt_py is not None:
@@ -221,6 +233,11 @@ class BatchedEngine:
             out["p_layout"] = self.p_layout.cpu().numpy()
         if self.sep_start is not None:
             out["sep_start"] = self.sep_start.cpu().numpy()
+        if self.p_rpg is not None:
+            out["p_rpg"] = self.p_rpg.cpu().numpy()
+        if self.item_pos is not None:
+            out["item_pos"] = self.item_pos.cpu().numpy().view(np.uint16)
+            out["item_mask"] = self.item_mask.cpu().numpy().view(np.uint32)
         if self.mt_py is not None:
             for f in ("mt_py", "mt_np"):
                 out[f] = getattr(self, f).cpu().numpy().view(np.uint32)
@@ -242,6 +259,13 @@ class BatchedEngine:
             self.p_layout.copy_(torch.from_numpy(np.ascontiguousarray(snap["p_layout"], np.int16)))
         if self.sep_start is not None and "sep_start" in snap:
             self.sep_start.copy_(torch.from_numpy(np.ascontiguousarray(snap["sep_start"], np.int32)))
+        if self.p_rpg is not None and "p_rpg" in snap:
+            self.p_rpg.copy_(torch.from_numpy(np.ascontiguousarray(snap["p_rpg"], np.int32)))
+        if self.item_pos is not None and "item_pos" in snap:
+            self.item_pos.copy_(torch.from_numpy(
+                np.ascontiguousarray(snap["item_pos"]).astype(np.uint16).view(np.int16)))
+            self.item_mask.copy_(torch.from_numpy(
+                np.ascontiguousarray(snap["item_mask"]).astype(np.uint32).view(np.int32)))
         if self.mt_py is not None:
             for f in ("mt_py", "mt_np", "dstore"):
                 if f in snap:

@@ -64,6 +64,15 @@ STATUS_RNG_EXHAUSTED = 17
 # mechanics, off by default, parity unpinned
 EXT_SEPARATION_DAMAGE = 1
 EXT_RANDOM_DOUBLE_DEATH = 2
+# the readme's character mechanics (readme.md:44, 72, 74), parameters in EnvConfig
+EXT_MANA = 4          # up to 1/3 of the manabar converted into attack damage
+EXT_HEAL = 8          # MOVE_HEAL: a Stay converting up to 1/3 of the manabar into health
+EXT_LEVELING = 16     # experience per NPC kill; a level refills health and mana
+EXT_ITEMS = 32        # NPC drops with flat bonuses, picked up into finite item spots
+EXT_RPG = EXT_MANA | EXT_HEAL | EXT_LEVELING | EXT_ITEMS
+MOVE_HEAL = 6         # action code of a heal (EXT_HEAL only; not a reference Move)
+# rows of the p_rpg player-attribute tensor (include/orx.h ORX_RPG_*)
+RPG_FIELDS = ("mana", "xp", "damage", "max_health", "items")
 
 # EnvConfig.rng (orx_cfg_t.rng, include/orx.h ORX_RNG_*)
 RNG_PHILOX = 0

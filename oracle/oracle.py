@@ -20,7 +20,8 @@ LIB_PATH = os.path.join(HERE, "liborx_oracle.so")
 CFG_FIELDS = ["width", "height", "despawn", "max_ticks", "start_mode", "p1_depth", "p2_depth",
               "n_npcs", "npc_health", "npc_damage", "npc_armor", "player_health",
               "player_damage", "player_armor", "autoreset", "flags", "n_layouts", "sep_period",
-              "rng"]
+              "rng", "mana_max", "mana_regen", "mana_per_point", "xp_per_kill", "xp_per_level",
+              "item_drop_pct", "item_bonus", "item_slots"]
 
 
 class _Cfg(ctypes.Structure):
@@ -30,7 +31,8 @@ class _Cfg(ctypes.Structure):
 DEFAULT_CFG = dict(width=32, height=32, despawn=1, max_ticks=1000, start_mode=1, p1_depth=0,
                    p2_depth=0, n_npcs=0, npc_health=3, npc_damage=1, npc_armor=0,
                    player_health=10, player_damage=2, player_armor=1, autoreset=1, flags=0,
-                   n_layouts=0, sep_period=0, rng=0)
+                   n_layouts=0, sep_period=0, rng=0, mana_max=9, mana_regen=1, mana_per_point=1,
+                   xp_per_kill=1, xp_per_level=3, item_drop_pct=50, item_bonus=1, item_slots=3)
 
 _lib = None
 
@@ -70,6 +72,7 @@ def lib():
         L.oracle_export_layout.argtypes = [vp, vp]
         L.oracle_export_sep.argtypes = [vp, vp]
         L.oracle_seed_mt.argtypes = [vp, u64]
+        L.oracle_export_rpg.argtypes = [vp, vp, vp, vp]
         _lib = L
     return _lib
 
@@ -160,6 +163,15 @@ class Oracle:
         if self.layouts is not None:
             out["p_layout"] = np.zeros((2, B), np.int16)
             lib().oracle_export_layout(self._h, _ptr(out["p_layout"]))
+        if self.cfg["flags"] & 60:  # ORX_EXT_RPG: player attributes, items
+            out["p_rpg"] = np.zeros((5, 2, B), np.int32)
+            items = self.cfg["flags"] & 32 and K > 0
+            if items:
+                out["item_pos"] = np.zeros((K, B), np.uint16)
+                out["item_mask"] = np.zeros((2, B), np.uint32)
+            lib().oracle_export_rpg(self._h, _ptr(out["p_rpg"]),
+                                    _ptr(out["item_pos"]) if items else None,
+                                    _ptr(out["item_mask"]) if items else None)
         return out
 
     def world(self, g: int):

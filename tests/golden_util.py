@@ -83,15 +83,16 @@ class Fixture:
 def compare_state(got: dict, want: dict, K: int, where: str = ""):
     """Asserts bit-exact equality of every state field (NPC slots only if K;
     the bank layout of each player's depth when both sides carry it)."""
-    keys = STATE_KEYS + [k for k in ("p_layout", "sep_start") if k in got and k in want]
+    keys = STATE_KEYS + [k for k in ("p_layout", "sep_start", "p_rpg", "item_mask", "item_pos")
+                         if k in got and k in want]
     for k in keys:
         if k.startswith("npc") and K == 0:
             continue
         g = np.asarray(got[k])
         w = np.asarray(want[k])
-        if k in ("npc_pos", "npc_health"):
-            # dead NPC slots are unspecified: compare alive slots only
-            alive = np.asarray(want["npc_alive"])
+        if k in ("npc_pos", "npc_health", "item_pos"):
+            # dead NPC slots / taken items are unspecified: compare live slots only
+            alive = np.asarray(want["item_mask"][0] if k == "item_pos" else want["npc_alive"])
             mask = ((alive[None, :] >> np.arange(K)[:, None]) & 1).astype(bool)
             g = np.where(mask, g, 0)
             w = np.where(mask, w, 0)
