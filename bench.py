@@ -270,6 +270,15 @@ def extras(torch, cfg, dev, B_cfg, K, large_rollout=False):
                                     65536, 1),
                        policy="2x RandomBot", grid="64x64, 16 layouts (15% walls)",
                        note="tiles staged in LDS (64 KiB)")
+    # configs[2] read literally, "64x64 grid with enemies+items enabled": C3 with
+    # the readme's character mechanics on (build extensions, no reference
+    # semantics, so not the bit-exact headline)
+    from optimax_rogue_amd.enums import EXT_RPG
+    out["c3_rpg"] = dict(rollout_rate(EnvConfig(width=64, height=64, n_npcs=8, flags=EXT_RPG),
+                                      65536, 1),
+                         policy="2x RandomBot", grid="64x64, 8 NPCs",
+                         note="mana, heal, experience, item drops/pickup on (EXT_RPG; engine "
+                              "vs oracle bit-exact, parity unpinned vs the reference)")
     c5 = {}
     for flag in (0, EXT_SEPARATION_DAMAGE):
         c = EnvConfig.c5()

@@ -133,6 +133,27 @@ extern "C" {
    takes it if it holds fewer than item_slots items: damage or max health
    (and health) += item_bonus                                              */
 #define ORX_EXT_RPG (ORX_EXT_MANA | ORX_EXT_HEAL | ORX_EXT_LEVELING | ORX_EXT_ITEMS)
+#define ORX_EXT_README_COMBAT 64 /* the readme's combat table (readme.md:69-70)
+   instead of handle_move's player-vs-player rules (updater.py:218-243), as
+   one simultaneous resolution before the moves (NPC combat unchanged).  With
+   a, b the players' cells and ta, tb their targets on one depth (a move
+   attacks the other's cell, or the cell both move into):
+     both attack each other's cell       -> each takes half the other's
+                                            damage, both stay, both get
+                                            combat_cooldown ticks of cooldown;
+     both move into one cell             -> each takes the other's full
+                                            damage, both stay;
+     A attacks b, B stays (or heals)     -> negated and A is stunned (1 tick
+                                            of cooldown), unless B is on
+                                            cooldown: then full damage;
+     A attacks b, B moves elsewhere      -> no damage.
+   An attacker never moves.  A player on cooldown cannot attack (an attack is
+   a Stay) nor defend.  Damage = damage - armor (+ mana with ORX_EXT_MANA,
+   spent only by an attack that deals damage).  Combat events: both-attack
+   PARRY, one-cell AMBUSH, stay BLOCK, moved-away FLEE.  State:
+   p_rpg row ORX_RPG_COOLDOWN                                              */
+/* the extensions that keep per-player attributes in orx_state_t.p_rpg       */
+#define ORX_EXT_CHARACTER (ORX_EXT_RPG | ORX_EXT_README_COMBAT)
 
 /* player attributes of the character mechanics: rows of orx_state_t.p_rpg  */
 #define ORX_RPG_MANA 0
@@ -140,7 +161,8 @@ extern "C" {
 #define ORX_RPG_DAMAGE 2      /* Entity.damage (base + damage items)         */
 #define ORX_RPG_MAX_HEALTH 3  /* Entity.max_health (base + health items)     */
 #define ORX_RPG_ITEMS 4       /* items held                                  */
-#define ORX_RPG_FIELDS 5
+#define ORX_RPG_COOLDOWN 5    /* ORX_EXT_README_COMBAT: ticks of cooldown left */
+#define ORX_RPG_FIELDS 6
 #define ORX_MOVE_HEAL 6       /* ORX_EXT_HEAL only                           */
 
 /* per-game event counters (rows of orx_state_t.counters)                    */
@@ -224,6 +246,8 @@ typedef struct orx_cfg {
   int32_t item_drop_pct;  /* 0..100: chance a dying NPC drops an item        */
   int32_t item_bonus;     /* flat attribute bonus of an item                 */
   int32_t item_slots;     /* items a player can hold                         */
+  int32_t combat_cooldown;/* ORX_EXT_README_COMBAT: ticks after a mutual
+                             attack (readme.md:69: 3)                        */
 } orx_cfg_t;
 
 /* ---- batch state (SoA, batch axis contiguous; all device pointers) ------- */
@@ -265,7 +289,7 @@ typedef struct orx_state {
                                    (layout + 1) << 16} of entered dungeons,
                                    slot depth % ORX_DSTORE (the staircases a
                                    keyed stream would regenerate)            */
-  /* character mechanics (any ORX_EXT_RPG flag; NULL otherwise)              */
+  /* character mechanics (any ORX_EXT_CHARACTER flag; NULL otherwise)        */
   int32_t* p_rpg;               /* [ORX_RPG_FIELDS][2][B] player attributes   */
   uint16_t* item_pos;           /* [K][B] ORX_EXT_ITEMS: item dropped by NPC
                                    slot k, x | y << 8 (on the NPCs' depth)    */

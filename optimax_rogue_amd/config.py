@@ -24,7 +24,7 @@ CFG_FIELDS = ("width", "height", "despawn", "max_ticks", "start_mode", "p1_depth
               "n_npcs", "npc_health", "npc_damage", "npc_armor", "player_health",
               "player_damage", "player_armor", "autoreset", "flags", "n_layouts", "sep_period",
               "rng", "mana_max", "mana_regen", "mana_per_point", "xp_per_kill", "xp_per_level",
-              "item_drop_pct", "item_bonus", "item_slots")
+              "item_drop_pct", "item_bonus", "item_slots", "combat_cooldown")
 
 
 class OrxCfg(ctypes.Structure):
@@ -66,6 +66,7 @@ class EnvConfig:
     item_drop_pct: int = 50         # chance (%) that a dying NPC drops an item
     item_bonus: int = 1             # flat bonus of an item (damage or max health)
     item_slots: int = 3             # items a player can hold
+    combat_cooldown: int = 3        # EXT_README_COMBAT: ticks after a mutual attack (readme: 3)
     # explicit-grid dungeon generator: [L, W, H] Tile codes (None =
     # EmptyDungeonGenerator).  spawn_dungeon(depth) returns layout randint(L).
     layouts: Optional[np.ndarray] = dataclasses.field(default=None, repr=False, compare=False)

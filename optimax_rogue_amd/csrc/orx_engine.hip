@@ -170,6 +170,7 @@ struct Player {
   // character mechanics (ORX_EXT_RPG; never touched by the kernels that are
   // compiled with those flags known off)
   int32_t mana, xp, dmg, mhp, nitems;
+  int32_t cool;   // ORX_EXT_README_COMBAT: ticks of cooldown left
   int32_t heal;   // this tick's move is ORX_MOVE_HEAL (a Stay)
   int32_t hd;     // damage of this tick's hit on an NPC
 };
@@ -193,6 +194,7 @@ __device__ __forceinline__ Player pick(bool c, const Player& a, const Player& b)
   r.dmg = c ? a.dmg : b.dmg;
   r.mhp = c ? a.mhp : b.mhp;
   r.nitems = c ? a.nitems : b.nitems;
+  r.cool = c ? a.cool : b.cool;
   r.heal = c ? a.heal : b.heal;
   r.hd = c ? a.hd : b.hd;
   return r;
@@ -204,7 +206,7 @@ struct Cfg {  // device copy of orx_cfg_t plus derived constants (all wave-unifo
   int32_t ext, sep_period;  // ORX_EXT_* build extensions (0 in FAST kernels)
   // character mechanics (ORX_EXT_RPG)
   int32_t player_dmg, player_armor, mana_max, mana_third, mana_regen, mana_pp;
-  int32_t xp_kill, xp_level, drop_pct, item_bonus, item_slots;
+  int32_t xp_kill, xp_level, drop_pct, item_bonus, item_slots, cooldown;
   int32_t ih;        // H - 2 (interior column height)
   // ceil(2^32 / d) for d = ih and d = H: n / d == umulhi(n, magic) for every
   // n < 2^16 (error < n / 2^32 <= 1/d), so set only when the dividends
@@ -320,6 +322,12 @@ struct Npcs {
       }
       return hitmask ? (int)__builtin_ctz(hitmask) : -1;
     }
+  }
+  // A live NPC holds `key` (with ORX_EXT_ITEMS a slot may hold its dropped
+  // item instead; keys of occupied slots are distinct).
+  __device__ __forceinline__ bool live(uint32_t key) const {
+    const int k = find(key);
+    return k >= 0 && ((alive >> k) & 1u);
   }
   // slot k := dead for a runtime k: 64-bit shifts over register pairs (a
   // switch on k lowers to a branch ladder)
@@ -692,6 +700,7 @@ __device__ __forceinline__ void setup_game(const Cfg& c, Key key, Src& src, Play
   p1.dmg = p2.dmg = c.player_dmg;
   p1.mhp = p2.mhp = c.player_hp;
   p1.nitems = p2.nitems = 0;
+  p1.cool = p2.cool = 0;
   tick = kStartTick;
   status = err ? ORX_STATUS_RNG_EXHAUSTED : ORX_IN_PROGRESS;
 }
@@ -760,7 +769,7 @@ __device__ __forceinline__ void descend(const Cfg& c, Key key, Src& src, Player&
       if (v <= gb.rng) {
         ground_cell<GRID>(c, v, lay, sx, sy, x, y);
         bool occ = other.d == nd && other.x == x && other.y == y;
-        if (npc_depth) occ = occ || npc.find(pack_xy(x, y)) >= 0;
+        if (npc_depth) occ = occ || npc_on(c, npc, pack_xy(x, y));
         done = !occ;
         if (done) {  // the stream now stands after its first word
           spawn.w = w;
@@ -777,7 +786,7 @@ __device__ __forceinline__ void descend(const Cfg& c, Key key, Src& src, Player&
     }
     ground_cell<GRID>(c, v, lay, sx, sy, x, y);
     bool occ = other.d == nd && other.x == x && other.y == y;
-    if (npc_depth) occ = occ || npc.find(pack_xy(x, y)) >= 0;
+    if (npc_depth) occ = occ || npc_on(c, npc, pack_xy(x, y));
     done = !occ;
   }
   if (!done) err = true;
@@ -993,14 +1002,22 @@ struct NpcHpRegs {
 // Character mechanics (ORX_EXT_MANA / HEAL / LEVELING / ITEMS; readme.md:44,
 // 72, 74 -- no reference code, parameters in orx_cfg_t, include/orx.h)
 // ---------------------------------------------------------------------------
-// Items on the floor of the NPCs' depth: slot k holds the item NPC k dropped,
-// packed like the NPC slots (dead = 0xFFFF), kind bit k: 1 = max health.
+// Items on the floor of the NPCs' depth.  The item NPC k dropped lies on its
+// cell and inherits its slot register (a slot holds a live NPC, its item or
+// nothing), so the one slot scan of a tick tests targets for both: `on` bit k
+// = slot k holds an item, `kind` bit k: 1 = max health.
 template <int NCAP>
 struct Items {
-  Npcs<NCAP> pos;
-  uint32_t kind;
-  __device__ __forceinline__ void clear() { pos.clear(); kind = 0; }
+  uint32_t on, kind;
+  __device__ __forceinline__ void clear() { on = kind = 0; }
 };
+
+// A live NPC stands on `key` (NPC occupancy for moves and spawn cells): with
+// items in the slots the slot must be a live NPC's.
+template <int NCAP>
+__device__ __forceinline__ bool npc_on(const Cfg& c, const Npcs<NCAP>& npc, uint32_t key) {
+  return (c.ext & ORX_EXT_ITEMS) ? npc.live(key) : npc.any(key);
+}
 
 // Whole points from up to a third of the manabar, at most `cap` of them.
 __device__ __forceinline__ int32_t mana_points(const Cfg& c, int32_t mana, int32_t cap) {
@@ -1035,11 +1052,12 @@ __device__ __forceinline__ void gain_xp(const Cfg& c, Player& p) {
 // its item (one Philox block of purpose ITEM, block index = slot).
 template <int NCAP>
 __device__ __forceinline__ void drop_item(const Cfg& c, Key key, uint32_t game, uint32_t ep,
-                                          int32_t tick, int k, uint32_t cell, Items<NCAP>& it) {
+                                          int32_t tick, int k, uint32_t cell, Npcs<NCAP>& npc,
+                                          Items<NCAP>& it) {
   const W4 w = philox(game, ep, (uint32_t)tick, tag(PUR_ITEM, 0) | (uint32_t)k, key);
   if ((int32_t)__umulhi(w.a, 100u) < c.drop_pct) {
-    it.pos.set(k, cell);
-    it.pos.alive |= 1u << k;
+    npc.set(k, cell);
+    it.on |= 1u << k;
     it.kind = (it.kind & ~(1u << k)) | ((w.b & 1u) << k);
   }
 }
@@ -1047,12 +1065,13 @@ __device__ __forceinline__ void drop_item(const Cfg& c, Key key, uint32_t game, 
 // ORX_EXT_ITEMS: a player that stepped onto an item's cell takes it when it
 // has a free item spot.
 template <int NCAP>
-__device__ __forceinline__ void pick_up(const Cfg& c, Player& self, Items<NCAP>& it) {
-  const int k = it.pos.find(pack_xy(self.x, self.y));
-  if (k >= 0 && self.nitems < c.item_slots) {
+__device__ __forceinline__ void pick_up(const Cfg& c, Player& self, Npcs<NCAP>& npc,
+                                        Items<NCAP>& it) {
+  const int k = npc.find(pack_xy(self.x, self.y));
+  if (k >= 0 && ((it.on >> k) & 1u) && self.nitems < c.item_slots) {
     const bool health_item = (it.kind >> k) & 1u;
-    it.pos.alive &= ~(1u << k);
-    it.pos.kill(k);
+    it.on &= ~(1u << k);
+    npc.kill(k);
     it.kind &= ~(1u << k);
     self.nitems += 1;
     if (health_item) {
@@ -1064,13 +1083,83 @@ __device__ __forceinline__ void pick_up(const Cfg& c, Player& self, Items<NCAP>&
   }
 }
 
+// ORX_EXT_README_COMBAT (readme.md:69-70): the players' combat as one
+// simultaneous resolution before the moves (include/orx.h has the table); an
+// attacker becomes a Stay, damage is applied here; NPC combat is left to
+// handle_move.  Called with player 1 then player 2 (event order).
+__device__ __forceinline__ void make_stay(Player& p) {
+  p.move = ORX_MOVE_STAY;
+  p.tx = p.x;
+  p.ty = p.y;
+}
+
+template <bool EV>
+__device__ __forceinline__ void readme_combat(const Cfg& c, Player& a, Player& b, Deltas& dl,
+                                              Events<EV>& ev) {
+  const bool cda = a.cool > 0, cdb = b.cool > 0;  // this tick's cooldowns
+  a.cool = max(a.cool - 1, 0);
+  b.cool = max(b.cool - 1, 0);
+  if (a.d != b.d) return;
+  bool amov = a.move != ORX_MOVE_STAY, bmov = b.move != ORX_MOVE_STAY;
+  // on cooldown an attack is measured as a Stay
+  if (cda && amov && ((a.tx == b.x && a.ty == b.y) || (bmov && a.tx == b.tx && a.ty == b.ty))) {
+    make_stay(a);
+    amov = false;
+  }
+  if (cdb && bmov && ((b.tx == a.x && b.ty == a.y) || (amov && b.tx == a.tx && b.ty == a.ty))) {
+    make_stay(b);
+    bmov = false;
+  }
+  const bool a_cur = amov && a.tx == b.x && a.ty == b.y;
+  const bool b_cur = bmov && b.tx == a.x && b.ty == a.y;
+  const bool same = amov && bmov && a.tx == b.tx && a.ty == b.ty;
+  if (a_cur && b_cur) {  // both attack the other's cell: half damage, cooldown
+    const int32_t da = rpg_attack(c, a) / 2, db = rpg_attack(c, b) / 2;
+    b.hp -= da;
+    a.hp -= db;
+    a.cool = b.cool = c.cooldown;
+    make_stay(a);
+    make_stay(b);
+    dl.combat += 2;
+    ev.emit(ORX_EV_COMBAT, 1, 2, ORX_FLAG_PARRY);
+    ev.emit(ORX_EV_COMBAT, 2, 1, ORX_FLAG_PARRY);
+    return;
+  }
+  if (same) {  // both into one cell: full damage
+    const int32_t da = rpg_attack(c, a), db = rpg_attack(c, b);
+    b.hp -= da;
+    a.hp -= db;
+    make_stay(a);
+    make_stay(b);
+    dl.combat += 2;
+    ev.emit(ORX_EV_COMBAT, 1, 2, ORX_FLAG_AMBUSH);
+    ev.emit(ORX_EV_COMBAT, 2, 1, ORX_FLAG_AMBUSH);
+    return;
+  }
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {  // one-sided: the attacker stays
+    Player& t = s ? b : a;
+    Player& v = s ? a : b;
+    if (!(s ? b_cur : a_cur)) continue;
+    const bool v_moves = v.move != ORX_MOVE_STAY, v_cd = s ? cda : cdb;
+    if (!v_moves && v_cd) {
+      v.hp -= rpg_attack(c, t);  // cannot defend: full damage
+    } else if (!v_moves) {
+      t.cool = max(t.cool, 1);   // negated; the attacker cannot attack or defend next tick
+    }
+    ev.emit(ORX_EV_COMBAT, s ? 2 : 1, s ? 1 : 2, v_moves ? ORX_FLAG_FLEE : ORX_FLAG_BLOCK);
+    dl.combat += 1;
+    make_stay(t);
+  }
+}
+
 // handle_move for `self` (updater.py:180-243), branch-free except for the
 // rare descend.  Returns true if the target cell holds an NPC (the slot is
 // resolved in npc_hits); combat against the other player is applied here.
 template <int NCAP, bool EV, bool GRID, class Src, class S>
 __device__ __forceinline__ bool handle_move(const Cfg& c, Key key, Src& src, Player& self,
                                             Player& other, int32_t other_start,
-                                            const Npcs<NCAP>& npc, Items<NCAP>& items,
+                                            Npcs<NCAP>& npc, Items<NCAP>& items,
                                             S& spawn, Deltas& dl, bool& err, int32_t self_iden,
                                             bool self_first, Events<EV>& ev) {
   if ((c.ext & ORX_EXT_HEAL) && self.heal && self.hp > 0) {  // readme.md:74
@@ -1084,7 +1173,7 @@ __device__ __forceinline__ bool handle_move(const Cfg& c, Key key, Src& src, Pla
   const bool occ_other = moving && other.d == self.d && other.x == tx && other.y == ty;
   // bitwise, not short-circuit: no branch around the slot scan
   const bool hit_npc = NCAP > 0 && (moving & !occ_other & (self.d == c.d1) &
-                                    npc.any(pack_xy(tx, ty)));
+                                    npc_on(c, npc, pack_xy(tx, ty)));
   const bool free = moving && !occ_other && !hit_npc;
   const bool stairs = free && stair_tile<GRID>(c, self, tx, ty);
   const bool step = free && !stairs;
@@ -1097,7 +1186,8 @@ __device__ __forceinline__ bool handle_move(const Cfg& c, Key key, Src& src, Pla
   if (c.ext & ORX_EXT_RPG) dmg = (occ_other || hit_npc) ? rpg_attack(c, self) : 0;
   other.hp -= occ_other ? dmg : 0;
   self.hd = dmg;  // an NPC hit's damage, applied by npc_hits after both moves
-  if (NCAP > 0 && (c.ext & ORX_EXT_ITEMS) && step && self.d == c.d1) pick_up(c, self, items);
+  if (NCAP > 0 && (c.ext & ORX_EXT_ITEMS) && step && self.d == c.d1)
+    pick_up(c, self, npc, items);
   if constexpr (EV) {
     if (occ_other) {
       int32_t ox, oy;
@@ -1169,6 +1259,11 @@ __device__ __forceinline__ void tick_game(const Cfg& c, Key key, Src& src, uint3
   if (blocked<GRID>(c, p1.lay, p1.tx, p1.ty)) p1.move = ORX_MOVE_STAY;
   calc_pos(p2.x, p2.y, p2.move, p2.tx, p2.ty);
   if (blocked<GRID>(c, p2.lay, p2.tx, p2.ty)) p2.move = ORX_MOVE_STAY;
+  if (c.ext & ORX_EXT_README_COMBAT) {  // the readme's combat table, before the moves
+    if (p1.move == ORX_MOVE_STAY) make_stay(p1);
+    if (p2.move == ORX_MOVE_STAY) make_stay(p2);
+    readme_combat(c, p1, p2, dl, ev);
+  }
 
   // p1_first: the player shuffle (updater.py:114).  The NPC shuffle (:127)
   // draws later words of the same per-tick stream and only orders Stay-ing
@@ -1194,9 +1289,9 @@ __device__ __forceinline__ void tick_game(const Cfg& c, Key key, Src& src, uint3
       if ((c.ext & ORX_EXT_LEVELING) && kA) gain_xp(c, A);
       if ((c.ext & ORX_EXT_LEVELING) && kB) gain_xp(c, Bp);
       if ((c.ext & ORX_EXT_ITEMS) && kA)
-        drop_item(c, key, game, ep, tick, h0, pack_xy(A.tx, A.ty), items);
+        drop_item(c, key, game, ep, tick, h0, pack_xy(A.tx, A.ty), npc, items);
       if ((c.ext & ORX_EXT_ITEMS) && kB)
-        drop_item(c, key, game, ep, tick, h1, pack_xy(Bp.tx, Bp.ty), items);
+        drop_item(c, key, game, ep, tick, h1, pack_xy(Bp.tx, Bp.ty), npc, items);
     }
   }
   p1 = pick(p1_first, A, Bp);
@@ -1257,12 +1352,13 @@ __device__ __forceinline__ void tick_game(const Cfg& c, Key key, uint32_t game, 
 // kernels that know the flags are off).
 template <int NCAP>
 __device__ __forceinline__ void load_rpg(const orx_state_t& st, const Cfg& c, uint32_t B,
-                                         uint32_t i, Player& p1, Player& p2, Items<NCAP>& it) {
+                                         uint32_t i, Player& p1, Player& p2, Npcs<NCAP>& npc,
+                                         Items<NCAP>& it) {
   it.clear();
   p1.heal = p2.heal = 0;
   p1.hd = p2.hd = 0;
-  if (!(c.ext & ORX_EXT_RPG)) {
-    p1.mana = p2.mana = p1.xp = p2.xp = p1.nitems = p2.nitems = 0;
+  if (!(c.ext & ORX_EXT_CHARACTER)) {
+    p1.mana = p2.mana = p1.xp = p2.xp = p1.nitems = p2.nitems = p1.cool = p2.cool = 0;
     p1.dmg = p2.dmg = c.player_dmg;
     p1.mhp = p2.mhp = c.player_hp;
     return;
@@ -1274,12 +1370,13 @@ __device__ __forceinline__ void load_rpg(const orx_state_t& st, const Cfg& c, ui
   p1.dmg = r[ORX_RPG_DAMAGE * f];          p2.dmg = r[ORX_RPG_DAMAGE * f + B];
   p1.mhp = r[ORX_RPG_MAX_HEALTH * f];      p2.mhp = r[ORX_RPG_MAX_HEALTH * f + B];
   p1.nitems = r[ORX_RPG_ITEMS * f];        p2.nitems = r[ORX_RPG_ITEMS * f + B];
+  p1.cool = r[ORX_RPG_COOLDOWN * f];       p2.cool = r[ORX_RPG_COOLDOWN * f + B];
   if constexpr (NCAP > 0) {
-    if (c.ext & ORX_EXT_ITEMS) {
-      it.pos.alive = st.item_mask[i];
+    if (c.ext & ORX_EXT_ITEMS) {  // (after load_npcs) items into their NPCs' slots
+      it.on = st.item_mask[i];
       it.kind = st.item_mask[B + i];
       for (int k = 0; k < c.K; ++k)
-        if ((it.pos.alive >> k) & 1u) it.pos.set(k, st.item_pos[(size_t)k * B + i]);
+        if ((it.on >> k) & 1u) npc.set(k, st.item_pos[(size_t)k * B + i]);
     }
   }
 }
@@ -1287,8 +1384,8 @@ __device__ __forceinline__ void load_rpg(const orx_state_t& st, const Cfg& c, ui
 template <int NCAP>
 __device__ __forceinline__ void store_rpg(const orx_state_t& st, const Cfg& c, uint32_t B,
                                           uint32_t i, const Player& p1, const Player& p2,
-                                          const Items<NCAP>& it) {
-  if (!(c.ext & ORX_EXT_RPG)) return;
+                                          const Npcs<NCAP>& npc, const Items<NCAP>& it) {
+  if (!(c.ext & ORX_EXT_CHARACTER)) return;
   int32_t* r = st.p_rpg + i;
   const size_t f = 2 * (size_t)B;
   r[ORX_RPG_MANA * f] = p1.mana;           r[ORX_RPG_MANA * f + B] = p2.mana;
@@ -1296,12 +1393,13 @@ __device__ __forceinline__ void store_rpg(const orx_state_t& st, const Cfg& c, u
   r[ORX_RPG_DAMAGE * f] = p1.dmg;          r[ORX_RPG_DAMAGE * f + B] = p2.dmg;
   r[ORX_RPG_MAX_HEALTH * f] = p1.mhp;      r[ORX_RPG_MAX_HEALTH * f + B] = p2.mhp;
   r[ORX_RPG_ITEMS * f] = p1.nitems;        r[ORX_RPG_ITEMS * f + B] = p2.nitems;
+  r[ORX_RPG_COOLDOWN * f] = p1.cool;       r[ORX_RPG_COOLDOWN * f + B] = p2.cool;
   if constexpr (NCAP > 0) {
     if (c.ext & ORX_EXT_ITEMS) {
-      st.item_mask[i] = it.pos.alive;
+      st.item_mask[i] = it.on;
       st.item_mask[B + i] = it.kind;
       for (int k = 0; k < c.K; ++k)
-        if ((it.pos.alive >> k) & 1u) st.item_pos[(size_t)k * B + i] = (uint16_t)it.pos.get(k);
+        if ((it.on >> k) & 1u) st.item_pos[(size_t)k * B + i] = (uint16_t)npc.get(k);
     }
   }
 }
@@ -1412,6 +1510,7 @@ __device__ __forceinline__ Cfg make_cfg(const orx_cfg_t& h, const orx_state_t& s
   c.mana_pp = h.mana_per_point > 0 ? h.mana_per_point : 1;
   c.xp_kill = h.xp_per_kill; c.xp_level = h.xp_per_level > 0 ? h.xp_per_level : 1;
   c.drop_pct = h.item_drop_pct; c.item_bonus = h.item_bonus; c.item_slots = h.item_slots;
+  c.cooldown = h.combat_cooldown;
   c.ih = h.height - 2;
   c.ih_magic = (int64_t)(h.width - 2) * (h.height - 2) <= 65536
                    ? (uint32_t)(0xFFFFFFFFu / (uint32_t)c.ih + 1u) : 0u;
@@ -1455,7 +1554,7 @@ __global__ void __launch_bounds__(256) reset_kernel(orx_cfg_t hc, orx_state_t st
   store_players<GRID>(st, B, i, p1, p2, true);
   Items<NCAP> items;
   items.clear();
-  store_rpg(st, c, B, i, p1, p2, items);
+  store_rpg(st, c, B, i, p1, p2, npc, items);
   st.tick[i] = tick;
   st.status[i] = status;
   if (c.ext & ORX_EXT_SEPARATION_DAMAGE) st.sep_start[i] = -1;
@@ -1487,7 +1586,7 @@ __global__ void __launch_bounds__(256) step_kernel(orx_cfg_t hc, orx_state_t st,
     store_players<GRID>(st, B, i, p1, p2, true);
     Items<NCAP> items;
     items.clear();
-    store_rpg(st, c, B, i, p1, p2, items);
+    store_rpg(st, c, B, i, p1, p2, npc, items);
     st.tick[i] = tick;
     st.status[i] = status;
     st.episode[i] = (int32_t)ep;
@@ -1511,7 +1610,7 @@ __global__ void __launch_bounds__(256) step_kernel(orx_cfg_t hc, orx_state_t st,
   load_players<GRID>(st, B, i, p1, p2);
   load_npcs(st, c, B, i, npc);
   Items<NCAP> items;
-  load_rpg(st, c, B, i, p1, p2, items);
+  load_rpg(st, c, B, i, p1, p2, npc, items);
   NpcMem m{st.npc_pos, st.npc_health, B, i};
   Deltas dl = {0, 0, 0, 0, 0, 0};
   Events<EV> ev{EV ? events + (size_t)i * ORX_MAX_EVENTS * 4 : nullptr, 0};
@@ -1521,7 +1620,7 @@ __global__ void __launch_bounds__(256) step_kernel(orx_cfg_t hc, orx_state_t st,
   tick_game<NCAP, EV, GRID>(c, key, game, ep, p1_first, p1, p2, npc, items, m, tick, status, err,
                             dl, ev, sep);
   if (c.ext & ORX_EXT_SEPARATION_DAMAGE) st.sep_start[i] = sep;
-  store_rpg(st, c, B, i, p1, p2, items);
+  store_rpg(st, c, B, i, p1, p2, npc, items);
   store_players<GRID>(st, B, i, p1, p2, dl.descend != 0);
   st.tick[i] = tick;
   st.status[i] = status;
@@ -1680,8 +1779,11 @@ __device__ __forceinline__ void rollout_tick(const Cfg& c, const orx_state_t& st
   const bool hit2 = NCAP > 0 && ((p2.d == c.d1) & n2);
   const bool st1 = GRID ? g_st1 : stair_tile<GRID>(c, p1, t1x, t1y);
   const bool st2 = GRID ? g_st2 : stair_tile<GRID>(c, p2, t2x, t2y);
-  const bool ext_ordered = (c.ext & ~ORX_EXT_SEPARATION_DAMAGE) != 0;  // uniform
-  // The rare games: finished, or a meet, an NPC hit, a staircase, an
+  const bool ext_ordered =  // uniform
+      (c.ext & ~(ORX_EXT_SEPARATION_DAMAGE | ORX_EXT_CHARACTER)) != 0;
+  // (ORX_EXT_ITEMS: items sit in their NPCs' slot registers, so hit1 / hit2
+  // also flag a target holding an item -- a rare game, sorted out below)
+  // The rare games: finished, or a meet, an NPC hit, a staircase, an item, an
   // extension that needs the literal sequence.  Only this union is formed
   // here; the rare block re-derives its parts (from laundered inputs, so they
   // are not kept live across the common path as 0/1 values).  The initiative
@@ -1713,11 +1815,17 @@ __device__ __forceinline__ void rollout_tick(const Cfg& c, const orx_state_t& st
                                (uint32_t)(t1x ^ t2x) | (uint32_t)(t1y ^ t2y)))) == 0u;
     const uint32_t k1 = (uint32_t)t1x | ((uint32_t)t1y << 8);
     const uint32_t k2 = (uint32_t)t2x | ((uint32_t)t2y << 8);
-    const bool hit1 = NCAP > 0 && (p1.d == c.d1) && npc.any(k1);
-    const bool hit2 = NCAP > 0 && (p2.d == c.d1) && npc.any(k2);
+    const bool hit1 = NCAP > 0 && (p1.d == c.d1) && npc_on(c, npc, k1);
+    const bool hit2 = NCAP > 0 && (p2.d == c.d1) && npc_on(c, npc, k2);
     const bool st1 = stair_tile<GRID>(c, p1, t1x, t1y), st2 = stair_tile<GRID>(c, p2, t2x, t2y);
-    const bool full0 = (meet & (st1 | st2)) | (st1 & st2) | ext_ordered;
     const bool desc_meet = (st1 & (p2.d == p1.d + 1)) | (st2 & (p1.d == p2.d + 1));
+    // the character mechanics (ORX_EXT_RPG) keep the common path's rules:
+    // each attacker's own mana and damage, NPC hits and the kill credit in the
+    // drawn order, steps onto items; a descend-meet (whose clash would undo a
+    // step) takes the ordered tick
+    const bool rpg_ordered = ((c.ext & ORX_EXT_CHARACTER) && desc_meet) ||
+                             ((c.ext & ORX_EXT_README_COMBAT) && meet);
+    const bool full0 = (meet & (st1 | st2)) | (st1 & st2) | ext_ordered | rpg_ordered;
     // the games that use the initiative order: the ordered tick, a meet, a
     // descend into the other's depth
     const bool ordered_use = in_progress & (full0 | meet | desc_meet);
@@ -1801,16 +1909,38 @@ __device__ __forceinline__ void rollout_tick(const Cfg& c, const orx_state_t& st
         }
         if (clash) deaths_over(p1, p2, end, status, dl);
       }
+      bool kc1 = false, kc2 = false;  // ORX_EXT_LEVELING: each player's kill this tick
       if (NCAP > 0 && (hit1 | hit2)) {  // NPCs are swept after both moves
 #ifdef ORX_STAMPS
         ORX_COUNT(dl.n_hits);
 #endif
         Events<false> ev{nullptr, 0};
         dl.combat += (hit1 ? 1 : 0) + (hit2 ? 1 : 0);
-        const int32_t dmg = c.player_dmg_net > 0 ? c.player_dmg_net : 0;
-        bool kc0, kc1;  // (kill credit: the character mechanics take the ordered tick)
-        npc_hits(c, npc, hp, hit1 ? npc.find(k1) : -1, hit2 ? npc.find(k2) : -1, dmg, dmg, dl,
-                 ev, kc0, kc1);
+        int32_t d1 = c.player_dmg_net > 0 ? c.player_dmg_net : 0, d2 = d1;
+        if (c.ext & ORX_EXT_RPG) {  // each attacker's own damage and mana
+          d1 = hit1 ? rpg_attack(c, p1) : 0;
+          d2 = hit2 ? rpg_attack(c, p2) : 0;
+        }
+        const int h1 = hit1 ? npc.find(k1) : -1, h2 = hit2 ? npc.find(k2) : -1;
+        if (c.ext & ORX_EXT_RPG) {
+          // hits in the drawn order: one NPC hit by both (a meet) credits the
+          // hit that takes it to zero
+          bool sw = false;
+          if (lean) {
+            const uint32_t sa = ~(pk_shf >> 1) & 0x55555555u;
+            sw = ((pk_shf >> __builtin_ctz(sa)) & 1u) == 0;
+          }
+          bool ka = false, kb = false;
+          npc_hits(c, npc, hp, sw ? h2 : h1, sw ? h1 : h2, sw ? d2 : d1, sw ? d1 : d2, dl, ev,
+                   ka, kb);
+          kc1 = sw ? kb : ka;
+          kc2 = sw ? ka : kb;
+          if ((c.ext & ORX_EXT_ITEMS) && kc1) drop_item(c, key, game, ep, t0, h1, k1, npc, items);
+          if ((c.ext & ORX_EXT_ITEMS) && kc2) drop_item(c, key, game, ep, t0, h2, k2, npc, items);
+        } else {
+          // two hits are then order-free: only the health left matters
+          npc_hits(c, npc, hp, h1, h2, d1, d2, dl, ev, kc1, kc2);
+        }
       }
       if (lean) {  // a meet: the two moves in the drawn order
 #ifdef ORX_STAMPS
@@ -1832,10 +1962,33 @@ __device__ __forceinline__ void rollout_tick(const Cfg& c, const orx_state_t& st
         p1.y = p1_first ? fy : sy;
         p2.x = p1_first ? sx : fx;
         p2.y = p1_first ? sy : fy;
-        p1.hp -= (p1_first ? occs : occf) ? dmg : 0;
-        p2.hp -= (p1_first ? occf : occs) ? dmg : 0;
+        if (NCAP > 0 && (c.ext & ORX_EXT_ITEMS)) {  // the meet's steps onto items (a
+          // health item may save a player hit in the tick: before the win check)
+          if ((p1.d == c.d1) & ((p1.x != x1o) | (p1.y != y1o))) pick_up(c, p1, npc, items);
+          if ((p2.d == c.d1) & ((p2.x != x2o) | (p2.y != y2o))) pick_up(c, p2, npc, items);
+        }
+        if (c.ext & ORX_EXT_RPG) {  // each attacker's own damage and mana
+          const bool a1 = p1_first ? occf : occs, a2 = p1_first ? occs : occf;
+          const int32_t e1 = a1 ? rpg_attack(c, p1) : 0, e2 = a2 ? rpg_attack(c, p2) : 0;
+          p2.hp -= e1;
+          p1.hp -= e2;
+        } else {
+          p1.hp -= (p1_first ? occs : occf) ? dmg : 0;
+          p2.hp -= (p1_first ? occf : occs) ? dmg : 0;
+        }
         dl.combat += (occf ? 1 : 0) + (occs ? 1 : 0);
         deaths_over(p1, p2, end, status, dl);
+      }
+      // the sweep's experience after every combat of the tick: a player the
+      // other killed in a meet is not refilled
+      if (NCAP > 0 && (c.ext & ORX_EXT_LEVELING)) {
+        if (kc1) gain_xp(c, p1);
+        if (kc2) gain_xp(c, p2);
+      }
+      if (NCAP > 0 && (c.ext & ORX_EXT_ITEMS) && !lean) {  // a step onto an item takes it
+        // (readme.md:44; a meet's steps were taken above)
+        if (!st1 & (p1.d == c.d1) & ((p1.x != x1o) | (p1.y != y1o))) pick_up(c, p1, npc, items);
+        if (!st2 & (p2.d == c.d1) & ((p2.x != x2o) | (p2.y != y2o))) pick_up(c, p2, npc, items);
       }
     }
   }
@@ -1848,6 +2001,17 @@ __device__ __forceinline__ void rollout_tick(const Cfg& c, const orx_state_t& st
   status = rare ? status : (end ? ORX_TIE : ORX_IN_PROGRESS);
   tick = rare ? tick : ft;
   const int32_t t0 = ft - 1;  // the pre-tick tick of every game
+  if (c.ext & ORX_EXT_README_COMBAT) {  // cooldowns run down (the ordered tick runs its own)
+    const bool base = in_progress & !took_ordered;
+    p1.cool = base ? max(p1.cool - 1, 0) : p1.cool;
+    p2.cool = base ? max(p2.cool - 1, 0) : p2.cool;
+  }
+  if (c.ext & ORX_EXT_MANA) {  // the end of the tick: mana regeneration (readme.md:72)
+    // (the in-progress games of the common path's rules; the ordered tick has its own)
+    const bool base = in_progress & !took_ordered;
+    p1.mana = base ? min(p1.mana + c.mana_regen, c.mana_max) : p1.mana;
+    p2.mana = base ? min(p2.mana + c.mana_regen, c.mana_max) : p2.mana;
+  }
   if (c.ext & ORX_EXT_SEPARATION_DAMAGE) {  // build extension (readme.md:46-47), C5's ladder
     // base: the in-progress games whose tick took the common path's rules
     // (free moves, or a hit, a descend or a meet in the rare block)
@@ -1935,7 +2099,9 @@ struct TrajWriter {
 
 // PM (policy mode, compile-time): 0 generic; 1 both players RandomBot, obs
 // and act given, no extension flags (the headline C3/C2 form); 2 both
-// StaircaseBot, obs and act given, at most separation damage (C5).  The
+// StaircaseBot, obs and act given, at most separation damage (C5); 3 both
+// RandomBot, obs and act given, the character mechanics on (configs[2]'s
+// "enemies + items": mana, experience and items, heal optional).  The
 // specialized forms carry no per-tick uniform branches on policy codes or
 // pointers and write the trajectory with buffer stores.
 template <int NCAP, int PM, bool GRID>
@@ -1947,10 +2113,10 @@ __global__ void __launch_bounds__(kRolloutBlock) rollout_kernel(orx_cfg_t hc, or
                                                       Key key, uint32_t off, uint32_t lanes,
                                                       uint32_t lds_n) {
   constexpr bool kTraj = PM != 0;
-  const int32_t pol1 = PM == 1 ? (int32_t)ORX_POLICY_RANDOM
-                               : PM == 2 ? (int32_t)ORX_POLICY_STAIRCASE : pol1_;
-  const int32_t pol2 = PM == 1 ? (int32_t)ORX_POLICY_RANDOM
-                               : PM == 2 ? (int32_t)ORX_POLICY_STAIRCASE : pol2_;
+  const int32_t pol1 = (PM == 1 || PM == 3) ? (int32_t)ORX_POLICY_RANDOM
+                       : PM == 2 ? (int32_t)ORX_POLICY_STAIRCASE : pol1_;
+  const int32_t pol2 = (PM == 1 || PM == 3) ? (int32_t)ORX_POLICY_RANDOM
+                       : PM == 2 ? (int32_t)ORX_POLICY_STAIRCASE : pol2_;
   bool lds_tiles = false;
   if constexpr (GRID) {  // stage the bank's tiles in LDS (the whole block, before any exit)
     const uint32_t n = lds_n;  // the bank's bytes, or 0: not staged (too large, or disabled)
@@ -1979,6 +2145,9 @@ __global__ void __launch_bounds__(kRolloutBlock) rollout_kernel(orx_cfg_t hc, or
   c.lds_tiles = lds_tiles;
   if (PM == 1) c.ext = 0;                           // launched only with flags == 0
   if (PM == 2) c.ext &= ORX_EXT_SEPARATION_DAMAGE;  // launched only with flags <= that
+  // launched only with MANA, LEVELING and ITEMS on (HEAL is inert here: the
+  // bots never heal), nothing else
+  if (PM == 3) c.ext = ORX_EXT_MANA | ORX_EXT_LEVELING | ORX_EXT_ITEMS;
   const uint32_t game = off + i;
   ORX_STAMP(0);
   Player p1, p2;
@@ -1991,7 +2160,7 @@ __global__ void __launch_bounds__(kRolloutBlock) rollout_kernel(orx_cfg_t hc, or
   NpcHpRegs<NCAP> hp;
   if constexpr (NCAP > 0) hp.load(st.npc_health, c.K, B, i);
   Items<NCAP> items;
-  load_rpg(st, c, B, i, p1, p2, items);
+  load_rpg(st, c, B, i, p1, p2, npc, items);
   Deltas dl = {0, 0, 0, 0, 0, 0};
   int32_t sep = (c.ext & ORX_EXT_SEPARATION_DAMAGE) ? st.sep_start[i] : -1;
   bool restarted = false;
@@ -2012,7 +2181,7 @@ __global__ void __launch_bounds__(kRolloutBlock) rollout_kernel(orx_cfg_t hc, or
   } while (++t < n_ticks);
   ORX_STAMP(3);
   store_players<GRID>(st, B, i, p1, p2, restarted || dl.descend != 0);
-  store_rpg(st, c, B, i, p1, p2, items);
+  store_rpg(st, c, B, i, p1, p2, npc, items);
   st.tick[i] = tick;
   st.status[i] = status;
   st.episode[i] = (int32_t)ep;
@@ -2131,7 +2300,7 @@ __global__ void __launch_bounds__(256) mt_reset_kernel(orx_cfg_t hc, orx_state_t
   store_players<GRID>(st, B, i, p1, p2, true);
   Items<NCAP> items;
   items.clear();
-  store_rpg(st, c, B, i, p1, p2, items);
+  store_rpg(st, c, B, i, p1, p2, npc, items);
   st.tick[i] = tick;
   st.status[i] = status;
   if (c.ext & ORX_EXT_SEPARATION_DAMAGE) st.sep_start[i] = -1;
@@ -2192,7 +2361,7 @@ __global__ void __launch_bounds__(256) mt_step_kernel(orx_cfg_t hc, orx_state_t 
     store_players<GRID>(st, B, i, p1, p2, true);
     Items<NCAP> items;
     items.clear();
-    store_rpg(st, c, B, i, p1, p2, items);
+    store_rpg(st, c, B, i, p1, p2, npc, items);
     st.tick[i] = tick;
     st.status[i] = status;
     st.episode[i] = (int32_t)ep;
@@ -2216,7 +2385,7 @@ __global__ void __launch_bounds__(256) mt_step_kernel(orx_cfg_t hc, orx_state_t 
   load_players<GRID>(st, B, i, p1, p2);
   load_npcs(st, c, B, i, npc);
   Items<NCAP> items;
-  load_rpg(st, c, B, i, p1, p2, items);
+  load_rpg(st, c, B, i, p1, p2, npc, items);
   NpcMem m{st.npc_pos, st.npc_health, B, i};
   Deltas dl = {0, 0, 0, 0, 0, 0};
   Events<EV> ev{EV ? events + (size_t)i * ORX_MAX_EVENTS * 4 : nullptr, 0};
@@ -2228,7 +2397,7 @@ __global__ void __launch_bounds__(256) mt_step_kernel(orx_cfg_t hc, orx_state_t 
   tick_game<NCAP, EV, GRID>(c, key, src, game, ep, p1_first, p1, p2, npc, items, m, tick, status,
                             err, dl, ev, sep);
   src.close();
-  store_rpg(st, c, B, i, p1, p2, items);
+  store_rpg(st, c, B, i, p1, p2, npc, items);
   if (c.ext & ORX_EXT_SEPARATION_DAMAGE) st.sep_start[i] = sep;
   store_players<GRID>(st, B, i, p1, p2, dl.descend != 0);
   st.tick[i] = tick;
@@ -2258,7 +2427,7 @@ __global__ void __launch_bounds__(256) mt_rollout_kernel(orx_cfg_t hc, orx_state
   load_npcs(st, c, B, i, npc);
   NpcMem m{st.npc_pos, st.npc_health, B, i};
   Items<NCAP> items;
-  load_rpg(st, c, B, i, p1, p2, items);
+  load_rpg(st, c, B, i, p1, p2, npc, items);
   Deltas dl = {0, 0, 0, 0, 0, 0};
   int32_t sep = (c.ext & ORX_EXT_SEPARATION_DAMAGE) ? st.sep_start[i] : -1;
   bool stairs_dirty = false, npc_dirty = false;
@@ -2290,7 +2459,7 @@ __global__ void __launch_bounds__(256) mt_rollout_kernel(orx_cfg_t hc, orx_state
   }
   src.close();
   store_players<GRID>(st, B, i, p1, p2, stairs_dirty);
-  store_rpg(st, c, B, i, p1, p2, items);
+  store_rpg(st, c, B, i, p1, p2, npc, items);
   st.tick[i] = tick;
   st.status[i] = status;
   st.episode[i] = (int32_t)ep;
@@ -2361,8 +2530,10 @@ int check_cfg(const orx_cfg_t* c) {
     return fail(ORX_EINVAL, "board too small for the players and NPCs");
   if (c->player_health < 1) return fail(ORX_EINVAL, "player_health must be >= 1");
   if (c->autoreset != 0 && c->autoreset != 1) return fail(ORX_EINVAL, "autoreset must be 0 or 1");
-  if (c->flags & ~(ORX_EXT_SEPARATION_DAMAGE | ORX_EXT_RANDOM_DOUBLE_DEATH | ORX_EXT_RPG))
+  if (c->flags & ~(ORX_EXT_SEPARATION_DAMAGE | ORX_EXT_RANDOM_DOUBLE_DEATH | ORX_EXT_CHARACTER))
     return fail(ORX_EINVAL, "unknown extension flag");
+  if ((c->flags & ORX_EXT_README_COMBAT) && c->combat_cooldown < 0)
+    return fail(ORX_EINVAL, "the readme's combat needs combat_cooldown >= 0");
   if ((c->flags & ORX_EXT_HEAL) && !(c->flags & ORX_EXT_MANA))
     return fail(ORX_EINVAL, "ORX_EXT_HEAL needs ORX_EXT_MANA");
   if ((c->flags & ORX_EXT_MANA) &&
@@ -2398,7 +2569,7 @@ int check_state(const orx_cfg_t* c, const orx_state_t* s, bool full) {
     return fail(ORX_EINVAL, "separation damage needs sep_start");
   if (c->rng == ORX_RNG_MT19937 && (!s->mt_py || !s->mt_np || !s->dstore))
     return fail(ORX_EINVAL, "stock-seed mode needs mt_py, mt_np and dstore");
-  if ((c->flags & ORX_EXT_RPG) && !s->p_rpg)
+  if ((c->flags & ORX_EXT_CHARACTER) && !s->p_rpg)
     return fail(ORX_EINVAL, "the character mechanics need p_rpg");
   if ((c->flags & ORX_EXT_ITEMS) && c->n_npcs > 0 && (!s->item_pos || !s->item_mask))
     return fail(ORX_EINVAL, "ORX_EXT_ITEMS needs item_pos and item_mask");
@@ -2645,11 +2816,12 @@ int orx_rollout(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p1, 
     return launch_status("orx_rollout");
   }
   const bool traj_fast = obs && act && (uint64_t)B * ORX_OBS_FIELDS * 4u < (1ull << 31);
+  const bool both_random = policy_p1 == ORX_POLICY_RANDOM && policy_p2 == ORX_POLICY_RANDOM;
   const int pm = !traj_fast ? 0
-                 : (cfg->flags == 0 && policy_p1 == ORX_POLICY_RANDOM &&
-                    policy_p2 == ORX_POLICY_RANDOM) ? 1
+                 : (cfg->flags == 0 && both_random) ? 1
                  : ((cfg->flags & ~ORX_EXT_SEPARATION_DAMAGE) == 0 &&
                     policy_p1 == ORX_POLICY_STAIRCASE && policy_p2 == ORX_POLICY_STAIRCASE) ? 2
+                 : ((cfg->flags | ORX_EXT_HEAL) == ORX_EXT_RPG && both_random) ? 3
                  : 0;
   const uint32_t lanes = rollout_lanes(B);
   const uint32_t per_block = (uint32_t)kRolloutBlock / 64u * lanes;
@@ -2669,6 +2841,8 @@ int orx_rollout(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p1, 
   ORX_ROLLOUT(0, 0, true) ORX_ROLLOUT(0, 1, true) ORX_ROLLOUT(0, 2, true)
   ORX_ROLLOUT(8, 0, true) ORX_ROLLOUT(8, 1, true) ORX_ROLLOUT(8, 2, true)
   ORX_ROLLOUT(16, 0, true) ORX_ROLLOUT(16, 1, true) ORX_ROLLOUT(16, 2, true)
+  ORX_ROLLOUT(0, 3, false) ORX_ROLLOUT(8, 3, false) ORX_ROLLOUT(16, 3, false)
+  ORX_ROLLOUT(0, 3, true) ORX_ROLLOUT(8, 3, true) ORX_ROLLOUT(16, 3, true)
 #undef ORX_ROLLOUT
   return launch_status("orx_rollout");
 }

@@ -17,8 +17,8 @@ import torch
 
 from . import _lib
 from .config import EnvConfig
-from .enums import (DSTORE, EXT_ITEMS, EXT_RPG, EXT_SEPARATION_DAMAGE, MAX_EVENTS, N_COUNTERS,
-                    OBS_FIELDS, RNG_MT19937, RPG_FIELDS, Policy)
+from .enums import (DSTORE, EXT_CHARACTER, EXT_ITEMS, EXT_SEPARATION_DAMAGE, MAX_EVENTS,
+                    N_COUNTERS, OBS_FIELDS, RNG_MT19937, RPG_FIELDS, Policy)
 
 STATE_FIELDS = ("p_x", "p_y", "p_depth", "p_health", "st_x", "st_y", "tick", "status", "episode",
                 "ret_sum", "ep_count", "counters", "npc_pos", "npc_health", "npc_alive")
@@ -97,11 +97,11 @@ class BatchedEngine:
             self.mt_py, self.mt_np = z(625, B), z(625, B)
             self.dstore = z(DSTORE, 2, B)
             ptrs.update({f: getattr(self, f).data_ptr() for f in ("mt_py", "mt_np", "dstore")})
-        # the readme's character mechanics (EXT_RPG flags): player attributes
+        # the readme's character mechanics (EXT_CHARACTER flags): player attributes
         # [RPG_FIELDS][2][B]; with EXT_ITEMS and NPCs the items each NPC slot
         # dropped (x | y << 8) and their on-floor / kind bit masks
         self.p_rpg = self.item_pos = self.item_mask = None
-        if int(cfg.flags) & EXT_RPG:
+        if int(cfg.flags) & EXT_CHARACTER:
             self.p_rpg = z(len(RPG_FIELDS), 2, B)
             ptrs["p_rpg"] = self.p_rpg.data_ptr()
             if int(cfg.flags) & EXT_ITEMS and K > 0:

@@ -70,9 +70,11 @@ EXT_HEAL = 8          # MOVE_HEAL: a Stay converting up to 1/3 of the manabar in
 EXT_LEVELING = 16     # experience per NPC kill; a level refills health and mana
 EXT_ITEMS = 32        # NPC drops with flat bonuses, picked up into finite item spots
 EXT_RPG = EXT_MANA | EXT_HEAL | EXT_LEVELING | EXT_ITEMS
+EXT_README_COMBAT = 64  # the readme's combat table (half damage, cooldowns, negation)
+EXT_CHARACTER = EXT_RPG | EXT_README_COMBAT   # the flags that keep p_rpg
 MOVE_HEAL = 6         # action code of a heal (EXT_HEAL only; not a reference Move)
 # rows of the p_rpg player-attribute tensor (include/orx.h ORX_RPG_*)
-RPG_FIELDS = ("mana", "xp", "damage", "max_health", "items")
+RPG_FIELDS = ("mana", "xp", "damage", "max_health", "items", "cooldown")
 
 # EnvConfig.rng (orx_cfg_t.rng, include/orx.h ORX_RNG_*)
 RNG_PHILOX = 0

@@ -21,7 +21,7 @@ CFG_FIELDS = ["width", "height", "despawn", "max_ticks", "start_mode", "p1_depth
               "n_npcs", "npc_health", "npc_damage", "npc_armor", "player_health",
               "player_damage", "player_armor", "autoreset", "flags", "n_layouts", "sep_period",
               "rng", "mana_max", "mana_regen", "mana_per_point", "xp_per_kill", "xp_per_level",
-              "item_drop_pct", "item_bonus", "item_slots"]
+              "item_drop_pct", "item_bonus", "item_slots", "combat_cooldown"]
 
 
 class _Cfg(ctypes.Structure):
@@ -32,7 +32,8 @@ DEFAULT_CFG = dict(width=32, height=32, despawn=1, max_ticks=1000, start_mode=1,
                    p2_depth=0, n_npcs=0, npc_health=3, npc_damage=1, npc_armor=0,
                    player_health=10, player_damage=2, player_armor=1, autoreset=1, flags=0,
                    n_layouts=0, sep_period=0, rng=0, mana_max=9, mana_regen=1, mana_per_point=1,
-                   xp_per_kill=1, xp_per_level=3, item_drop_pct=50, item_bonus=1, item_slots=3)
+                   xp_per_kill=1, xp_per_level=3, item_drop_pct=50, item_bonus=1, item_slots=3,
+                   combat_cooldown=3)
 
 _lib = None
 
@@ -115,7 +116,10 @@ class Oracle:
 
     def __del__(self):
         if getattr(self, "_h", None):
-            lib().oracle_free(self._h)
+            try:
+                lib().oracle_free(self._h)
+            except Exception:  # interpreter shutdown: the module's globals are gone
+                pass
             self._h = None
 
     def reset(self, mask=None, episode=None):
@@ -163,8 +167,8 @@ class Oracle:
         if self.layouts is not None:
             out["p_layout"] = np.zeros((2, B), np.int16)
             lib().oracle_export_layout(self._h, _ptr(out["p_layout"]))
-        if self.cfg["flags"] & 60:  # ORX_EXT_RPG: player attributes, items
-            out["p_rpg"] = np.zeros((5, 2, B), np.int32)
+        if self.cfg["flags"] & 124:  # ORX_EXT_CHARACTER: player attributes, items
+            out["p_rpg"] = np.zeros((6, 2, B), np.int32)
             items = self.cfg["flags"] & 32 and K > 0
             if items:
                 out["item_pos"] = np.zeros((K, B), np.uint16)

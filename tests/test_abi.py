@@ -101,9 +101,11 @@ def test_validate_cfg(lib):
     ok.append(EnvConfig(width=6, height=5, layouts=np.ones((3, 6, 5), np.uint8)))
     # build extensions: known bits only; separation damage needs a period
     ok.append(EnvConfig(flags=3, sep_period=5))
-    bad += [EnvConfig(flags=64), EnvConfig(flags=1, sep_period=0)]
+    bad += [EnvConfig(flags=1, sep_period=0)]
     # the readme's character mechanics: heal needs mana; every parameter in range
     ok += [EnvConfig(flags=4 | 8 | 16 | 32, n_npcs=4), EnvConfig(flags=16, xp_per_kill=0)]
+    ok.append(EnvConfig(flags=64))
+    bad += [EnvConfig(flags=128), EnvConfig(flags=64, combat_cooldown=-1)]
     bad += [EnvConfig(flags=8), EnvConfig(flags=4, mana_max=2), EnvConfig(flags=4, mana_per_point=0),
             EnvConfig(flags=4, mana_regen=-1), EnvConfig(flags=16, xp_per_level=0),
             EnvConfig(flags=32, item_drop_pct=101), EnvConfig(flags=32, item_slots=-1)]
@@ -125,7 +127,7 @@ def test_plain_c_consumer(lib, tmp_path):
                     "-Wl,-rpath," + os.path.join(ROOT, "optimax_rogue_amd")], check=True)
     r = subprocess.run([str(exe)], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert "sizeof(orx_cfg_t)=108" in r.stdout
+    assert "sizeof(orx_cfg_t)=112" in r.stdout
 
 
 def test_engine_refuses_cpu():

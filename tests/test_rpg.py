@@ -137,6 +137,75 @@ def test_items_drop_and_pickup(oracle_lib, tmp_path):
     assert int(ex["item_mask"][0, 0]) == 0
 
 
+README = 64
+DUEL = [(1, 0, 2, 2, 10), (2, 0, 3, 2, 10)]   # player 1 left of player 2
+LEFT, DOWN = 4, 3
+
+
+def _duel(oracle_lib, moves, ents=DUEL, flags=README, **kw):
+    return _one(oracle_lib, flags, ents=ents, moves=moves, n_npcs=0, player_damage=5,
+                player_armor=1, **kw)
+
+
+def test_readme_combat_mutual(oracle_lib):
+    """Both attack the other's cell: each takes half of 5 - 1 = 4, nobody
+    moves, both get combat_cooldown (3) ticks of cooldown."""
+    ex, evs = _duel(oracle_lib, ((RIGHT, LEFT),))
+    assert ex["p_health"][:, 0].tolist() == [8, 8]
+    assert ex["p_x"][:, 0].tolist() == [2, 3]
+    assert _rpg(ex, 0, "cooldown") == 3 and _rpg(ex, 1, "cooldown") == 3
+    assert evs[0] == [(1, 1, 2, 4), (1, 2, 1, 4)]
+    # the next three ticks their attacks are Stays and they cannot defend:
+    # player 1 attacking is a Stay, player 2 attacks it (full damage, no stun)
+    ex, evs = _duel(oracle_lib, ((RIGHT, LEFT), (RIGHT, LEFT)))
+    assert ex["p_health"][:, 0].tolist() == [8, 8]   # both attacks measured as Stays
+    assert evs[1] == []
+    # cooldown runs out after combat_cooldown ticks
+    ex, _ = _duel(oracle_lib, ((RIGHT, LEFT), (STAY, STAY), (STAY, STAY), (STAY, STAY)))
+    assert _rpg(ex, 0, "cooldown") == 0
+    ex, _ = _duel(oracle_lib, ((RIGHT, LEFT),), combat_cooldown=5)
+    assert _rpg(ex, 1, "cooldown") == 5
+
+
+def test_readme_combat_same_cell(oracle_lib):
+    """Both move into one cell: full damage each, nobody moves."""
+    ents = [(1, 0, 2, 2, 10), (2, 0, 4, 2, 10)]
+    ex, evs = _duel(oracle_lib, ((RIGHT, LEFT),), ents=ents)
+    assert ex["p_health"][:, 0].tolist() == [6, 6]
+    assert ex["p_x"][:, 0].tolist() == [2, 4]
+    assert evs[0] == [(1, 1, 2, 2), (1, 2, 1, 2)]
+
+
+def test_readme_combat_negation_and_stun(oracle_lib):
+    """A attacks B who stays: negated, A is stunned one tick (cannot attack or
+    defend); B then attacks the stunned A: full damage."""
+    ex, evs = _duel(oracle_lib, ((RIGHT, STAY),))
+    assert ex["p_health"][:, 0].tolist() == [10, 10]
+    assert _rpg(ex, 0, "cooldown") == 1 and evs[0] == [(1, 1, 2, 1)]
+    ex, evs = _duel(oracle_lib, ((RIGHT, STAY), (RIGHT, LEFT)))
+    assert ex["p_health"][:, 0].tolist() == [6, 10]
+    assert evs[1] == [(1, 2, 1, 1)]
+    assert _rpg(ex, 1, "cooldown") == 0            # an undefended hit stuns nobody
+    # a healer stays too: its attacker is negated
+    ex, _ = _duel(oracle_lib, ((RIGHT, HEAL_MOVE),), flags=README | MANA | HEAL)
+    assert int(ex["p_health"][1, 0]) == 10
+
+
+def test_readme_combat_flee(oracle_lib):
+    """A attacks B's cell but B moves away: no damage, A stays."""
+    ex, evs = _duel(oracle_lib, ((RIGHT, DOWN),))
+    assert ex["p_health"][:, 0].tolist() == [10, 10]
+    assert (ex["p_x"][:, 0].tolist(), ex["p_y"][:, 0].tolist()) == ([2, 3], [2, 3])
+    assert evs[0][0] == (1, 1, 2, 3)
+
+
+def test_readme_combat_mana(oracle_lib):
+    """Mana joins the readme's damage: half of (4 + 3) = 3 in a mutual attack."""
+    ex, _ = _duel(oracle_lib, ((RIGHT, LEFT),), flags=README | MANA)
+    assert ex["p_health"][:, 0].tolist() == [7, 7]
+    assert _rpg(ex, 0, "mana") == 9 - 3 + 1
+
+
 def test_rpg_oracle_runs_many_games(oracle_lib):
     """Many random games with every mechanic on: invariants of the attributes."""
     cfg = dict(width=10, height=9, n_npcs=6, npc_health=3, max_ticks=200, flags=MANA | HEAL | LEVEL | ITEMS,
@@ -176,6 +245,19 @@ RPG_CASES = {
                       2048, 300, 33, 0),
     "rpg_c3_64": (dict(width=64, height=64, n_npcs=8, max_ticks=1000,
                        flags=MANA | HEAL | LEVEL | ITEMS), 4096, 400, 34, 0),
+    # deadly and cramped: players die in meets the same tick they pick up health
+    # items or level up; one item spot; every kill a level
+    "rpg_deadly_5x6": (dict(width=5, height=6, n_npcs=5, npc_health=2, player_health=2,
+                            max_ticks=0, flags=MANA | LEVEL | ITEMS, mana_max=3,
+                            xp_per_level=1, item_drop_pct=90, item_bonus=2, item_slots=1),
+                       2048, 300, 36, 0),
+    # the readme's combat table, alone and with every other mechanic
+    "readme_combat_5x5": (dict(width=5, height=5, n_npcs=2, max_ticks=300, flags=README,
+                               player_damage=4), 2048, 300, 37, 0),
+    "readme_all_8x7": (dict(width=8, height=7, n_npcs=5, max_ticks=200,
+                            flags=README | MANA | HEAL | LEVEL | ITEMS | 1, sep_period=5,
+                            start_mode=2, p1_depth=0, p2_depth=1, xp_per_level=2),
+                       2048, 300, 38, 0),
     # stock-seed mode with the mechanics (drops keep their Philox block)
     "rpg_stock": (dict(width=10, height=9, n_npcs=4, max_ticks=150, rng=1,
                        flags=MANA | HEAL | LEVEL | ITEMS), 1024, 300, 35, 0),
@@ -217,13 +299,23 @@ def test_rpg_engine_vs_oracle(name, oracle_lib):
         assert n_heal_ev > 0
     ex = ora.export()
     assert ex["p_rpg"][1].sum() > 0 if cfg["flags"] & LEVEL else True
-    # the fused rollout on the same configuration
-    ora2 = oracle_lib.Oracle(cfg, B, seed, off)
-    ora2.reset(episode=np.zeros(B, np.int32))
-    eng2 = BatchedEngine(EnvConfig.from_dict(cfg), B, seed=seed, game_offset=off, device=dev)
-    for c in range(3):
-        for _ in range(T // 3):
-            ora2.step(ora2.policy(2, 1))
-        eng2.rollout(T // 3, 2, 1)
-        compare_state(eng2.snapshot(), ora2.export(), ora2.K, f"{name} rollout chunk {c}")
+    # the fused rollout on the same configuration: the generic form (StaircaseBot
+    # vs RandomBot) and the RandomBot-pair form with trajectories (PM 3)
+    from optimax_rogue_amd.enums import OBS_FIELDS
+    for pol in ((2, 1), (1, 1)):
+        ora2 = oracle_lib.Oracle(cfg, B, seed, off)
+        ora2.reset(episode=np.zeros(B, np.int32))
+        eng2 = BatchedEngine(EnvConfig.from_dict(cfg), B, seed=seed, game_offset=off, device=dev)
+        n = T // 3
+        obs = torch.zeros((n, len(OBS_FIELDS), B), dtype=torch.int32, device=dev)
+        act = torch.zeros((n, B, 2), dtype=torch.int8, device=dev)
+        for c in range(3):
+            want_act = []
+            for _ in range(n):
+                a = ora2.policy(*pol)
+                want_act.append(a)
+                ora2.step(a)
+            eng2.rollout(n, *pol, obs=obs, act=act)
+            compare_state(eng2.snapshot(), ora2.export(), ora2.K, f"{name} rollout {pol} {c}")
+            assert np.array_equal(act.cpu().numpy(), np.stack(want_act)), (name, pol, c)
     torch.cuda.synchronize()
