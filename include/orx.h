@@ -187,7 +187,11 @@ extern "C" {
                             a heal +amount, ORX_EXT_HEAL)                   */
 #define ORX_MAX_EVENTS 8 /* per game per tick (at most 6 occur)            */
 
-#define ORX_MAX_NPCS 16 /* NPCs per game (alive mask is 32-bit; registers)  */
+#define ORX_MAX_NPCS 255     /* NPCs per game                                 */
+#define ORX_MAX_REG_NPCS 16  /* up to this many the kernels keep the NPCs in
+                                registers; above, in an occupancy grid in HBM
+                                (orx_state_t.npc_grid; ORX_EXT_ITEMS needs
+                                n_npcs <= ORX_MAX_REG_NPCS)                   */
 #define ORX_MAX_GRID_NPC 256 /* NPC (x,y) pack into 8+8 bits when K > 0    */
 
 /* trajectory fields, rows of one orx_rollout tick record                    */
@@ -268,7 +272,8 @@ typedef struct orx_state {
   int32_t* counters;   /* [ORX_NCOUNTERS][B] event counters (may be NULL)    */
   uint16_t* npc_pos;   /* [K][B] x | y << 8  (NULL when K == 0)              */
   int8_t* npc_health;  /* [K][B]                                             */
-  uint32_t* npc_alive; /* [B]    bit k = NPC k still in GameState.entities   */
+  uint32_t* npc_alive; /* [ceil(K/32)][B] bit k % 32 of row k / 32 = NPC k
+                                 still in GameState.entities ([B] for K <= 32) */
   /* dungeon bank (cfg->n_layouts = L > 0; all NULL otherwise)               */
   int16_t* p_layout;            /* [2][B] layout of each player's depth       */
   const uint8_t* bank_tiles;    /* [L][W][H] Tile codes, Dungeon.tiles layout
@@ -296,6 +301,9 @@ typedef struct orx_state {
   uint32_t* item_mask;          /* [2][B] ORX_EXT_ITEMS: row 0 bit k = item k
                                    lies on the floor, row 1 bit k = its kind
                                    (0 damage, 1 max health)                  */
+  /* dense NPCs (n_npcs > ORX_MAX_REG_NPCS; NULL otherwise)                   */
+  uint8_t* npc_grid;            /* [B][W * H] occupancy of the NPCs' depth:
+                                   slot + 1 per cell (x * H + y), 0 = empty   */
 } orx_state_t;
 
 /* ---- entry points --------------------------------------------------------- */

@@ -22,7 +22,7 @@ class OrxState(ctypes.Structure):
         "p_x", "p_y", "p_depth", "p_health", "st_x", "st_y", "tick", "status", "episode",
         "ret_sum", "ep_count", "counters", "npc_pos", "npc_health", "npc_alive",
         "p_layout", "bank_tiles", "bank_ground", "bank_meta", "sep_start", "mt_py", "mt_np",
-        "dstore", "p_rpg", "item_pos", "item_mask")]
+        "dstore", "p_rpg", "item_pos", "item_mask", "npc_grid")]
 
 
 class OrxError(RuntimeError):

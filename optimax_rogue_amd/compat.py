@@ -302,10 +302,11 @@ def game_state(snap: dict, i: int, cfg, extra_stairs: Optional[Dict[int, tuple]]
             dungeons[d] = view(*(cur[d] if d in cur else extra_stairs[d]))
     K = int(cfg.n_npcs)
     if K:
-        alive = int(snap["npc_alive"][i])
+        alive = np.asarray(snap["npc_alive"])
+        alive = [int(v) for v in (alive[i:i + 1] if alive.ndim == 1 else alive[:, i])]
         npc_depth = int(cfg.p1_depth) if int(cfg.start_mode) == 2 else 0
         for k in range(K):
-            if (alive >> k) & 1:
+            if (alive[k // 32] >> (k % 32)) & 1:
                 v = int(snap["npc_pos"][k][i])
                 ents.append(EntityView(3 + k, npc_depth, v & 0xFF, v >> 8, snap["npc_health"][k][i],
                                        cfg.npc_health, cfg.npc_damage, cfg.npc_armor))

@@ -230,6 +230,7 @@ struct Cfg {  // device copy of orx_cfg_t plus derived constants (all wave-unifo
 // hides that latency).
 extern __shared__ uint8_t orx_lds_tiles[];
 constexpr uint32_t kMaxLdsTiles = 64 * 1024;
+constexpr uint32_t kMaxLdsBlock = 160 * 1024;  // LDS per CU (one workgroup may take it all)
 
 struct Deltas {  // counter / return increments, flushed once per launch
   int32_t combat, descend, dungeon, npc_death, ret, eps;
@@ -281,6 +282,16 @@ struct Npcs {
     q0 = q1 = q2 = q3 = q4 = q5 = q6 = q7 = 0xFFFFFFFFu;
     alive = 0;
   }
+  // the alive mask (GameState.entities membership), one bit per slot
+  __device__ __forceinline__ void bind(const orx_state_t&, const Cfg&, uint32_t, uint32_t) {}
+  __device__ __forceinline__ bool is_alive(int k) const { return (alive >> k) & 1u; }
+  __device__ __forceinline__ void mark_alive(int k) { alive |= 1u << k; }
+  __device__ __forceinline__ void mark_dead(int k) { alive &= ~(1u << k); }
+  __device__ __forceinline__ bool any_alive() const { return alive != 0; }
+  __device__ __forceinline__ int count_alive() const { return __popc(alive); }
+  __device__ __forceinline__ void store_alive(uint32_t* rows, uint32_t, uint32_t i) const {
+    rows[i] = alive;
+  }
   __device__ __forceinline__ uint32_t get(int k) const {
     return (rd(k >> 1) >> ((k & 1) * 16)) & 0xFFFFu;
   }
@@ -327,7 +338,7 @@ struct Npcs {
   // item instead; keys of occupied slots are distinct).
   __device__ __forceinline__ bool live(uint32_t key) const {
     const int k = find(key);
-    return k >= 0 && ((alive >> k) & 1u);
+    return k >= 0 && is_alive(k);
   }
   // slot k := dead for a runtime k: 64-bit shifts over register pairs (a
   // switch on k lowers to a branch ladder)
@@ -353,6 +364,109 @@ struct Npcs {
   }
 };
 
+// Dense NPCs (K > 16, up to 255): the NPCs of a game live in HBM -- an
+// occupancy grid of its NPC depth, one byte per cell (slot + 1, 0 = empty;
+// st.npc_grid [B][W*H], cell x * H + y, one game's grid contiguous so a reset
+// clears it with wide stores), the slot rows npc_pos / npc_health, and the
+// alive bits as rows of 32 (npc_alive [ceil(K/32)][B]).  A target test is one
+// byte load instead of a register scan; it is the form for NPC counts that
+// no register file holds (GameState.entities is unbounded, state.py:25-34).
+constexpr int kDense = 256;
+
+// The rollout also stages each game's occupancy as a bitmap in LDS (one bit
+// per cell, 512 B per 64x64 game), so the tick's two target tests read LDS:
+// at one wave per SIMD an HBM round trip per tick would not be hidden.
+template <>
+struct Npcs<kDense> {
+  uint8_t* grid;   // this game's grid
+  uint16_t* pos;   // npc_pos + i (stride B)
+  uint32_t* rows;  // npc_alive + i (stride B)
+  uint32_t B;
+  int32_t H, cells, K;
+  bool staged;     // the bitmap copy in LDS (rollout) is kept in step
+  uint32_t boff;   // its first word in orx_lds_tiles
+
+  __device__ __forceinline__ void bind(const orx_state_t& st, const Cfg& c, uint32_t B_,
+                                       uint32_t i) {
+    B = B_; H = c.H; cells = c.W * c.H; K = c.K;
+    grid = st.npc_grid + (size_t)i * (size_t)cells;
+    pos = st.npc_pos + i;
+    rows = st.npc_alive + i;
+    staged = false;
+    boff = 0;
+  }
+  __device__ __forceinline__ uint32_t* lds() const {
+    return reinterpret_cast<uint32_t*>(orx_lds_tiles);
+  }
+  __device__ __forceinline__ int cell(uint32_t key) const {
+    return (int)(key & 0xFFu) * H + (int)(key >> 8);
+  }
+  __device__ __forceinline__ void clear_bits() {
+    for (int w = 0; w < (cells + 31) >> 5; ++w) lds()[boff + w] = 0u;
+  }
+  // builds this game's LDS bitmap at word `off` from its live NPCs
+  __device__ __forceinline__ void stage(uint32_t off) {
+    boff = off;
+    staged = true;
+    clear_bits();
+    // per row of 32 slots: its alive word and all 32 positions in flight at
+    // once (one HBM round trip per row, not per NPC)
+    for (int r = 0; r < (K + 31) >> 5; ++r) {
+      const uint32_t a = rows[(size_t)r * B];
+      uint32_t p[32];
+#pragma unroll
+      for (int j = 0; j < 32; ++j) p[j] = pos[(size_t)min(r * 32 + j, K - 1) * B];
+#pragma unroll
+      for (int j = 0; j < 32; ++j)
+        if ((a >> j) & 1u) {
+          const int cl = cell(p[j]);
+          lds()[boff + (cl >> 5)] |= 1u << (cl & 31);
+        }
+    }
+  }
+  __device__ __forceinline__ void clear() {  // the grid and the alive rows
+    uint32_t* g4 = reinterpret_cast<uint32_t*>(grid);
+    for (int j = 0; j < (cells >> 2); ++j) g4[j] = 0u;
+    for (int j = cells & ~3; j < cells; ++j) grid[j] = 0;
+    for (int r = 0; r < (K + 31) >> 5; ++r) rows[(size_t)r * B] = 0u;
+    if (staged) clear_bits();
+  }
+  __device__ __forceinline__ bool is_alive(int k) const {
+    return (rows[(size_t)(k >> 5) * B] >> (k & 31)) & 1u;
+  }
+  __device__ __forceinline__ void mark_alive(int k) { rows[(size_t)(k >> 5) * B] |= 1u << (k & 31); }
+  __device__ __forceinline__ void mark_dead(int k) { rows[(size_t)(k >> 5) * B] &= ~(1u << (k & 31)); }
+  __device__ __forceinline__ bool any_alive() const { return true; }  // (an optimization only)
+  __device__ __forceinline__ int count_alive() const {
+    int n = 0;
+    for (int r = 0; r < (K + 31) >> 5; ++r) n += __popc(rows[(size_t)r * B]);
+    return n;
+  }
+  __device__ __forceinline__ void store_alive(uint32_t*, uint32_t, uint32_t) const {}  // in place
+  __device__ __forceinline__ uint32_t get(int k) const { return pos[(size_t)k * B]; }
+  __device__ __forceinline__ void set(int k, uint32_t key) {
+    const int cl = cell(key);
+    grid[cl] = (uint8_t)(k + 1);
+    pos[(size_t)k * B] = (uint16_t)key;
+    if (staged) lds()[boff + (cl >> 5)] |= 1u << (cl & 31);
+  }
+  __device__ __forceinline__ bool any(uint32_t key) const {
+    const int cl = cell(key);
+    if (staged) return (lds()[boff + (cl >> 5)] >> (cl & 31)) & 1u;
+    return grid[cl] != 0;
+  }
+  __device__ __forceinline__ int find(uint32_t key) const { return (int)grid[cell(key)] - 1; }
+  __device__ __forceinline__ bool live(uint32_t key) const {
+    const int k = find(key);
+    return k >= 0 && is_alive(k);
+  }
+  __device__ __forceinline__ void kill(int k) {
+    const int cl = cell(get(k));
+    grid[cl] = 0;
+    if (staged) lds()[boff + (cl >> 5)] &= ~(1u << (cl & 31));
+  }
+};
+
 // Both players' NPC occupancy tests in one pass over the slot registers
 // (the rollout's common path): with K = k1 | k2 << 16 and its half-swap Ks,
 // the packed 16-bit minimum over (slots ^ K) has a zero low half iff some
@@ -363,6 +477,9 @@ __device__ __forceinline__ void npc_any2(const Npcs<NCAP>& npc, uint32_t k1, uin
                                          bool& h1, bool& h2) {
   if constexpr (NCAP == 0) {
     h1 = h2 = false;
+  } else if constexpr (NCAP == kDense) {
+    h1 = npc.any(k1);
+    h2 = npc.any(k2);
   } else {
     typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
     const uint32_t K = k1 | (k2 << 16), Ks = k2 | (k1 << 16);
@@ -687,7 +804,7 @@ __device__ __forceinline__ void setup_game(const Cfg& c, Key key, Src& src, Play
     else if (placed == 1) { p2.x = x; p2.y = y; }
     else if constexpr (NCAP > 0) {
       npc.set(placed - 2, pack_xy(x, y));
-      npc.alive |= 1u << (placed - 2);
+      npc.mark_alive(placed - 2);
     }
     ++placed;
   }
@@ -756,7 +873,7 @@ __device__ __forceinline__ void descend(const Cfg& c, Key key, Src& src, Player&
     dl.dungeon += 1;
     ev.emit(ORX_EV_DUNGEON, 0, nd, 0);                 // updater.py:278-280
   }
-  const bool npc_depth = NCAP > 0 && nd == c.d1 && npc.alive;
+  const bool npc_depth = NCAP > 0 && nd == c.d1 && npc.any_alive();
   int32_t x = 0, y = 0;
   bool done = false;
   const NpBound gb = ground_bound<GRID>(c, lay);
@@ -1231,8 +1348,8 @@ __device__ __forceinline__ void npc_hits(const Cfg& c, Npcs<NCAP>& npc, M& m, in
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int k = ks[j];
-    if (k >= 0 && vs[j] <= 0 && ((npc.alive >> k) & 1u)) {
-      npc.alive &= ~(1u << k);
+    if (k >= 0 && vs[j] <= 0 && npc.is_alive(k)) {
+      npc.mark_dead(k);
       npc.kill(k);
       dl.npc_death += 1;
       ev.emit(ORX_EV_DEATH, 3 + k, 0, 0);
@@ -1444,16 +1561,20 @@ __device__ __forceinline__ void store_players(const orx_state_t& st, uint32_t B,
 template <int NCAP>
 __device__ __forceinline__ void load_npcs(const orx_state_t& st, const Cfg& c, uint32_t B,
                                           uint32_t i, Npcs<NCAP>& npc) {
-  npc.clear();
-  if constexpr (NCAP > 0) {
-    uint32_t v[NCAP];
+  if constexpr (NCAP == kDense) {  // the grid stays in HBM
+    npc.bind(st, c, B, i);
+  } else {
+    npc.clear();
+    if constexpr (NCAP > 0) {
+      uint32_t v[NCAP];
 #pragma unroll
-    for (int k = 0; k < NCAP; ++k)
-      v[k] = st.npc_pos[(size_t)min(k, c.K - 1) * B + i];
-    npc.alive = st.npc_alive[i];
+      for (int k = 0; k < NCAP; ++k)
+        v[k] = st.npc_pos[(size_t)min(k, c.K - 1) * B + i];
+      npc.alive = st.npc_alive[i];
 #pragma unroll
-    for (int k = 0; k < NCAP; ++k)
-      npc.set(k, (k < c.K && ((npc.alive >> k) & 1u)) ? v[k] : kDeadSlot);
+      for (int k = 0; k < NCAP; ++k)
+        npc.set(k, (k < c.K && ((npc.alive >> k) & 1u)) ? v[k] : kDeadSlot);
+    }
   }
 }
 
@@ -1464,7 +1585,8 @@ __device__ __forceinline__ void store_new_npcs(const orx_state_t& st, const Cfg&
                                             bool health = true) {
   if constexpr (NCAP > 0) {
     for (int k = 0; k < c.K; ++k) {
-      st.npc_pos[(size_t)k * B + i] = (uint16_t)npc.get(k);
+      // (dense NPCs: set() wrote the positions)
+      if constexpr (NCAP != kDense) st.npc_pos[(size_t)k * B + i] = (uint16_t)npc.get(k);
       if (health) st.npc_health[(size_t)k * B + i] = (int8_t)c.npc_hp;
     }
   }
@@ -1549,6 +1671,7 @@ __global__ void __launch_bounds__(256) reset_kernel(orx_cfg_t hc, orx_state_t st
   const Cfg c = make_cfg(hc, st);
   Player p1, p2;
   Npcs<NCAP> npc;
+  npc.bind(st, c, B, i);
   int32_t tick, status;
   setup_game<NCAP, GRID>(c, key, off + i, (uint32_t)st.episode[i], p1, p2, npc, tick, status);
   store_players<GRID>(st, B, i, p1, p2, true);
@@ -1559,7 +1682,7 @@ __global__ void __launch_bounds__(256) reset_kernel(orx_cfg_t hc, orx_state_t st
   st.status[i] = status;
   if (c.ext & ORX_EXT_SEPARATION_DAMAGE) st.sep_start[i] = -1;
   if constexpr (NCAP > 0) {
-    st.npc_alive[i] = npc.alive;
+    npc.store_alive(st.npc_alive, B, i);
     store_new_npcs(st, c, B, i, npc);
   }
 }
@@ -1576,6 +1699,7 @@ __global__ void __launch_bounds__(256) step_kernel(orx_cfg_t hc, orx_state_t st,
   const uint32_t game = off + i;
   int32_t status = st.status[i];
   Npcs<NCAP> npc;
+  npc.bind(st, c, B, i);
   Player p1, p2;
   if (status != ORX_IN_PROGRESS) {
     if (EV) n_events[i] = 0;
@@ -1592,7 +1716,7 @@ __global__ void __launch_bounds__(256) step_kernel(orx_cfg_t hc, orx_state_t st,
     st.episode[i] = (int32_t)ep;
     if (c.ext & ORX_EXT_SEPARATION_DAMAGE) st.sep_start[i] = -1;
     if constexpr (NCAP > 0) {
-      st.npc_alive[i] = npc.alive;
+      npc.store_alive(st.npc_alive, B, i);
       store_new_npcs(st, c, B, i, npc);
     }
     return;
@@ -1624,7 +1748,7 @@ __global__ void __launch_bounds__(256) step_kernel(orx_cfg_t hc, orx_state_t st,
   store_players<GRID>(st, B, i, p1, p2, dl.descend != 0);
   st.tick[i] = tick;
   st.status[i] = status;
-  if (NCAP > 0 && dl.npc_death) st.npc_alive[i] = npc.alive;
+  if (NCAP > 0 && dl.npc_death) npc.store_alive(st.npc_alive, B, i);
   flush_deltas(st, B, i, dl);
   if (EV) n_events[i] = ev.n;
 }
@@ -1844,8 +1968,12 @@ __device__ __forceinline__ void rollout_tick(const Cfg& c, const orx_state_t& st
         setup_game<NCAP, GRID>(c, key, game, ep, p1, p2, npc, tick, status);
         items.clear();
         if constexpr (NCAP > 0) {
-          store_new_npcs(st, c, B, i, npc, false);  // health: from hp at the end
-          hp.fill(c.npc_hp);
+          if constexpr (NCAP == kDense) {
+            store_new_npcs(st, c, B, i, npc, true);  // health rows in HBM
+          } else {
+            store_new_npcs(st, c, B, i, npc, false);  // health: from hp at the end
+            hp.fill(c.npc_hp);
+          }
         }
         restarted = true;
         sep = -1;
@@ -2111,7 +2239,7 @@ __global__ void __launch_bounds__(kRolloutBlock) rollout_kernel(orx_cfg_t hc, or
                                                       int32_t* __restrict__ obs,
                                                       int8_t* __restrict__ act, uint32_t B,
                                                       Key key, uint32_t off, uint32_t lanes,
-                                                      uint32_t lds_n) {
+                                                      uint32_t lds_n, uint32_t lds_bits) {
   constexpr bool kTraj = PM != 0;
   const int32_t pol1 = (PM == 1 || PM == 3) ? (int32_t)ORX_POLICY_RANDOM
                        : PM == 2 ? (int32_t)ORX_POLICY_STAIRCASE : pol1_;
@@ -2156,9 +2284,21 @@ __global__ void __launch_bounds__(kRolloutBlock) rollout_kernel(orx_cfg_t hc, or
   int32_t status = st.status[i];
   uint32_t ep = (uint32_t)st.episode[i];
   Npcs<NCAP> npc;
+  npc.bind(st, c, B, i);
   load_npcs(st, c, B, i, npc);
-  NpcHpRegs<NCAP> hp;
-  if constexpr (NCAP > 0) hp.load(st.npc_health, c.K, B, i);
+  if constexpr (NCAP == kDense) {
+    // lds_bits: bytes of one game's occupancy bitmap (0: not staged), after
+    // the bank's tiles; a lane's bitmap is its own (no barrier)
+    if (lds_bits) {
+      const uint32_t li = (threadIdx.x >> 6) * lanes + (threadIdx.x & 63u);
+      npc.stage((((lds_n + 15u) & ~15u) + li * lds_bits) >> 2);
+    }
+  }
+  // NPC health: registers, loaded and stored once per launch; the dense form's
+  // rows stay in HBM
+  std::conditional_t<NCAP == kDense, NpcMem, NpcHpRegs<NCAP>> hp;
+  if constexpr (NCAP == kDense) hp = NpcMem{st.npc_pos, st.npc_health, B, i};
+  else if constexpr (NCAP > 0) hp.load(st.npc_health, c.K, B, i);
   Items<NCAP> items;
   load_rpg(st, c, B, i, p1, p2, npc, items);
   Deltas dl = {0, 0, 0, 0, 0, 0};
@@ -2187,8 +2327,9 @@ __global__ void __launch_bounds__(kRolloutBlock) rollout_kernel(orx_cfg_t hc, or
   st.episode[i] = (int32_t)ep;
   if (c.ext & ORX_EXT_SEPARATION_DAMAGE) st.sep_start[i] = sep;
   if constexpr (NCAP > 0) {
-    if (restarted || dl.npc_death) st.npc_alive[i] = npc.alive;
-    if (restarted || dl.combat) hp.store(st.npc_health, c.K, B, i);
+    if (restarted || dl.npc_death) npc.store_alive(st.npc_alive, B, i);
+    if constexpr (NCAP != kDense)
+      if (restarted || dl.combat) hp.store(st.npc_health, c.K, B, i);
   }
   flush_deltas(st, B, i, dl);
 #ifdef ORX_STAMPS
@@ -2277,7 +2418,7 @@ template <int NCAP>
 __device__ __forceinline__ bool mt_shuffles(MtStream& py, const Npcs<NCAP>& npc, bool& err) {
   const bool p1_first = py_randbelow(py, Key{0, 0}, 2u, err) == 1u;
   if constexpr (NCAP > 0)
-    for (int32_t n = __popc(npc.alive) - 1; n >= 1; --n)
+    for (int32_t n = npc.count_alive() - 1; n >= 1; --n)
       py_randbelow(py, Key{0, 0}, (uint32_t)n + 1u, err);
   return p1_first;
 }
@@ -2294,6 +2435,7 @@ __global__ void __launch_bounds__(256) mt_reset_kernel(orx_cfg_t hc, orx_state_t
   src.open(st, B, i);
   Player p1, p2;
   Npcs<NCAP> npc;
+  npc.bind(st, c, B, i);
   int32_t tick, status;
   setup_game<NCAP, GRID>(c, Key{0, 0}, src, p1, p2, npc, tick, status);
   src.close();
@@ -2305,7 +2447,7 @@ __global__ void __launch_bounds__(256) mt_reset_kernel(orx_cfg_t hc, orx_state_t
   st.status[i] = status;
   if (c.ext & ORX_EXT_SEPARATION_DAMAGE) st.sep_start[i] = -1;
   if constexpr (NCAP > 0) {
-    st.npc_alive[i] = npc.alive;
+    npc.store_alive(st.npc_alive, B, i);
     store_new_npcs(st, c, B, i, npc);
   }
 }
@@ -2348,6 +2490,7 @@ __global__ void __launch_bounds__(256) mt_step_kernel(orx_cfg_t hc, orx_state_t 
   const uint32_t game = off + i;
   int32_t status = st.status[i];
   Npcs<NCAP> npc;
+  npc.bind(st, c, B, i);
   Player p1, p2;
   if (status != ORX_IN_PROGRESS) {
     if (EV) n_events[i] = 0;
@@ -2367,7 +2510,7 @@ __global__ void __launch_bounds__(256) mt_step_kernel(orx_cfg_t hc, orx_state_t 
     st.episode[i] = (int32_t)ep;
     if (c.ext & ORX_EXT_SEPARATION_DAMAGE) st.sep_start[i] = -1;
     if constexpr (NCAP > 0) {
-      st.npc_alive[i] = npc.alive;
+      npc.store_alive(st.npc_alive, B, i);
       store_new_npcs(st, c, B, i, npc);
     }
     return;
@@ -2402,7 +2545,7 @@ __global__ void __launch_bounds__(256) mt_step_kernel(orx_cfg_t hc, orx_state_t 
   store_players<GRID>(st, B, i, p1, p2, dl.descend != 0);
   st.tick[i] = tick;
   st.status[i] = status;
-  if (NCAP > 0 && dl.npc_death) st.npc_alive[i] = npc.alive;
+  if (NCAP > 0 && dl.npc_death) npc.store_alive(st.npc_alive, B, i);
   flush_deltas(st, B, i, dl);
   if (EV) n_events[i] = ev.n;
 }
@@ -2424,6 +2567,7 @@ __global__ void __launch_bounds__(256) mt_rollout_kernel(orx_cfg_t hc, orx_state
   int32_t status = st.status[i];
   uint32_t ep = (uint32_t)st.episode[i];
   Npcs<NCAP> npc;
+  npc.bind(st, c, B, i);
   load_npcs(st, c, B, i, npc);
   NpcMem m{st.npc_pos, st.npc_health, B, i};
   Items<NCAP> items;
@@ -2464,7 +2608,7 @@ __global__ void __launch_bounds__(256) mt_rollout_kernel(orx_cfg_t hc, orx_state
   st.status[i] = status;
   st.episode[i] = (int32_t)ep;
   if (c.ext & ORX_EXT_SEPARATION_DAMAGE) st.sep_start[i] = sep;
-  if (NCAP > 0 && (npc_dirty || dl.npc_death)) st.npc_alive[i] = npc.alive;
+  if (NCAP > 0 && (npc_dirty || dl.npc_death)) npc.store_alive(st.npc_alive, B, i);
   flush_deltas(st, B, i, dl);
 }
 
@@ -2516,7 +2660,9 @@ int check_cfg(const orx_cfg_t* c) {
       (c->p1_depth == c->p2_depth || c->p1_depth < 0 || c->p2_depth < 0))
     return fail(ORX_EINVAL, "SeparatedGameStartGenerator needs p1_depth != p2_depth, both >= 0");
   if (c->n_npcs < 0 || c->n_npcs > ORX_MAX_NPCS)
-    return fail(ORX_EINVAL, "n_npcs must be in [0, 16]");
+    return fail(ORX_EINVAL, "n_npcs must be in [0, 255]");
+  if (c->n_npcs > ORX_MAX_REG_NPCS && (c->flags & ORX_EXT_ITEMS))
+    return fail(ORX_EINVAL, "ORX_EXT_ITEMS needs n_npcs <= 16");
   if (c->n_npcs > 0 && (c->width > ORX_MAX_GRID_NPC || c->height > ORX_MAX_GRID_NPC))
     return fail(ORX_EINVAL, "NPC positions pack 8+8 bits: W, H <= 256 when n_npcs > 0");
   if (c->n_npcs > 0 && (c->npc_health < 1 || c->npc_health > 127))
@@ -2563,6 +2709,8 @@ int check_state(const orx_cfg_t* c, const orx_state_t* s, bool full) {
     return fail(ORX_EINVAL, "ret_sum / ep_count are NULL");
   if (c->n_npcs > 0 && (!s->npc_pos || !s->npc_health || !s->npc_alive))
     return fail(ORX_EINVAL, "n_npcs > 0 needs npc_pos, npc_health and npc_alive");
+  if (c->n_npcs > ORX_MAX_REG_NPCS && !s->npc_grid)
+    return fail(ORX_EINVAL, "n_npcs > 16 needs npc_grid ([B][W * H] uint8)");
   if (c->n_layouts > 0 && (!s->p_layout || !s->bank_tiles || !s->bank_ground || !s->bank_meta))
     return fail(ORX_EINVAL, "n_layouts > 0 needs p_layout and the bank_* arrays");
   if ((c->flags & ORX_EXT_SEPARATION_DAMAGE) && !s->sep_start)
@@ -2606,7 +2754,9 @@ int check_sizes(int64_t B, int64_t off) {
 }
 
 // NPC slot capacity of the kernel instance for K NPCs.
-inline int ncap_for(int K) { return K == 0 ? 0 : K <= 8 ? 8 : 16; }
+inline int ncap_for(int K) {
+  return K == 0 ? 0 : K <= 8 ? 8 : K <= ORX_MAX_REG_NPCS ? 16 : kDense;
+}
 
 // Games per rollout wave.  A rollout lane runs its game's whole tick stream,
 // so a wave's time is set by its instruction stream, not by how many of its
@@ -2703,8 +2853,8 @@ int orx_reset(const orx_cfg_t* cfg, const orx_state_t* st, const uint8_t* mask, 
 #define ORX_RESET(N, G)                                                                         \
   if (nc == N && grid == G)                                                                     \
     hipLaunchKernelGGL((mt_reset_kernel<N, G>), grid_for(B), dim3(kBlock), 0, s, *cfg, *st, mask, B);
-    ORX_RESET(0, false) ORX_RESET(8, false) ORX_RESET(16, false)
-    ORX_RESET(0, true) ORX_RESET(8, true) ORX_RESET(16, true)
+    ORX_RESET(0, false) ORX_RESET(8, false) ORX_RESET(16, false) ORX_RESET(kDense, false)
+    ORX_RESET(0, true) ORX_RESET(8, true) ORX_RESET(16, true) ORX_RESET(kDense, true)
 #undef ORX_RESET
     return launch_status("orx_reset");
   }
@@ -2712,8 +2862,8 @@ int orx_reset(const orx_cfg_t* cfg, const orx_state_t* st, const uint8_t* mask, 
   if (nc == N && grid == G)                                                                     \
     hipLaunchKernelGGL((reset_kernel<N, G>), grid_for(B), dim3(kBlock), 0, s, *cfg, *st, mask, B, \
                        k, off);
-  ORX_RESET(0, false) ORX_RESET(8, false) ORX_RESET(16, false)
-  ORX_RESET(0, true) ORX_RESET(8, true) ORX_RESET(16, true)
+  ORX_RESET(0, false) ORX_RESET(8, false) ORX_RESET(16, false) ORX_RESET(kDense, false)
+  ORX_RESET(0, true) ORX_RESET(8, true) ORX_RESET(16, true) ORX_RESET(kDense, true)
 #undef ORX_RESET
   return launch_status("orx_reset");
 }
@@ -2747,6 +2897,8 @@ static int launch_step(const orx_cfg_t* cfg, const orx_state_t* st, const int8_t
   ORX_STEP(8, true, false) ORX_STEP(16, false, false) ORX_STEP(16, true, false)
   ORX_STEP(0, false, true) ORX_STEP(0, true, true) ORX_STEP(8, false, true)
   ORX_STEP(8, true, true) ORX_STEP(16, false, true) ORX_STEP(16, true, true)
+  ORX_STEP(kDense, false, false) ORX_STEP(kDense, true, false)
+  ORX_STEP(kDense, false, true) ORX_STEP(kDense, true, true)
 #undef ORX_STEP
   return launch_status(name);
 }
@@ -2810,8 +2962,8 @@ int orx_rollout(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p1, 
   if (nc == N && grid == G)                                                                     \
     hipLaunchKernelGGL((mt_rollout_kernel<N, G>), grid_for(B), dim3(kBlock), 0, s, *cfg, *st,   \
                        policy_p1, policy_p2, n_ticks, obs, act, B, k, off);
-    ORX_ROLLOUT(0, false) ORX_ROLLOUT(8, false) ORX_ROLLOUT(16, false)
-    ORX_ROLLOUT(0, true) ORX_ROLLOUT(8, true) ORX_ROLLOUT(16, true)
+    ORX_ROLLOUT(0, false) ORX_ROLLOUT(8, false) ORX_ROLLOUT(16, false) ORX_ROLLOUT(kDense, false)
+    ORX_ROLLOUT(0, true) ORX_ROLLOUT(8, true) ORX_ROLLOUT(16, true) ORX_ROLLOUT(kDense, true)
 #undef ORX_ROLLOUT
     return launch_status("orx_rollout");
   }
@@ -2829,12 +2981,28 @@ int orx_rollout(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p1, 
   const uint64_t tiles = grid ? (uint64_t)cfg->n_layouts * (uint64_t)(cfg->width * cfg->height) : 0;
   const bool use_lds = tiles && tiles <= kMaxLdsTiles && !getenv("ORX_NO_LDS_TILES");
   const uint32_t lds_n = use_lds ? (uint32_t)tiles : 0u;
-  const uint32_t lds = use_lds ? (uint32_t)((tiles + 15u) & ~15ull) : 0u;
+  uint32_t lds = use_lds ? (uint32_t)((tiles + 15u) & ~15ull) : 0u;
+  // dense NPCs: one occupancy bitmap per game of the block after the tiles,
+  // when they fit the CU's LDS (a workgroup may take all 160 KiB on gfx950)
+  uint32_t lds_bits = 0;
+  if (nc == kDense && !getenv("ORX_NO_LDS_BITS")) {
+    const uint32_t bb = (uint32_t)((cfg->width * cfg->height + 31) / 32) * 4u;
+    if ((uint64_t)lds + (uint64_t)per_block * bb <= kMaxLdsBlock) {
+      lds_bits = bb;
+      lds += per_block * bb;
+    }
+  }
 #define ORX_ROLLOUT(N, P, G)                                                                    \
-  if (nc == N && pm == P && grid == G)                                                          \
+  if (nc == N && pm == P && grid == G) {                                                        \
+    if (lds > 65536u &&                                                                         \
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&rollout_kernel<N, P, G>),            \
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) \
+      return fail(ORX_EIO, "orx_rollout: cannot raise the LDS limit");                          \
     hipLaunchKernelGGL((rollout_kernel<N, P, G>), dim3((B + per_block - 1) / per_block),        \
                        dim3(kRolloutBlock), lds, s, *cfg, *st,                                  \
-                       policy_p1, policy_p2, n_ticks, obs, act, B, k, off, lanes, lds_n);
+                       policy_p1, policy_p2, n_ticks, obs, act, B, k, off, lanes, lds_n,        \
+                       lds_bits);                                                               \
+  }
   ORX_ROLLOUT(0, 0, false) ORX_ROLLOUT(0, 1, false) ORX_ROLLOUT(0, 2, false)
   ORX_ROLLOUT(8, 0, false) ORX_ROLLOUT(8, 1, false) ORX_ROLLOUT(8, 2, false)
   ORX_ROLLOUT(16, 0, false) ORX_ROLLOUT(16, 1, false) ORX_ROLLOUT(16, 2, false)
@@ -2843,6 +3011,8 @@ int orx_rollout(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p1, 
   ORX_ROLLOUT(16, 0, true) ORX_ROLLOUT(16, 1, true) ORX_ROLLOUT(16, 2, true)
   ORX_ROLLOUT(0, 3, false) ORX_ROLLOUT(8, 3, false) ORX_ROLLOUT(16, 3, false)
   ORX_ROLLOUT(0, 3, true) ORX_ROLLOUT(8, 3, true) ORX_ROLLOUT(16, 3, true)
+  ORX_ROLLOUT(kDense, 0, false) ORX_ROLLOUT(kDense, 1, false) ORX_ROLLOUT(kDense, 2, false)
+  ORX_ROLLOUT(kDense, 0, true) ORX_ROLLOUT(kDense, 1, true) ORX_ROLLOUT(kDense, 2, true)
 #undef ORX_ROLLOUT
   return launch_status("orx_rollout");
 }

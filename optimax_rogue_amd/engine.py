@@ -18,7 +18,7 @@ import torch
 from . import _lib
 from .config import EnvConfig
 from .enums import (DSTORE, EXT_CHARACTER, EXT_ITEMS, EXT_SEPARATION_DAMAGE, MAX_EVENTS,
-                    N_COUNTERS, OBS_FIELDS, RNG_MT19937, RPG_FIELDS, Policy)
+                    MAX_REG_NPCS, N_COUNTERS, OBS_FIELDS, RNG_MT19937, RPG_FIELDS, Policy)
 
 STATE_FIELDS = ("p_x", "p_y", "p_depth", "p_health", "st_x", "st_y", "tick", "status", "episode",
                 "ret_sum", "ep_count", "counters", "npc_pos", "npc_health", "npc_alive")
@@ -65,7 +65,8 @@ class BatchedEngine:
         # uint16 / uint32 payloads are stored in same-width signed tensors
         self.npc_pos = z(max(K, 1), B, dt=torch.int16)
         self.npc_health = z(max(K, 1), B, dt=torch.int8)
-        self.npc_alive = z(B)
+        # alive bits: [B] for K <= 32, rows of 32 above (include/orx.h)
+        self.npc_alive = z(B) if K <= 32 else z((K + 31) // 32, B)
         self.actions = torch.full((B, 2), 5, dtype=torch.int8, device=device)
         ptrs = {f: getattr(self, f).data_ptr() for f in STATE_FIELDS}
         # explicit-grid dungeon generator (cfg.layouts): the bank and each
@@ -108,6 +109,13 @@ class BatchedEngine:
                 self.item_pos = z(K, B, dt=torch.int16)
                 self.item_mask = z(2, B)
                 ptrs.update(item_pos=self.item_pos.data_ptr(), item_mask=self.item_mask.data_ptr())
+        # dense NPCs (K > MAX_REG_NPCS): each game's occupancy grid of the NPC
+        # depth in HBM (slot + 1 per cell; 4 KiB per 64x64 game)
+        self.npc_grid = None
+        if K > MAX_REG_NPCS:
+            self.npc_grid = torch.zeros((B, int(cfg.width) * int(cfg.height)), dtype=torch.uint8,
+                                        device=device)
+            ptrs["npc_grid"] = self.npc_grid.data_ptr()
         self._st = _lib.OrxState(**ptrs)
         self._pcfg, self._pst = ctypes.byref(self._ccfg), ctypes.byref(self._st)
         if self.mt_py is not None:
@@ -291,6 +299,20 @@ class BatchedEngine:
             else:
                 a = a.astype(np.int32)
             dst.copy_(torch.from_numpy(a.reshape(dst.shape)))
+        if self.npc_grid is not None and ("npc_pos" in snap or "npc_alive" in snap):
+            self._rebuild_npc_grid()
+
+    def _rebuild_npc_grid(self) -> None:
+        """Dense NPCs: the occupancy grid (slot + 1 per cell of the NPC depth)
+        from npc_pos / npc_alive, after state was written from the host."""
+        from .enums import npc_alive_bits
+        K, B, H = self.K, self.B, int(self.cfg.height)
+        pos = self.npc_pos[:K].cpu().numpy().view(np.uint16).astype(np.int64)
+        live = npc_alive_bits(self.npc_alive.cpu().numpy().view(np.uint32), K)
+        grid = np.zeros((B, int(self.cfg.width) * H), np.uint8)
+        k, g = np.nonzero(live)
+        grid[g, (pos[k, g] & 0xFF) * H + (pos[k, g] >> 8)] = (k + 1).astype(np.uint8)
+        self.npc_grid.copy_(torch.from_numpy(grid))
 
     def dungeon_stairs(self, games, episodes, depths, gens) -> np.ndarray:
         """Staircase and layout of (local game, episode, depth, generation)

@@ -84,7 +84,19 @@ DSTORE = 256        # ORX_DSTORE: remembered dungeons per game in stock-seed mod
 # per-game event counter rows (include/orx.h ORX_CNT_*)
 CNT_COMBAT, CNT_DESCEND, CNT_DUNGEON, CNT_NPC_DEATH = range(4)
 N_COUNTERS = 4
-MAX_NPCS = 16
+MAX_NPCS = 255       # ORX_MAX_NPCS
+MAX_REG_NPCS = 16    # ORX_MAX_REG_NPCS: above, the NPCs live in an HBM occupancy grid
+
+
+def npc_alive_bits(alive, K: int):
+    """bool [K, B] from an npc_alive array ([B] for K <= 32, else
+    [ceil(K / 32), B] rows of 32 bits)."""
+    import numpy as np
+    a = np.asarray(alive).astype(np.uint64)
+    if a.ndim == 1:
+        a = a[None, :]
+    k = np.arange(K)
+    return ((a[k // 32] >> (k % 32)[:, None].astype(np.uint64)) & 1).astype(bool)
 
 OBS_FIELDS = ("p1_x", "p1_y", "p1_depth", "p1_health", "p2_x", "p2_y", "p2_depth",
               "p2_health", "tick", "status", "p1_stair_x", "p1_stair_y", "p2_stair_x",

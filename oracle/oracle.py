@@ -156,7 +156,7 @@ class Oracle:
         out["counters"] = np.zeros((4, B), np.int32)
         out["npc_pos"] = np.zeros((K, B), np.uint16)
         out["npc_health"] = np.zeros((K, B), np.int8)
-        out["npc_alive"] = np.zeros(B, np.uint32)
+        out["npc_alive"] = np.zeros(B if K <= 32 else ((K + 31) // 32, B), np.uint32)
         order = ["p_x", "p_y", "p_depth", "p_health", "st_x", "st_y", "tick", "status",
                  "episode", "ret_sum", "ep_count", "counters", "npc_pos", "npc_health",
                  "npc_alive"]

@@ -92,8 +92,8 @@ def compare_state(got: dict, want: dict, K: int, where: str = ""):
         w = np.asarray(want[k])
         if k in ("npc_pos", "npc_health", "item_pos"):
             # dead NPC slots / taken items are unspecified: compare live slots only
-            alive = np.asarray(want["item_mask"][0] if k == "item_pos" else want["npc_alive"])
-            mask = ((alive[None, :] >> np.arange(K)[:, None]) & 1).astype(bool)
+            from optimax_rogue_amd.enums import npc_alive_bits
+            mask = npc_alive_bits(want["item_mask"][0] if k == "item_pos" else want["npc_alive"], K)
             g = np.where(mask, g, 0)
             w = np.where(mask, w, 0)
         if g.shape != w.shape or not np.array_equal(g.astype(np.int64), w.astype(np.int64)):

@@ -87,10 +87,12 @@ def test_enum_values_match_header():
 def test_validate_cfg(lib):
     from optimax_rogue_amd import EnvConfig
     ok = [EnvConfig.c1(), EnvConfig.c3(), EnvConfig.c5(), EnvConfig(width=4, height=4),
+          EnvConfig(n_npcs=17), EnvConfig(n_npcs=255, width=20, height=20),
           EnvConfig(start_mode=2, p1_depth=0, p2_depth=1000, n_npcs=16, width=40, height=10)]
     bad = [EnvConfig(width=3), EnvConfig(despawn=3), EnvConfig(start_mode=2, p1_depth=5,
                                                                 p2_depth=5),
-           EnvConfig(n_npcs=17), EnvConfig(n_npcs=2, width=300), EnvConfig(max_ticks=-1),
+           EnvConfig(n_npcs=256), EnvConfig(n_npcs=2, width=300), EnvConfig(max_ticks=-1),
+           EnvConfig(n_npcs=17, flags=32),
            EnvConfig(width=4, height=4, n_npcs=2), EnvConfig(flags=1),
            EnvConfig(n_npcs=1, npc_health=0)]
     # dungeon bank: n_layouts rides in the struct (the layouts themselves are

@@ -135,6 +135,19 @@ ORACLE_CASES = {
     # rollout's descend-into-the-other's-depth path in both drawn orders
     "desc_meet_5x4": (dict(width=5, height=4, start_mode=2, p1_depth=2, p2_depth=1,
                            max_ticks=200), (1, 2), 2048, 200, 25),
+    # dense NPCs (K > 16): the occupancy-grid form, from crowded to packed
+    "npc_dense_40_16x16": (dict(width=16, height=16, n_npcs=40, npc_health=2, max_ticks=150),
+                           (1, 2), 2048, 300, 40),
+    "npc_dense_200_20x20": (dict(width=20, height=20, n_npcs=200, npc_health=1, max_ticks=80,
+                                 despawn=2), (1, 1), 1024, 200, 41),
+    "npc_dense_64_c3": (dict(width=64, height=64, n_npcs=64, max_ticks=1000), (1, 1), 4096, 400,
+                        42),
+    "npc_dense_bank": (dict(width=12, height=10, n_npcs=24, max_ticks=200, start_mode=2,
+                            p1_depth=1, p2_depth=0), (2, 1), 2048, 300, 43),
+    "npc_dense_stock": (dict(width=10, height=9, n_npcs=20, despawn=2, max_ticks=150, rng=1),
+                        (1, 2), 1024, 300, 44),
+    "npc_dense_rpg": (dict(width=12, height=12, n_npcs=30, npc_health=2, max_ticks=200,
+                           flags=4 | 16 | 64, xp_per_level=2), (1, 1), 2048, 300, 45),
     # build extensions (readme-only mechanics, parity unpinned: engine vs oracle)
     "ext_separation": (dict(width=9, height=9, start_mode=2, p1_depth=0, p2_depth=2, n_npcs=2,
                             max_ticks=300, flags=1, sep_period=4), (2, 1), 2048, 400, 17),
@@ -150,6 +163,7 @@ ORACLE_CASES = {
                        rng=1), (1, 1), 2048, 200, 23),
 }
 ORACLE_BANKS = {"bank_64_npc": (64, 64, 16, 21, (1,)), "bank_stairs_unused": (12, 10, 5, 22, (1, 3)),
+                "npc_dense_bank": (12, 10, 6, 46, (1, 2)),
                 "bank_big_global": (36, 36, 64, 27, (1, 2)),
                 "stock_bank_separated": (12, 10, 7, 24, (1, 2))}
 
@@ -175,7 +189,24 @@ def test_vs_oracle_large(name, oracle_lib):
         want = ora.export()
         compare_state(eng.snapshot(), want, ora.K, f"{name} step chunk {c}")
         compare_state(eng2.snapshot(), want, ora.K, f"{name} rollout chunk {c}")
+        for e in (eng, eng2):
+            if e.npc_grid is not None:
+                _check_npc_grid(e, want, f"{name} chunk {c}")
     torch.cuda.synchronize()
+
+
+def _check_npc_grid(eng, snap, where):
+    """Dense NPCs: the HBM occupancy grid holds slot + 1 exactly on the live
+    NPCs' cells and 0 elsewhere."""
+    from optimax_rogue_amd.enums import npc_alive_bits
+    K, H = eng.K, int(eng.cfg.height)
+    grid = eng.npc_grid.cpu().numpy()
+    want = np.zeros_like(grid)
+    live = npc_alive_bits(snap["npc_alive"], K)
+    pos = np.asarray(snap["npc_pos"]).astype(np.int64)
+    k, g = np.nonzero(live)
+    want[g, (pos[k, g] & 0xFF) * H + (pos[k, g] >> 8)] = k + 1
+    assert np.array_equal(grid, want), where
 
 
 def test_ext_events_vs_oracle(oracle_lib):
