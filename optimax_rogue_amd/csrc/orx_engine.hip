@@ -2189,7 +2189,11 @@ struct TrajWriter {
     if constexpr (FAST) {
 #pragma unroll
       for (int f = 0; f < ORX_OBS_FIELDS; ++f) {
+#ifdef ORX_OBS_TILED  // diagnostic: [T][B/64][14][64] tiles (B a multiple of 64)
+        vo[f] = ((i >> 6) * (uint32_t)ORX_OBS_FIELDS * 64u + (uint32_t)f * 64u + (i & 63u)) * 4u;
+#else
         vo[f] = i * 4u + (uint32_t)f * B * 4u;
+#endif
         asm volatile("" : "+v"(vo[f]));
       }
       va = i * 2u;
