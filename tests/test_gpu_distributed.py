@@ -50,3 +50,37 @@ def test_two_ranks_equal_one_process(tmp_path, global_batch):
     assert got.shape == want.shape
     assert np.array_equal(got, want)
     assert want[1].sum() >= global_batch  # every game finished an episode
+
+
+def test_c4_eight_shards_equal_whole_batch():
+    """BASELINE configs[3] (C4) at its full size: 524,288 games as the eight
+    per-GPU shards of parallel.shard (each a BatchedEngine at its game_offset,
+    here on one card) equal one engine over all 524,288 games -- state, and
+    the per-game returns gather_returns would assemble in global id order."""
+    import torch
+    from golden_util import STATE_KEYS
+    from optimax_rogue_amd import EnvConfig
+    from optimax_rogue_amd.engine import BatchedEngine
+    from optimax_rogue_amd.parallel import shard
+    G, T, dev = 524288, 64, torch.device("cuda", 0)
+    cfg = EnvConfig.c4()
+    cfg.max_ticks = 40          # episodes end inside the window
+    whole = BatchedEngine(cfg, G, seed=4, device=dev)
+    whole.rollout(T, 1, 1)
+    want = whole.snapshot()
+    want_ret = whole.episode_returns().cpu().numpy()
+    del whole
+    parts, rets = [], []
+    for r in range(8):
+        off, cnt = shard(G, r, 8)
+        e = BatchedEngine(cfg, cnt, seed=4, game_offset=off, device=dev)
+        e.rollout(T, 1, 1)
+        parts.append(e.snapshot())
+        rets.append(e.episode_returns().cpu().numpy())
+        del e
+    for k in STATE_KEYS:
+        got = np.concatenate([p[k] for p in parts], axis=np.asarray(want[k]).ndim - 1)
+        assert np.array_equal(got, want[k]), k
+    assert np.array_equal(np.concatenate(rets, axis=1), want_ret)
+    assert want_ret[1].sum() >= G   # every game finished at least one episode
+    torch.cuda.synchronize()
