@@ -314,6 +314,32 @@ class BatchedEngine:
         grid[g, (pos[k, g] & 0xFF) * H + (pos[k, g] >> 8)] = (k + 1).astype(np.uint8)
         self.npc_grid.copy_(torch.from_numpy(grid))
 
+    # -- checkpoint / resume -------------------------------------------------
+    def save(self, path) -> None:
+        """Checkpoint: the whole SoA state (snapshot()) with the configuration,
+        seed and game offset, as one .npz (the reference's counterpart is a
+        GameState.to_prims snapshot per game, state.py:94-132)."""
+        import json
+        snap = self.snapshot()
+        extra = {} if self.cfg.layouts is None else {"layouts": np.asarray(self.cfg.layouts)}
+        np.savez(path, cfg_json=np.frombuffer(json.dumps(self.cfg.to_dict()).encode(), np.uint8),
+                 seed=np.array([self.seed], np.uint64),
+                 game_offset=np.array([self.game_offset], np.int64), **extra, **snap)
+
+    @classmethod
+    def load(cls, path, device: Optional[torch.device] = None) -> "BatchedEngine":
+        """Resume from save(): a new engine whose state, and therefore every
+        later tick, equals the saved one's."""
+        import json
+        z = np.load(path, allow_pickle=False)
+        cfg = EnvConfig.from_dict(json.loads(bytes(z["cfg_json"]).decode()),
+                                  layouts=z["layouts"] if "layouts" in z.files else None)
+        n = int(np.asarray(z["tick"]).shape[-1])
+        eng = cls(cfg, n, seed=int(z["seed"][0]), game_offset=int(z["game_offset"][0]),
+                  device=device, reset=False)
+        eng.load_snapshot({k: z[k] for k in z.files})
+        return eng
+
     def dungeon_stairs(self, games, episodes, depths, gens) -> np.ndarray:
         """Staircase and layout of (local game, episode, depth, generation)
         dungeons via orx_dungeon_spawn; returns int32 [n, 3] (sx, sy, layout;
