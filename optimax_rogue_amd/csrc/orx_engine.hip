@@ -425,9 +425,14 @@ struct Npcs<kDense> {
     }
   }
   __device__ __forceinline__ void clear() {  // the grid and the alive rows
-    uint32_t* g4 = reinterpret_cast<uint32_t*>(grid);
-    for (int j = 0; j < (cells >> 2); ++j) g4[j] = 0u;
-    for (int j = cells & ~3; j < cells; ++j) grid[j] = 0;
+    // (a game's row starts on a 4-byte boundary only when W * H is a
+    // multiple of 4: bytes up to the first boundary, words, the tail bytes)
+    const int head = min((int)((4u - ((uint32_t)(uintptr_t)grid & 3u)) & 3u), cells);
+    for (int j = 0; j < head; ++j) grid[j] = 0;
+    uint32_t* g4 = reinterpret_cast<uint32_t*>(grid + head);
+    const int words = (cells - head) >> 2;
+    for (int j = 0; j < words; ++j) g4[j] = 0u;
+    for (int j = head + 4 * words; j < cells; ++j) grid[j] = 0;
     for (int r = 0; r < (K + 31) >> 5; ++r) rows[(size_t)r * B] = 0u;
     if (staged) clear_bits();
   }
@@ -2796,6 +2801,17 @@ int lanes_override() {  // read per launch, so a sweep can change it in-process
   return (x >= 1 && x <= 64 && (x & (x - 1)) == 0) ? x : 0;
 }
 
+// Threads per rollout workgroup: kRolloutBlock (env ORX_ROLLOUT_THREADS = 64
+// / 128 / 256 overrides, for measurements).
+uint32_t rollout_threads(uint32_t B, uint32_t lanes) {
+  const char* e = getenv("ORX_ROLLOUT_THREADS");
+  const int x = e ? atoi(e) : 0;
+  if (x == 64 || x == 128 || x == 256) return (uint32_t)x;
+  (void)B; (void)lanes;  // single-wave workgroups for small batches measured within
+                         // +-3% (profiles/r02_v6/threads_ab.jsonl): not the default
+  return (uint32_t)kRolloutBlock;
+}
+
 uint32_t rollout_lanes(uint32_t B) {
   if (const int o = lanes_override()) return (uint32_t)o;
   const uint64_t simds = (uint64_t)device_simds();
@@ -2980,7 +2996,8 @@ int orx_rollout(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p1, 
                  : ((cfg->flags | ORX_EXT_HEAL) == ORX_EXT_RPG && both_random) ? 3
                  : 0;
   const uint32_t lanes = rollout_lanes(B);
-  const uint32_t per_block = (uint32_t)kRolloutBlock / 64u * lanes;
+  const uint32_t threads = rollout_threads(B, lanes);
+  const uint32_t per_block = threads / 64u * lanes;
   // dynamic LDS: the bank's tiles when they fit (rollout_kernel stages them)
   const uint64_t tiles = grid ? (uint64_t)cfg->n_layouts * (uint64_t)(cfg->width * cfg->height) : 0;
   const bool use_lds = tiles && tiles <= kMaxLdsTiles && !getenv("ORX_NO_LDS_TILES");
@@ -3003,7 +3020,7 @@ int orx_rollout(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p1, 
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) \
       return fail(ORX_EIO, "orx_rollout: cannot raise the LDS limit");                          \
     hipLaunchKernelGGL((rollout_kernel<N, P, G>), dim3((B + per_block - 1) / per_block),        \
-                       dim3(kRolloutBlock), lds, s, *cfg, *st,                                  \
+                       dim3(threads), lds, s, *cfg, *st,                                        \
                        policy_p1, policy_p2, n_ticks, obs, act, B, k, off, lanes, lds_n,        \
                        lds_bits);                                                               \
   }

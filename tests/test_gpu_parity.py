@@ -146,6 +146,9 @@ ORACLE_CASES = {
                             p1_depth=1, p2_depth=0), (2, 1), 2048, 300, 43),
     "npc_dense_stock": (dict(width=10, height=9, n_npcs=20, despawn=2, max_ticks=150, rng=1),
                         (1, 2), 1024, 300, 44),
+    # W * H = 99: the game rows of the grid start at every byte offset mod 4
+    "npc_dense_odd_9x11": (dict(width=9, height=11, n_npcs=21, npc_health=1, max_ticks=40),
+                           (1, 1), 1023, 200, 47),
     "npc_dense_rpg": (dict(width=12, height=12, n_npcs=30, npc_health=2, max_ticks=200,
                            flags=4 | 16 | 64, xp_per_level=2), (1, 1), 2048, 300, 45),
     # build extensions (readme-only mechanics, parity unpinned: engine vs oracle)
