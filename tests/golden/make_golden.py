@@ -597,6 +597,13 @@ CASES = {
                                             layouts=make_layouts(8, 9, 3, 104, n_stairs=(1, 2))),
                                    seed=4000, games=12, ticks=320),
     # a one-layout bank (no dungeon draw), Separated start, both StaircaseBots
+    # dense NPCs (more than the engine's 16 register slots: its occupancy-grid
+    # form); the reference's updater takes any number of entities
+    "dense_npc_12x12": dict(cfg=dict(width=12, height=12, n_npcs=30, npc_health=2,
+                                     max_ticks=120), seed=61, games=12, ticks=300),
+    "dense_npc_64": dict(cfg=dict(width=64, height=64, n_npcs=32), seed=62, games=8, ticks=400),
+    "dense_npc_stairs": dict(cfg=dict(width=10, height=9, n_npcs=20, max_ticks=100, despawn=2,
+                                      policy=(2, 1)), seed=63, games=12, ticks=260),
     # games whose first tick's draws overflow the tick block (fallback streams)
     "overflow_shuffle": dict(cfg=dict(width=6, height=6, max_ticks=30), seed=5, games=3,
                              ticks=40, offset=("shuffle", 5, 0, 1)),
