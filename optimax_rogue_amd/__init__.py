@@ -10,7 +10,8 @@ from .enums import (CombatFlag, DungeonDespawningStrategy, Move, OBS_FIELDS, Pol
                     Tile, UpdateResult)
 
 __all__ = ["EnvConfig", "DungeonBank", "Move", "UpdateResult", "DungeonDespawningStrategy", "Tile", "CombatFlag",
-           "StartMode", "Policy", "OBS_FIELDS", "BatchedEngine", "StreamShardedEngine", "BatchedUpdater"]
+           "StartMode", "Policy", "OBS_FIELDS", "BatchedEngine", "StreamShardedEngine", "BatchedUpdater",
+           "VecEnv"]
 
 
 def __getattr__(name):
@@ -21,4 +22,7 @@ def __getattr__(name):
     if name == "BatchedUpdater":
         from .updater import BatchedUpdater
         return BatchedUpdater
+    if name == "VecEnv":
+        from .vecenv import VecEnv
+        return VecEnv
     raise AttributeError(name)

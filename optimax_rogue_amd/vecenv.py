@@ -1,0 +1,102 @@
+"""VecEnv: the learner-facing batched environment over BatchedEngine.
+
+The reference runs one game per server process and hands each bot a
+``GameState`` view every tick (server/main.py:110-113,
+optimax_rogue_bots/main.py:118-155).  A learner over hundreds of thousands of
+games wants tensors instead: this wraps the engine's C-ABI calls in the
+usual reset / step / rollout shape, everything resident on the GPU.
+
+* observation: int32 [n_games, 14], the fields of ``OBS_FIELDS`` (the same
+  row ``orx_rollout`` writes per tick);
+* reward: float32 [n_games], player 1's view: +1 Player1Win, -1 Player2Win,
+  0 otherwise, on the step that ends an episode;
+* done: bool [n_games], that step.  The step after ``done`` starts the game's
+  next episode (the engine's autoreset: that step's actions are not played).
+
+Player 2 is the learner's opponent: a device policy (``Policy.Random``,
+``Policy.Staircase``, ``Policy.Stay``), or ``None`` for self-play, where
+``step`` takes both players' actions.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from .config import EnvConfig
+from .engine import BatchedEngine
+from .enums import OBS_FIELDS, Policy, UpdateResult
+
+_STATUS = OBS_FIELDS.index("status")
+
+
+class VecEnv:
+    def __init__(self, cfg: EnvConfig, n_games: int, seed: int = 0, game_offset: int = 0,
+                 device: Optional[torch.device] = None,
+                 opponent: Optional[int] = Policy.Random):
+        if not int(cfg.autoreset):
+            raise ValueError("VecEnv needs cfg.autoreset = 1 (finished games restart)")
+        self.engine = BatchedEngine(cfg, n_games, seed=seed, game_offset=game_offset,
+                                    device=device)
+        self.B = self.engine.B
+        self.device = self.engine.device
+        self.opponent = None if opponent is None else int(opponent)
+
+    # -- observation -----------------------------------------------------------
+    def observe(self) -> torch.Tensor:
+        """The current observation rows, int32 [n_games, 14] (OBS_FIELDS order)."""
+        e = self.engine
+        return torch.stack([e.p_x[0], e.p_y[0], e.p_depth[0], e.p_health[0],
+                            e.p_x[1], e.p_y[1], e.p_depth[1], e.p_health[1],
+                            e.tick, e.status, e.st_x[0], e.st_y[0], e.st_x[1], e.st_y[1]], dim=1)
+
+    @staticmethod
+    def outcome(before: torch.Tensor, after: torch.Tensor):
+        """(reward, done) of a transition between two status tensors."""
+        done = (before == UpdateResult.InProgress) & (after >= UpdateResult.Player1Win) \
+            & (after <= UpdateResult.Tie)
+        reward = torch.where(done, (after == UpdateResult.Player1Win).float()
+                             - (after == UpdateResult.Player2Win).float(),
+                             torch.zeros((), device=after.device))
+        return reward, done
+
+    # -- reset / step / rollout ----------------------------------------------------
+    def reset(self, mask: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Starts the masked games (all if None) at their next episode's setup."""
+        self.engine.reset(mask)
+        return self.observe()
+
+    def step(self, actions: torch.Tensor):
+        """Plays one tick: ``actions`` int8 [n_games] (player 1; the opponent
+        policy moves player 2) or [n_games, 2] (self-play).  Returns
+        (observation, reward, done, status)."""
+        e = self.engine
+        a = actions.to(device=self.device, dtype=torch.int8)
+        if a.dim() == 1:
+            if self.opponent is None:
+                raise ValueError("self-play (opponent=None) takes [n_games, 2] actions")
+            e.actions[:, 0].copy_(a)
+            e.policy(Policy.NONE, self.opponent)   # player 2's move; player 1's kept
+        else:
+            e.actions.copy_(a)
+        before = e.status.clone()
+        status = e.step(e.actions)
+        reward, done = self.outcome(before, status)
+        return self.observe(), reward, done, status
+
+    def rollout(self, n_ticks: int, p1: int = Policy.Random, p2: Optional[int] = None) -> dict:
+        """``n_ticks`` ticks with device policies for both players in one fused
+        launch (orx_rollout).  Returns obs int32 [T, 14, n_games], act int8
+        [T, n_games, 2], reward float32 [T, n_games], done bool [T, n_games]."""
+        p2 = self.opponent if p2 is None else int(p2)
+        if p2 is None:
+            raise ValueError("rollout needs a policy for player 2")
+        e = self.engine
+        obs = torch.empty((n_ticks, len(OBS_FIELDS), self.B), dtype=torch.int32, device=self.device)
+        act = torch.empty((n_ticks, self.B, 2), dtype=torch.int8, device=self.device)
+        before = e.status.clone()
+        e.rollout(n_ticks, int(p1), p2, obs=obs, act=act)
+        status = obs[:, _STATUS]
+        prev = torch.cat([before[None], status[:-1]], dim=0)
+        reward, done = self.outcome(prev, status)
+        return {"obs": obs, "act": act, "reward": reward, "done": done}

@@ -248,3 +248,41 @@ def test_checkpoint_resume(case, tmp_path):
         assert np.array_equal(sa[k], sb[k]), (case, k)
     if a.npc_grid is not None:
         assert torch.equal(a.npc_grid, b.npc_grid)
+
+
+def test_vecenv_step_and_rollout(oracle_lib):
+    """VecEnv against the oracle: observations are the state rows, the
+    rewards / dones of every step sum to the oracle's episode returns and
+    counts; rollout's rewards equal the engine's own return bookkeeping."""
+    import torch
+    from optimax_rogue_amd import EnvConfig, VecEnv
+    cfg = EnvConfig(width=6, height=6, n_npcs=2, max_ticks=25, player_health=3)
+    B, dev = 1024, torch.device("cuda", 0)
+    env = VecEnv(cfg, B, seed=9, device=dev, opponent=2)     # StaircaseBot opponent
+    ora = oracle_lib.Oracle(cfg.to_dict(), B, 9)
+    ora.reset(episode=np.zeros(B, np.int32))
+    obs = env.reset()
+    rs = np.random.RandomState(2)
+    rew_sum = np.zeros(B)
+    dones = np.zeros(B, np.int64)
+    for t in range(120):
+        a1 = rs.randint(1, 6, size=B).astype(np.int8)
+        want_a = ora.policy(0, 2, np.stack([a1, np.full(B, 5, np.int8)], 1))
+        ora.step(want_a)
+        obs, r, d, _ = env.step(torch.from_numpy(a1))
+        ex = ora.export()
+        want = np.stack([ex["p_x"][0], ex["p_y"][0], ex["p_depth"][0], ex["p_health"][0],
+                         ex["p_x"][1], ex["p_y"][1], ex["p_depth"][1], ex["p_health"][1],
+                         ex["tick"], ex["status"], ex["st_x"][0], ex["st_y"][0],
+                         ex["st_x"][1], ex["st_y"][1]], 1)
+        assert np.array_equal(obs.cpu().numpy(), want), t
+        rew_sum += r.cpu().numpy()
+        dones += d.cpu().numpy()
+    ex = ora.export()
+    assert np.array_equal(rew_sum, ex["ret_sum"]) and np.array_equal(dones, ex["ep_count"])
+    assert dones.sum() > B // 2
+    before = env.engine.episode_returns().cpu().numpy().copy()
+    out = env.rollout(200, 1, 2)
+    after = env.engine.episode_returns().cpu().numpy()
+    assert np.array_equal(out["reward"].sum(0).cpu().numpy(), after[0] - before[0])
+    assert np.array_equal(out["done"].sum(0).cpu().numpy(), after[1] - before[1])
