@@ -2182,7 +2182,10 @@ __device__ __forceinline__ void rollout_tick(const Cfg& c, const orx_state_t& st
 // otherwise per-pointer checks and flat stores.  Nontemporal: the rows are
 // written once and read by the caller later (measured -4% per launch).
 constexpr int32_t kBufferDword3 = 0x00020000;  // gfx9 raw buffer, 32-bit elements
-constexpr int32_t kStreamAux = 2;               // cache policy nt
+#ifndef ORX_STREAM_AUX
+#define ORX_STREAM_AUX 2
+#endif
+constexpr int32_t kStreamAux = ORX_STREAM_AUX;  // cache policy: nt (measured)
 template <bool FAST>
 struct TrajWriter {
   int32_t* obs;
