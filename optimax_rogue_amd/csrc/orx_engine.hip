@@ -2322,23 +2322,6 @@ __global__ void __launch_bounds__(kRolloutBlock) rollout_kernel(orx_cfg_t hc, or
 #endif
   ORX_STAMP(1);
   int32_t t = 0;
-#ifdef ORX_PIPE_STORES  // diagnostic: tick t's row stored at the top of tick t + 1
-  if constexpr (kTraj) {
-    int32_t a1 = ORX_MOVE_STAY, a2 = ORX_MOVE_STAY;
-    rollout_tick<NCAP, GRID>(c, st, B, i, key, game, ep, pol1, pol2, p1, p2, npc, items, hp,
-                             tick, status, dl, sep, restarted, a1, a2);
-    Player q1 = p1, q2 = p2;
-    int32_t qt = tick, qs = status, qa1 = a1, qa2 = a2;
-    for (t = 1; t < n_ticks; ++t) {
-      traj.write(t - 1, q1, q2, qt, qs, qa1, qa2);
-      a1 = ORX_MOVE_STAY; a2 = ORX_MOVE_STAY;
-      rollout_tick<NCAP, GRID>(c, st, B, i, key, game, ep, pol1, pol2, p1, p2, npc, items, hp,
-                               tick, status, dl, sep, restarted, a1, a2);
-      q1 = p1; q2 = p2; qt = tick; qs = status; qa1 = a1; qa2 = a2;
-    }
-    traj.write(n_ticks - 1, q1, q2, qt, qs, qa1, qa2);
-  } else
-#endif
   do {  // n_ticks >= 1: orx_rollout returns before launching 0 ticks
 #ifdef ORX_STAMPS
     if (t == 64) { ORX_STAMP(2); }
