@@ -1,0 +1,54 @@
+"""CPU: host-side helpers that need no GPU (the engine itself is tested
+with -m gpu)."""
+import numpy as np
+import pytest
+
+
+def test_vecenv_outcome():
+    """reward / done of a status transition: only games in progress before
+    the step that end in it count; player 1's view."""
+    torch = pytest.importorskip("torch")
+    from optimax_rogue_amd.vecenv import VecEnv
+    before = torch.tensor([1, 1, 1, 1, 2, 3, 4, 16], dtype=torch.int32)
+    after = torch.tensor([1, 2, 3, 4, 1, 3, 4, 16], dtype=torch.int32)
+    reward, done = VecEnv.outcome(before, after)
+    assert done.tolist() == [False, True, True, True, False, False, False, False]
+    assert reward.tolist() == [0.0, 1.0, -1.0, 0.0, 0.0, 0.0, 0.0, 0.0]
+
+
+def test_npc_alive_bits():
+    from optimax_rogue_amd.enums import npc_alive_bits
+    a = np.array([0b101, 0xFFFFFFFF], np.uint32)
+    bits = npc_alive_bits(a, 3)
+    assert bits.shape == (3, 2)
+    assert bits[:, 0].tolist() == [True, False, True] and bits[:, 1].all()
+    rows = np.zeros((2, 3), np.uint32)       # K = 40: two rows of 32
+    rows[1, 2] = 1 << 7                      # NPC 39 of game 2
+    rows[0, 0] = 1 << 31                     # NPC 31 of game 0
+    b = npc_alive_bits(rows, 40)
+    assert b.shape == (40, 3)
+    assert sorted(zip(*np.nonzero(b))) == [(31, 0), (39, 2)]
+
+
+def test_env_config_round_trip():
+    """EnvConfig <-> dict <-> the orx_cfg_t mirror keeps every field."""
+    from optimax_rogue_amd import EnvConfig
+    from optimax_rogue_amd.config import CFG_FIELDS
+    c = EnvConfig(width=40, height=12, n_npcs=30, flags=4 | 16 | 64, mana_max=12,
+                  combat_cooldown=5, item_slots=2, rng=1)
+    d = c.to_dict()
+    assert set(d) == set(CFG_FIELDS)
+    c2 = EnvConfig.from_dict(d)
+    assert c2.to_dict() == d
+    cc = c.to_c()
+    assert [getattr(cc, f) for f in CFG_FIELDS] == [d[f] for f in CFG_FIELDS]
+
+
+def test_dungeon_bank_random_is_valid():
+    from optimax_rogue_amd import DungeonBank
+    bank = DungeonBank.random(12, 10, 5, seed=3, n_stairs=2)
+    assert bank.layouts.shape == (5, 12, 10)
+    for lay in bank.layouts:
+        assert (lay == 3).sum() == 2                  # two staircases
+        assert (lay[[0, -1], :] == 2).all() and (lay[:, [0, -1]] == 2).all()
+    assert bank.min_ground >= 2
