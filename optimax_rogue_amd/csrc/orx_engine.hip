@@ -465,8 +465,9 @@ struct Npcs<kDense> {
     const int k = find(key);
     return k >= 0 && is_alive(k);
   }
-  __device__ __forceinline__ void kill(int k) {
-    const int cl = cell(get(k));
+  __device__ __forceinline__ void kill(int k) { kill_at(get(k)); }
+  __device__ __forceinline__ void kill_at(uint32_t key) {  // the NPC on cell `key`
+    const int cl = cell(key);
     grid[cl] = 0;
     if (staged) lds()[boff + (cl >> 5)] &= ~(1u << (cl & 31));
   }
@@ -1336,7 +1337,8 @@ __device__ __forceinline__ bool handle_move(const Cfg& c, Key key, Src& src, Pla
 template <int NCAP, bool EV, class M>
 __device__ __forceinline__ void npc_hits(const Cfg& c, Npcs<NCAP>& npc, M& m, int h0, int h1,
                                          int d0, int d1, Deltas& dl, Events<EV>& ev,
-                                         bool& kill0, bool& kill1) {
+                                         bool& kill0, bool& kill1, uint32_t key0 = 0,
+                                         uint32_t key1 = 0) {
   int v0 = m.get(h0 >= 0 ? h0 : h1), v1 = m.get(h1 >= 0 ? h1 : h0);
   if (h0 >= 0) v0 -= d0;
   const int v0a = v0;
@@ -1350,12 +1352,17 @@ __device__ __forceinline__ void npc_hits(const Cfg& c, Npcs<NCAP>& npc, M& m, in
   const bool swap = h1 > h0;
   const int ks[2] = {swap ? h1 : h0, swap ? h0 : h1};
   const int vs[2] = {swap ? v1 : v0, swap ? v0 : v1};
+  const uint32_t cs[2] = {swap ? key1 : key0, swap ? key0 : key1};
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int k = ks[j];
-    if (k >= 0 && vs[j] <= 0 && npc.is_alive(k)) {
+    // dense NPCs: a hit slot is a live NPC's (the grid holds nothing else), so
+    // only a second hit on the same NPC is not (no HBM re-read of the alive row)
+    const bool live = NCAP == kDense ? !(j == 1 && ks[1] == ks[0]) : npc.is_alive(k);
+    if (k >= 0 && vs[j] <= 0 && live) {
       npc.mark_dead(k);
-      npc.kill(k);
+      if constexpr (NCAP == kDense) npc.kill_at(cs[j]);  // the cell is known: no slot lookup
+      else npc.kill(k);
       dl.npc_death += 1;
       ev.emit(ORX_EV_DEATH, 3 + k, 0, 0);
     }
@@ -1406,7 +1413,8 @@ __device__ __forceinline__ void tick_game(const Cfg& c, Key key, Src& src, uint3
     const int h0 = hA ? npc.find(pack_xy(A.tx, A.ty)) : -1;
     const int h1 = hB ? npc.find(pack_xy(Bp.tx, Bp.ty)) : -1;
     bool kA = false, kB = false;
-    npc_hits(c, npc, m, h0, h1, A.hd, Bp.hd, dl, ev, kA, kB);
+    npc_hits(c, npc, m, h0, h1, A.hd, Bp.hd, dl, ev, kA, kB, pack_xy(A.tx, A.ty),
+             pack_xy(Bp.tx, Bp.ty));
     if (c.ext & (ORX_EXT_LEVELING | ORX_EXT_ITEMS)) {  // readme.md:44
       if ((c.ext & ORX_EXT_LEVELING) && kA) gain_xp(c, A);
       if ((c.ext & ORX_EXT_LEVELING) && kB) gain_xp(c, Bp);
@@ -2065,14 +2073,14 @@ __device__ __forceinline__ void rollout_tick(const Cfg& c, const orx_state_t& st
           }
           bool ka = false, kb = false;
           npc_hits(c, npc, hp, sw ? h2 : h1, sw ? h1 : h2, sw ? d2 : d1, sw ? d1 : d2, dl, ev,
-                   ka, kb);
+                   ka, kb, sw ? k2 : k1, sw ? k1 : k2);
           kc1 = sw ? kb : ka;
           kc2 = sw ? ka : kb;
           if ((c.ext & ORX_EXT_ITEMS) && kc1) drop_item(c, key, game, ep, t0, h1, k1, npc, items);
           if ((c.ext & ORX_EXT_ITEMS) && kc2) drop_item(c, key, game, ep, t0, h2, k2, npc, items);
         } else {
           // two hits are then order-free: only the health left matters
-          npc_hits(c, npc, hp, h1, h2, d1, d2, dl, ev, kc1, kc2);
+          npc_hits(c, npc, hp, h1, h2, d1, d2, dl, ev, kc1, kc2, k1, k2);
         }
       }
       if (lean) {  // a meet: the two moves in the drawn order
