@@ -235,7 +235,8 @@ constexpr uint32_t kMaxLdsBlock = 160 * 1024;  // LDS per CU (one workgroup may 
 struct Deltas {  // counter / return increments, flushed once per launch
   int32_t combat, descend, dungeon, npc_death, ret, eps;
 #ifdef ORX_STAMPS
-  uint32_t n_rare = 0, n_ordered = 0, n_hits = 0, n_desc = 0, n_meet = 0;  // rare-block entries
+  uint32_t n_rare = 0, n_ordered = 0, n_hits = 0, n_desc = 0, n_meet = 0,  // rare-block entries
+           n_reset = 0;
 #endif
 };
 
@@ -772,10 +773,21 @@ __device__ __forceinline__ void setup_game(const Cfg& c, Key key, Src& src, Play
   const bool sep = c.start_mode == ORX_START_SEPARATED;
   p1.d = sep ? c.d1 : 0;
   p2.d = sep ? c.d2 : 0;
-  src.template dungeon<GRID>(c, p1.d, 0, p1.sx, p1.sy, p1.lay, err);
+  // keyed streams: a staircase straight from its stream's first block (the
+  // loop in dungeon_draw only when that block holds no accepted pair)
+  bool drawn1 = false, drawn2 = false;
+  if constexpr (!Src::kMt && !GRID) {
+    p1.lay = p2.lay = -1;
+    drawn1 = stair_from_block(c, philox(src.game, src.ep, (uint32_t)p1.d, tag(PUR_DUNGEON, 0),
+                                        key), p1.sx, p1.sy);
+    if (sep)
+      drawn2 = stair_from_block(c, philox(src.game, src.ep, (uint32_t)p2.d, tag(PUR_DUNGEON, 0),
+                                          key), p2.sx, p2.sy);
+  }
+  if (!drawn1) src.template dungeon<GRID>(c, p1.d, 0, p1.sx, p1.sy, p1.lay, err);
   src.remember(p1.d, p1.sx, p1.sy, p1.lay);
   if (sep) {
-    src.template dungeon<GRID>(c, p2.d, 0, p2.sx, p2.sy, p2.lay, err);
+    if (!drawn2) src.template dungeon<GRID>(c, p2.d, 0, p2.sx, p2.sy, p2.lay, err);
     src.remember(p2.d, p2.sx, p2.sy, p2.lay);
   } else {
     p2.sx = p1.sx; p2.sy = p1.sy; p2.lay = p1.lay;
@@ -786,7 +798,44 @@ __device__ __forceinline__ void setup_game(const Cfg& c, Key key, Src& src, Play
   int placed = 0;
   p1.x = p1.y = p2.x = p2.y = 0;
   const NpBound g1 = ground_bound<GRID>(c, p1.lay), g2 = ground_bound<GRID>(c, p2.lay);
-  for (uint32_t t = 0; t < kWordCap && placed < total; ++t) {
+  uint32_t t_start = 0;  // words the loop's cap counts as taken
+  if constexpr (!Src::kMt && !GRID) {
+    // both players from the INIT stream's first block, as selects over its
+    // four words (the loop below takes the same words one at a time); the
+    // stream is left after the last word taken, for the NPCs.  A block with
+    // fewer than two accepted, distinct cells (~1e-3 at 64x64) falls through
+    // to the loop from word 0.
+    if (g1.rng != 0u && g2.rng != 0u) {
+      const W4 w = philox(s.c0, s.c1, s.c2, s.c3, key);
+      int n = 0;
+      uint32_t used = 0;
+      int32_t x1 = 0, y1 = 0, x2 = 0, y2 = 0;
+#pragma unroll
+      for (uint32_t j = 0; j < 4; ++j) {
+        const uint32_t word = j == 0 ? w.a : j == 1 ? w.b : j == 2 ? w.c : w.d;
+        const bool is_p2 = n == 1;
+        const NpBound gb = is_p2 ? g2 : g1;
+        const uint32_t v = word & gb.mask;
+        int32_t x, y;
+        ground_cell<GRID>(c, v, -1, is_p2 ? p2.sx : p1.sx, is_p2 ? p2.sy : p1.sy, x, y);
+        const bool take = n < 2 && v <= gb.rng && !(is_p2 && !sep && x == x1 && y == y1);
+        x1 = (take && n == 0) ? x : x1;
+        y1 = (take && n == 0) ? y : y1;
+        x2 = (take && is_p2) ? x : x2;
+        y2 = (take && is_p2) ? y : y2;
+        used = take ? j + 1u : used;
+        n += take ? 1 : 0;
+      }
+      if (n == 2) {
+        p1.x = x1; p1.y = y1; p2.x = x2; p2.y = y2;
+        s.w = w;
+        s.idx = used;
+        t_start = used;
+        placed = 2;
+      }
+    }
+  }
+  for (uint32_t t = t_start; t < kWordCap && placed < total; ++t) {
     // placement 0: player 1, 1: player 2, 2+k: NPC k (all NPCs on p1's depth)
     const bool is_p2 = placed == 1;
     const NpBound gb = is_p2 ? g2 : g1;
@@ -1977,6 +2026,9 @@ __device__ __forceinline__ void rollout_tick(const Cfg& c, const orx_state_t& st
     const bool end = c.max_ticks && ft >= c.max_ticks;
     if (!in_progress) {
       if (c.autoreset) {  // the next episode (worldgen.py:77-87, 124-135)
+#ifdef ORX_STAMPS
+        ORX_COUNT(dl.n_reset);
+#endif
         ep += 1;
         setup_game<NCAP, GRID>(c, key, game, ep, p1, p2, npc, tick, status);
         items.clear();
@@ -2357,14 +2409,14 @@ __global__ void __launch_bounds__(kRolloutBlock) rollout_kernel(orx_cfg_t hc, or
 #endif
   ORX_STAMP(4);
 #ifdef ORX_STAMPS
-  uint32_t r[5] = {dl.n_rare, dl.n_ordered, dl.n_hits, dl.n_desc, dl.n_meet};
+  uint32_t r[6] = {dl.n_rare, dl.n_ordered, dl.n_hits, dl.n_desc, dl.n_meet, dl.n_reset};
 #pragma unroll
-  for (int j = 0; j < 5; ++j)
+  for (int j = 0; j < 6; ++j)
     for (int o = 32; o > 0; o >>= 1) r[j] += __shfl_xor(r[j], o);
   if ((threadIdx.x & 63) == 0) {
     const size_t w = (size_t)((blockIdx.x * blockDim.x + threadIdx.x) >> 6) * 16;
 #pragma unroll
-    for (int j = 0; j < 5; ++j) g_stamps[w + 5 + j] = r[j];
+    for (int j = 0; j < 6; ++j) g_stamps[w + 5 + j] = r[j];
   }
 #endif
 }

@@ -41,8 +41,16 @@ def child(arg, large, ticks=50):
     shapes = [(65536, ticks, 40, "c3", 1)] + ([(1 << 21, 20, 6, "c3", 1)] if large else [])
     if os.environ.get("AB_C5"):   # C5: 128x128 StaircaseBot at 16,384 and 131,072 games
         shapes += [(16384, 128, 20, "c5", 2), (131072, 128, 10, "c5", 2)]
+    if os.environ.get("AB_C5SEP"):   # the same with separation damage (sep_period 8)
+        shapes += [(16384, 128, 20, "c5sep", 2), (131072, 128, 10, "c5sep", 2)]
     for B, T, reps, cname, pol in shapes:
-        e = BatchedEngine(getattr(EnvConfig, cname)(), B, seed=1, device=dev)
+        if cname == "c5sep":
+            from optimax_rogue_amd.enums import EXT_SEPARATION_DAMAGE
+            cfg = EnvConfig.c5()
+            cfg.flags, cfg.sep_period = EXT_SEPARATION_DAMAGE, 8
+        else:
+            cfg = getattr(EnvConfig, cname)()
+        e = BatchedEngine(cfg, B, seed=1, device=dev)
         obs = torch.empty((T, len(OBS_FIELDS), B), dtype=torch.int32, device=dev) \
             if with_obs else None
         act = torch.empty((T, B, 2), dtype=torch.int8, device=dev) if with_obs else None

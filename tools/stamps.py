@@ -25,9 +25,13 @@ def main():
     _lib.LIB_PATH = lib
     from optimax_rogue_amd.engine import BatchedEngine
     dev = torch.device("cuda", 0)
-    cname = os.environ.get("STAMPS_CFG", "c3")   # c5: StaircaseBot on C5's dungeon
-    pol = 2 if cname == "c5" else 1
-    e = BatchedEngine(getattr(EnvConfig, cname)(), B, seed=1, device=dev)
+    cname = os.environ.get("STAMPS_CFG", "c3")   # c5 / c5sep: StaircaseBot on C5's dungeon
+    pol = 2 if cname.startswith("c5") else 1
+    cfg = EnvConfig.c5() if cname == "c5sep" else getattr(EnvConfig, cname)()
+    if cname == "c5sep":
+        from optimax_rogue_amd.enums import EXT_SEPARATION_DAMAGE
+        cfg.flags, cfg.sep_period = EXT_SEPARATION_DAMAGE, 8
+    e = BatchedEngine(cfg, B, seed=1, device=dev)
     obs = torch.empty((T, 14, B), dtype=torch.int32, device=dev)
     act = torch.empty((T, B, 2), dtype=torch.int8, device=dev)
     for _ in range(4):
@@ -38,7 +42,7 @@ def main():
     e.rollout(T, pol, pol, obs=obs, act=act)
     f.record()
     torch.cuda.synchronize()
-    W = B // 64
+    W = -(-B // e.rollout_lanes())    # one game per lane, rollout_lanes() games per wave
     buf = np.zeros(W * 16, dtype=np.uint64)
     dl = ctypes.CDLL(lib)
     dl.orx_diag_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int64]
@@ -47,7 +51,7 @@ def main():
     t0 = st[:, 0].min()
     st = st - t0
     # s_memtime counts the shader clock; report cycles and the event time
-    out = {"B": B, "ticks": T, "event_us": round(s.elapsed_time(f) * 1e3, 2)}
+    out = {"B": B, "ticks": T, "cfg": cname, "lanes": e.rollout_lanes(), "event_us": round(s.elapsed_time(f) * 1e3, 2)}
     names = ["entry", "loaded", "tick64", "loop_end", "drained"]
     for j, n in enumerate(names):
         v = st[:, j]
@@ -61,8 +65,8 @@ def main():
     out["loop_by_xcd_p50"] = [int(np.median(tot[xcd == x])) for x in range(8)]
     out["loop_by_xcd_max"] = [int(tot[xcd == x].max()) for x in range(8)]
     out["loop_pct"] = {q: int(np.percentile(tot, q)) for q in (1, 10, 50, 90, 99, 100)}
-    rare = buf.reshape(W, 16)[:, 5:10].astype(np.int64)
-    for j, n in enumerate(["rare_block", "ordered", "npc_hits", "descend", "meet"]):
+    rare = buf.reshape(W, 16)[:, 5:11].astype(np.int64)
+    for j, n in enumerate(["rare_block", "ordered", "npc_hits", "descend", "meet", "reset"]):
         out["ticks_with_" + n] = {"mean": float(rare[:, j].mean()), "max": int(rare[:, j].max())}
     slow = np.argsort(tot)[-10:]
     out["slowest10_rare"] = rare[slow].tolist()
