@@ -761,6 +761,16 @@ struct MtSrc {
   }
 };
 
+// An empty asm that "changes" its operands: values derived from them after
+// this point are recomputed rather than kept live from before it (and the
+// operands are computed before it, not sunk into a later branch).
+__device__ __forceinline__ void launder(int32_t& a, int32_t& b, int32_t& c, int32_t& d) {
+  asm volatile("" : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+}
+__device__ __forceinline__ void launder_w4(W4& w) {
+  asm volatile("" : "+v"(w.a), "+v"(w.b), "+v"(w.c), "+v"(w.d));
+}
+
 // ---------------------------------------------------------------------------
 // Game start (setup_game + NPC spawner), all placements in one rejection loop
 // over the INIT stream (one Philox call site, one division site).
@@ -776,10 +786,16 @@ __device__ __forceinline__ void setup_game(const Cfg& c, Key key, Src& src, Play
   // keyed streams: a staircase straight from its stream's first block (the
   // loop in dungeon_draw only when that block holds no accepted pair)
   bool drawn1 = false, drawn2 = false;
+  W4 wi = {0u, 0u, 0u, 0u};  // the INIT stream's first block (keyed streams)
   if constexpr (!Src::kMt && !GRID) {
+    // the dungeon's and the INIT stream's first blocks are independent: drawn
+    // side by side, one Philox dependency chain's latency covers both
     p1.lay = p2.lay = -1;
-    drawn1 = stair_from_block(c, philox(src.game, src.ep, (uint32_t)p1.d, tag(PUR_DUNGEON, 0),
-                                        key), p1.sx, p1.sy);
+    W4 wd = philox(src.game, src.ep, (uint32_t)p1.d, tag(PUR_DUNGEON, 0), key);
+    wi = philox(src.game, src.ep, 0u, tag(PUR_INIT, 0), key);
+    launder_w4(wd);
+    launder_w4(wi);
+    drawn1 = stair_from_block(c, wd, p1.sx, p1.sy);
     if (sep)
       drawn2 = stair_from_block(c, philox(src.game, src.ep, (uint32_t)p2.d, tag(PUR_DUNGEON, 0),
                                           key), p2.sx, p2.sy);
@@ -806,7 +822,7 @@ __device__ __forceinline__ void setup_game(const Cfg& c, Key key, Src& src, Play
     // fewer than two accepted, distinct cells (~1e-3 at 64x64) falls through
     // to the loop from word 0.
     if (g1.rng != 0u && g2.rng != 0u) {
-      const W4 w = philox(s.c0, s.c1, s.c2, s.c3, key);
+      const W4 w = wi;  // block 0 of s
       int n = 0;
       uint32_t used = 0;
       int32_t x1 = 0, y1 = 0, x2 = 0, y2 = 0;
@@ -908,6 +924,17 @@ __device__ __forceinline__ void descend(const Cfg& c, Key key, Src& src, Player&
     present = other.d == nd;
     gen = (!present && other_start <= nd && nd < other.d) ? 1u : 0u;
   }
+  // keyed streams: the new dungeon's first block and the SPAWN stream's are
+  // independent, so they are drawn side by side (one Philox chain's latency
+  // for both) even when the dungeon is the other player's
+  constexpr bool kFirst = !Src::kMt && !GRID && std::is_same<S, Stream>::value;
+  W4 wd = {0u, 0u, 0u, 0u}, ws = {0u, 0u, 0u, 0u};
+  if constexpr (kFirst) {
+    wd = philox(src.game, src.ep, (uint32_t)nd, tag(PUR_DUNGEON, gen), key);
+    ws = philox(spawn.c0, spawn.c1, spawn.c2, spawn.c3, key);
+    launder_w4(wd);
+    launder_w4(ws);
+  }
   int32_t sx, sy, lay;
   if (present && other.d == nd) {
     sx = other.sx; sy = other.sy; lay = other.lay;
@@ -918,8 +945,10 @@ __device__ __forceinline__ void descend(const Cfg& c, Key key, Src& src, Player&
     bool drawn = false;
     if constexpr (!Src::kMt && !GRID) {  // straight from the stream's first block
       lay = -1;
-      drawn = stair_from_block(c, philox(src.game, src.ep, (uint32_t)nd, tag(PUR_DUNGEON, gen),
-                                         key), sx, sy);
+      if constexpr (kFirst) drawn = stair_from_block(c, wd, sx, sy);
+      else
+        drawn = stair_from_block(c, philox(src.game, src.ep, (uint32_t)nd, tag(PUR_DUNGEON, gen),
+                                           key), sx, sy);
     }
     if (!drawn) src.template dungeon<GRID>(c, nd, gen, sx, sy, lay, err);
   }
@@ -936,7 +965,7 @@ __device__ __forceinline__ void descend(const Cfg& c, Key key, Src& src, Player&
     // the common spawn: the first word of a fresh SPAWN stream accepted and
     // the cell free; otherwise the loop below replays the stream from there
     if (spawn.idx == 0u && gb.rng != 0u) {
-      const W4 w = philox(spawn.c0, spawn.c1, spawn.c2, spawn.c3, key);
+      const W4 w = ws;  // block 0 of spawn
       const uint32_t v = w.a & gb.mask;
       if (v <= gb.rng) {
         ground_cell<GRID>(c, v, lay, sx, sy, x, y);
@@ -994,12 +1023,6 @@ __device__ __forceinline__ int32_t med3_i32(int32_t x, int32_t lo, int32_t hi) {
   int32_t r;
   asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(lo), "s"(hi));
   return r;
-}
-
-// An empty asm that "changes" its operands: values derived from them after
-// this point are recomputed rather than kept live from before it.
-__device__ __forceinline__ void launder(int32_t& a, int32_t& b, int32_t& c, int32_t& d) {
-  asm volatile("" : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
 }
 
 // v_ffbl_b32: index of the lowest set bit, 0xFFFFFFFF for 0 (an opaque asm
