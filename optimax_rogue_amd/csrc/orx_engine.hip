@@ -87,9 +87,17 @@ __device__ uint64_t g_stamps[65536 * 16];
 // active lane counts the entry; the lanes' counts are summed at the end
 #define ORX_COUNT(var)                                                                   \
   var += (__lane_id() == (uint32_t)__builtin_ctzll(__builtin_amdgcn_read_exec())) ? 1u : 0u
+// shader-clock cycles a wave spends in a rare-block branch (stamp slots 11..14),
+// accumulated by the branch's first active lane
+#define ORX_CYC_BEGIN(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#define ORX_CYC_END(var, v)                                                            \
+  var += (__lane_id() == (uint32_t)__builtin_ctzll(__builtin_amdgcn_read_exec()))     \
+             ? (uint32_t)(__builtin_amdgcn_s_memtime() - (v)) : 0u
 #else
 #define ORX_STAMP(j) ((void)0)
 #define ORX_COUNT(var) ((void)0)
+#define ORX_CYC_BEGIN(v) ((void)0)
+#define ORX_CYC_END(var, v) ((void)0)
 #endif
 #ifndef ORX_ROLLOUT_BLOCK
 #define ORX_ROLLOUT_BLOCK 256
@@ -237,6 +245,7 @@ struct Deltas {  // counter / return increments, flushed once per launch
 #ifdef ORX_STAMPS
   uint32_t n_rare = 0, n_ordered = 0, n_hits = 0, n_desc = 0, n_meet = 0,  // rare-block entries
            n_reset = 0;
+  uint32_t cy_rare = 0, cy_reset = 0, cy_ordered = 0, cy_desc = 0;  // cycles in them
 #endif
 };
 
@@ -2012,6 +2021,7 @@ __device__ __forceinline__ void rollout_tick(const Cfg& c, const orx_state_t& st
   if (ORX_UNLIKELY(rare)) {
 #ifdef ORX_STAMPS
     ORX_COUNT(dl.n_rare);
+    ORX_CYC_BEGIN(cy0);
 #endif
     launder(t1x, t1y, t2x, t2y);
     launder(p1.x, p1.y, p2.x, p2.y);
@@ -2051,6 +2061,7 @@ __device__ __forceinline__ void rollout_tick(const Cfg& c, const orx_state_t& st
       if (c.autoreset) {  // the next episode (worldgen.py:77-87, 124-135)
 #ifdef ORX_STAMPS
         ORX_COUNT(dl.n_reset);
+        ORX_CYC_BEGIN(cy1);
 #endif
         ep += 1;
         setup_game<NCAP, GRID>(c, key, game, ep, p1, p2, npc, tick, status);
@@ -2065,16 +2076,23 @@ __device__ __forceinline__ void rollout_tick(const Cfg& c, const orx_state_t& st
         }
         restarted = true;
         sep = -1;
+#ifdef ORX_STAMPS
+        ORX_CYC_END(dl.cy_reset, cy1);
+#endif
       }
     } else if (full) {  // the ordered tick
 #ifdef ORX_STAMPS
       ORX_COUNT(dl.n_ordered);
+      ORX_CYC_BEGIN(cy1);
 #endif
       bool err = false;
       const bool p1_first = first_from_packed(pk_shf, key, game, ep, t0, err);
       Events<false> ev{nullptr, 0};
       tick_game<NCAP, false, GRID>(c, key, game, ep, p1_first, p1, p2, npc, items, hp, tick,
                                    status, err, dl, ev, sep);
+#ifdef ORX_STAMPS
+      ORX_CYC_END(dl.cy_ordered, cy1);
+#endif
     } else {
       // the common path's rules, then the one-sided events: a player that
       // hits an NPC, descends or meets the other does not move freely
@@ -2091,6 +2109,7 @@ __device__ __forceinline__ void rollout_tick(const Cfg& c, const orx_state_t& st
       if (!lean & (st1 | st2)) {  // one player descends
 #ifdef ORX_STAMPS
         ORX_COUNT(dl.n_desc);
+        ORX_CYC_BEGIN(cy1);
 #endif
         PhiloxSrc src{key, game, ep};
         auto spawn = src.spawn(t0);
@@ -2124,6 +2143,9 @@ __device__ __forceinline__ void rollout_tick(const Cfg& c, const orx_state_t& st
           status = ORX_STATUS_RNG_EXHAUSTED;
         }
         if (clash) deaths_over(p1, p2, end, status, dl);
+#ifdef ORX_STAMPS
+        ORX_CYC_END(dl.cy_desc, cy1);
+#endif
       }
       bool kc1 = false, kc2 = false;  // ORX_EXT_LEVELING: each player's kill this tick
       if (NCAP > 0 && (hit1 | hit2)) {  // NPCs are swept after both moves
@@ -2207,6 +2229,9 @@ __device__ __forceinline__ void rollout_tick(const Cfg& c, const orx_state_t& st
         if (!st2 & (p2.d == c.d1) & ((p2.x != x2o) | (p2.y != y2o))) pick_up(c, p2, npc, items);
       }
     }
+#ifdef ORX_STAMPS
+    ORX_CYC_END(dl.cy_rare, cy0);
+#endif
   }
   // the common tick: both players move to their effective targets
   p1.x = rare ? p1.x : t1x;
@@ -2432,14 +2457,15 @@ __global__ void __launch_bounds__(kRolloutBlock) rollout_kernel(orx_cfg_t hc, or
 #endif
   ORX_STAMP(4);
 #ifdef ORX_STAMPS
-  uint32_t r[6] = {dl.n_rare, dl.n_ordered, dl.n_hits, dl.n_desc, dl.n_meet, dl.n_reset};
+  uint32_t r[10] = {dl.n_rare, dl.n_ordered, dl.n_hits, dl.n_desc, dl.n_meet, dl.n_reset,
+                    dl.cy_rare, dl.cy_reset, dl.cy_ordered, dl.cy_desc};
 #pragma unroll
-  for (int j = 0; j < 6; ++j)
+  for (int j = 0; j < 10; ++j)
     for (int o = 32; o > 0; o >>= 1) r[j] += __shfl_xor(r[j], o);
   if ((threadIdx.x & 63) == 0) {
     const size_t w = (size_t)((blockIdx.x * blockDim.x + threadIdx.x) >> 6) * 16;
 #pragma unroll
-    for (int j = 0; j < 6; ++j) g_stamps[w + 5 + j] = r[j];
+    for (int j = 0; j < 10; ++j) g_stamps[w + 5 + j] = r[j];
   }
 #endif
 }

@@ -1,7 +1,9 @@
 """In-kernel timeline of one rollout launch (diagnostics; needs a build with
 -DORX_STAMPS): lane 0 of each wave records s_memtime at kernel entry (0),
 after the state loads landed (1), at tick 64 (2), after the tick loop (3) and
-after the epilogue's stores drained (4).
+after the epilogue's stores drained (4); per wave, the rare-block entries by
+kind and the cycles spent in the rare block, its reset, ordered-tick and
+descend branches.
 
     python tools/stamps.py tools/ab_libs/stamps.so [B] [ticks]
 """
@@ -65,9 +67,13 @@ def main():
     out["loop_by_xcd_p50"] = [int(np.median(tot[xcd == x])) for x in range(8)]
     out["loop_by_xcd_max"] = [int(tot[xcd == x].max()) for x in range(8)]
     out["loop_pct"] = {q: int(np.percentile(tot, q)) for q in (1, 10, 50, 90, 99, 100)}
-    rare = buf.reshape(W, 16)[:, 5:11].astype(np.int64)
+    rare = buf.reshape(W, 16)[:, 5:15].astype(np.int64)
     for j, n in enumerate(["rare_block", "ordered", "npc_hits", "descend", "meet", "reset"]):
         out["ticks_with_" + n] = {"mean": float(rare[:, j].mean()), "max": int(rare[:, j].max())}
+    # shader-clock cycles per wave inside the rare block and three of its branches
+    for j, n in enumerate(["rare_block", "reset", "ordered", "descend"]):
+        v = rare[:, 6 + j]
+        out["cycles_in_" + n] = {"p50": int(np.median(v)), "mean": float(v.mean())}
     slow = np.argsort(tot)[-10:]
     out["slowest10_rare"] = rare[slow].tolist()
     out["slowest10_loop"] = tot[slow].tolist()
