@@ -169,6 +169,8 @@ class BatchedEngine:
 
         ``episode`` (int or tensor) sets the episode index first; by default
         a full reset starts every game at episode 0."""
+        if mask is not None and mask.numel() != self.B:
+            raise ValueError("mask must have n_games elements")
         if mask is None and episode is None:
             episode = 0
         if episode is not None:
@@ -181,8 +183,6 @@ class BatchedEngine:
         m8 = None
         if mask is not None:
             m8 = mask.to(device=self.device, dtype=torch.uint8).contiguous()
-            if m8.numel() != self.B:
-                raise ValueError("mask must have n_games elements")
         self._call("orx_reset", _ptr(m8), self.B, self.seed, self.game_offset, self._stream())
 
     def step(self, actions: Optional[torch.Tensor] = None, events: bool = False):
@@ -190,12 +190,11 @@ class BatchedEngine:
         values.  Returns the status tensor (UpdateResult codes, asynchronous);
         with ``events=True`` returns ``(status, events, n_events)``: the tick's
         update-event records int32 [n_games, MAX_EVENTS, 4] and their counts
-        (include/orx.h ORX_EV_*), in the reference's GameStateUpdate order."""
+        (include/orx.h ORX_EV_*), in the reference's GameStateUpdate order;
+        both buffers belong to the engine and are overwritten by the next
+        ``step(events=True)``."""
         a = self.actions if actions is None else actions
-        if a.dtype != torch.int8 or a.shape != (self.B, 2) or not a.is_contiguous() \
-                or a.device != self.device:
-            raise ValueError("actions must be a contiguous int8 [n_games, 2] tensor on "
-                             f"{self.device}")
+        self._check_actions(a, "actions")
         if not events:
             self._call("orx_step", _ptr(a), self.B, self.seed, self.game_offset, self._stream())
             return self.status
@@ -210,6 +209,7 @@ class BatchedEngine:
                out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """RandomBot / StaircaseBot moves for both players into ``out``."""
         a = self.actions if out is None else out
+        self._check_actions(a, "out")
         self._call("orx_policy", int(p1), int(p2), _ptr(a), self.B, self.seed, self.game_offset,
                    self._stream())
         return a
@@ -222,6 +222,14 @@ class BatchedEngine:
         self._check_traj(n_ticks, obs, act)
         self._call("orx_rollout", int(p1), int(p2), int(n_ticks), _ptr(obs), _ptr(act), self.B,
                    self.seed, self.game_offset, self._stream())
+
+    def _check_actions(self, a: torch.Tensor, what: str) -> None:
+        # the kernels index [n_games, 2] blindly: a wrong buffer would be an
+        # out-of-bounds device access, so it is refused here
+        if a.dtype != torch.int8 or tuple(a.shape) != (self.B, 2) or not a.is_contiguous() \
+                or a.device != self.device:
+            raise ValueError(f"{what} must be a contiguous int8 [n_games, 2] tensor on "
+                             f"{self.device}")
 
     def _check_traj(self, n_ticks, obs, act):
         for t, dt, n, what in ((obs, torch.int32, n_ticks * len(OBS_FIELDS) * self.B,
@@ -261,8 +269,37 @@ class BatchedEngine:
             out[f] = a
         return out
 
+    def _check_snapshot(self, snap: dict) -> None:
+        """Refuses host state the kernels would index out of bounds with:
+        players or NPCs off the grid, layout indices outside the bank."""
+        W, H = int(self.cfg.width), int(self.cfg.height)
+
+        def within(name, lo, hi, sel=None):
+            if name not in snap:
+                return
+            a = np.asarray(snap[name]).astype(np.int64)
+            if sel is not None:
+                a = a[sel]
+            if a.size and (a.min() < lo or a.max() >= hi):
+                raise ValueError(f"snapshot {name} outside [{lo}, {hi})")
+        within("p_x", 0, W)
+        within("p_y", 0, H)
+        within("p_depth", 0, 1 << 30)
+        if self.bank is not None:
+            within("p_layout", 0, len(self.bank))
+        if self.K and "npc_pos" in snap:
+            from .enums import npc_alive_bits
+            pos = np.asarray(snap["npc_pos"]).astype(np.uint16).astype(np.int64)[: self.K]
+            alive = snap.get("npc_alive")
+            live = (npc_alive_bits(np.asarray(alive).astype(np.uint32), self.K)
+                    if alive is not None else np.ones_like(pos, bool))
+            if ((pos & 0xFF)[live] >= W).any() or ((pos >> 8)[live] >= H).any():
+                raise ValueError("snapshot npc_pos: a live NPC outside the grid")
+
     def load_snapshot(self, snap: dict) -> None:
-        """Writes host arrays (engine layout) into the device state."""
+        """Writes host arrays (engine layout) into the device state (checked
+        first: positions and layout indices the kernels would index with)."""
+        self._check_snapshot(snap)
         if self.bank is not None and "p_layout" in snap:
             self.p_layout.copy_(torch.from_numpy(np.ascontiguousarray(snap["p_layout"], np.int16)))
         if self.sep_start is not None and "sep_start" in snap:

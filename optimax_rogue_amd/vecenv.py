@@ -72,6 +72,8 @@ class VecEnv:
         (observation, reward, done, status)."""
         e = self.engine
         a = actions.to(device=self.device, dtype=torch.int8)
+        if tuple(a.shape) not in ((self.B,), (self.B, 2)):   # no silent broadcasting
+            raise ValueError(f"actions must be [n_games] or [n_games, 2], got {tuple(a.shape)}")
         if a.dim() == 1:
             if self.opponent is None:
                 raise ValueError("self-play (opponent=None) takes [n_games, 2] actions")

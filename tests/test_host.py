@@ -52,3 +52,38 @@ def test_dungeon_bank_random_is_valid():
         assert (lay == 3).sum() == 2                  # two staircases
         assert (lay[[0, -1], :] == 2).all() and (lay[:, [0, -1]] == 2).all()
     assert bank.min_ground >= 2
+
+
+def _bare_engine(cfg, B):
+    """A BatchedEngine shell with no device state: enough for its host checks."""
+    import torch
+    from optimax_rogue_amd.engine import BatchedEngine
+    e = BatchedEngine.__new__(BatchedEngine)
+    e.cfg, e.B, e.K, e.bank, e.device = cfg, B, int(cfg.n_npcs), None, torch.device("cpu")
+    return e
+
+
+def test_engine_refuses_action_buffers_it_would_overrun():
+    import torch
+    from optimax_rogue_amd import EnvConfig
+    e = _bare_engine(EnvConfig.c2(), 8)
+    e._check_actions(torch.zeros((8, 2), dtype=torch.int8), "actions")
+    for bad in (torch.zeros((4, 2), dtype=torch.int8), torch.zeros((8, 2), dtype=torch.int32),
+                torch.zeros((2, 8), dtype=torch.int8).t(), torch.zeros(16, dtype=torch.int8)):
+        with pytest.raises(ValueError):
+            e._check_actions(bad, "actions")
+
+
+def test_engine_refuses_snapshots_off_the_grid():
+    from optimax_rogue_amd import EnvConfig
+    cfg = EnvConfig(width=8, height=6, n_npcs=2)
+    e = _bare_engine(cfg, 3)
+    ok = {"p_x": np.full((2, 3), 7), "p_y": np.full((2, 3), 5), "p_depth": np.zeros((2, 3)),
+          "npc_pos": np.array([[7 | 5 << 8] * 3, [0] * 3]), "npc_alive": np.full(3, 3)}
+    e._check_snapshot(ok)
+    for key, val in (("p_x", np.full((2, 3), 8)), ("p_y", np.full((2, 3), -1)),
+                     ("npc_pos", np.array([[8] * 3, [0] * 3]))):
+        with pytest.raises(ValueError):
+            e._check_snapshot(dict(ok, **{key: val}))
+    # a dead NPC's slot is not read: any position passes
+    e._check_snapshot(dict(ok, npc_pos=np.array([[200] * 3, [0] * 3]), npc_alive=np.full(3, 2)))
