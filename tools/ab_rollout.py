@@ -41,6 +41,8 @@ def child(arg, large, ticks=50):
     shapes = [(65536, ticks, 40, "c3", 1)] + ([(1 << 21, 20, 6, "c3", 1)] if large else [])
     if os.environ.get("AB_C5"):   # C5: 128x128 StaircaseBot at 16,384 and 131,072 games
         shapes += [(16384, 128, 20, "c5", 2), (131072, 128, 10, "c5", 2)]
+    if os.environ.get("AB_SMALL"):   # batches below 64 games per wave: C2, a C3 stream shard
+        shapes += [(4096, 128, 40, "c2", 1), (32768, 128, 20, "c3", 1), (16384, 128, 20, "c3", 1)]
     if os.environ.get("AB_C5SEP"):   # the same with separation damage (sep_period 8)
         shapes += [(16384, 128, 20, "c5sep", 2), (131072, 128, 10, "c5sep", 2)]
     for B, T, reps, cname, pol in shapes:
