@@ -1,7 +1,8 @@
-"""GPU: the sharded HIP path.  Two torchrun ranks on cuda:0 (gloo), each
+"""GPU: the sharded HIP path.  Two (and four) torchrun ranks on cuda:0 (gloo), each
 stepping its parallel.shard() of the global batch with BatchedEngine at its
 game_offset, all-gathered with parallel.gather_returns, equal a single
-BatchedEngine over the whole batch -- for an even and an odd global batch.
+BatchedEngine over the whole batch -- for even and odd global batches
+(bit-identical for any rank count).
 (The 8-GPU RCCL run is the driver's; this covers the same code path on one
 card.)"""
 import json
@@ -28,15 +29,15 @@ def _port():
     return p
 
 
-@pytest.mark.parametrize("global_batch", [6000, 6001])
-def test_two_ranks_equal_one_process(tmp_path, global_batch):
+@pytest.mark.parametrize("ranks,global_batch", [(2, 6000), (2, 6001), (4, 4097)])
+def test_ranks_equal_one_process(tmp_path, ranks, global_batch):
     import torch
     from dist_worker import rows_of
     from optimax_rogue_amd import EnvConfig
     from optimax_rogue_amd.engine import BatchedEngine
     out = str(tmp_path / "gathered.npy")
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="1")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ranks}",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()),
            os.path.join(HERE, "dist_worker.py"), "--global-batch", str(global_batch),
            "--ticks", str(TICKS), "--cfg", json.dumps(CFG), "--policy", "1,2", "--out", out]
