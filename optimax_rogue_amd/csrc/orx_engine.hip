@@ -71,7 +71,9 @@ constexpr int32_t kStartTick = 1;     // GameState.tick of a fresh game (worldge
 constexpr uint32_t kDeadSlot = 0xFFFFu;
 
 // Diagnostic builds only (-DORX_DIAG=bits; results are wrong): rollout_kernel
-// 16 writes no trajectory.  Used by tools/ab_rollout.py to attribute time.
+// 16 writes no trajectory; 32 runs no tick (the trajectory stores alone: the
+// store ceiling of the launch's own output pattern).  Used by
+// tools/ab_rollout.py and tools/ab_bench_step.py to attribute time.
 #ifndef ORX_DIAG
 #define ORX_DIAG 0
 #endif
@@ -2435,8 +2437,9 @@ __global__ void __launch_bounds__(kRolloutBlock) rollout_kernel(orx_cfg_t hc, or
     if (t == 64) { ORX_STAMP(2); }
 #endif
     int32_t a1 = ORX_MOVE_STAY, a2 = ORX_MOVE_STAY;
-    rollout_tick<NCAP, GRID>(c, st, B, i, key, game, ep, pol1, pol2, p1, p2, npc, items, hp,
-                             tick, status, dl, sep, restarted, a1, a2);
+    if (!(ORX_DIAG & 32))
+      rollout_tick<NCAP, GRID>(c, st, B, i, key, game, ep, pol1, pol2, p1, p2, npc, items, hp,
+                               tick, status, dl, sep, restarted, a1, a2);
     if (!(ORX_DIAG & 16)) traj.write(t, p1, p2, tick, status, a1, a2);
   } while (++t < n_ticks);
   ORX_STAMP(3);
