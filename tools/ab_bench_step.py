@@ -4,7 +4,10 @@ library path given, a fresh child process times the headline step -- C3,
 obs+act -- over `steps` steps after `warmup`, like bench.py (HIP events, the
 shards joined on the caller's stream).  Libraries alternate, `reps` rounds.
 
-    python tools/ab_bench_step.py old.so new.so [--reps=3] [--steps=20]
+    python tools/ab_bench_step.py old.so new.so[@VAR=value...] [--reps=3] [--steps=20]
+
+(``@STREAMS=n`` sets the shard count; other ``@VAR=value`` set environment
+variables, e.g. ``@ORX_PC=1``.)
 """
 import json
 import os
@@ -14,14 +17,23 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def child(lib, steps, warmup=5, T=128, B=65536):
+def child(arg, steps, warmup=5, T=128, B=65536):
+    lib, *envs = arg.split("@")   # path@VAR=value: run that library with VAR set
+    streams = 2
+    for env in envs:
+        k, _, v = env.partition("=")
+        if k == "STREAMS":
+            streams = int(v)
+        else:
+            os.environ[k] = v
     sys.path.insert(0, ROOT)
     import torch
     from optimax_rogue_amd import _lib, EnvConfig
     _lib.LIB_PATH = os.path.abspath(lib)
     from optimax_rogue_amd.engine import StreamShardedEngine
     dev = torch.device("cuda", 0)
-    eng = StreamShardedEngine(EnvConfig.c3(), B, seed=0, device=dev, n_streams=2)
+    eng = StreamShardedEngine(EnvConfig.c3(), B, seed=0, device=dev,
+                              n_streams=streams)
     obs, act = eng.trajectory_buffers(T)
     go = eng.rollout_launcher(T, 1, 1, obs=obs, act=act)
     eng.fork()
@@ -38,7 +50,7 @@ def child(lib, steps, warmup=5, T=128, B=65536):
     b.record()
     torch.cuda.synchronize()
     us = a.elapsed_time(b) * 1e3 / steps
-    print(json.dumps({"lib": lib, "us_per_step": round(us, 2),
+    print(json.dumps({"lib": arg, "us_per_step": round(us, 2),
                       "env_steps_per_s": B * T / us * 1e6}), flush=True)
 
 
