@@ -311,6 +311,26 @@ struct Npcs {
     const int sh = (k & 1) * 16;
     wr(k >> 1, (rd(k >> 1) & ~(0xFFFFu << sh)) | ((v & 0xFFFFu) << sh));
   }
+  // The game setup fills slots 0, 1, ... in order with a per-lane count: a
+  // runtime slot index would lower to a branch ladder, so each placement is
+  // shifted in at the top of the slot chain (v_alignbit per register, kept
+  // where `take` is false) and align(n) moves the n placed slots down to 0.
+  __device__ __forceinline__ void push_top(uint32_t v, bool take) {
+    if constexpr (NCAP > 0) {
+#pragma unroll
+      for (int r = 0; r < kRegs; ++r) {  // ascending: q[r + 1] is still the old one
+        const uint32_t hi = r + 1 < kRegs ? rd(r + 1) : v;
+        const uint32_t n = __builtin_amdgcn_alignbit(hi, rd(r), 16);
+        wr(r, take ? n : rd(r));
+      }
+    }
+  }
+  __device__ __forceinline__ void align(int n) {
+    if (n < NCAP) {
+#pragma unroll
+      for (int k = 0; k < NCAP; ++k) push_top(0xFFFFu, k < NCAP - n);
+    }
+  }
   // True iff some slot holds `key`: zero-halfword test on (slots ^ key),
   // (v - 0x00010001) & ~v & 0x80008000 is nonzero iff a 16-bit half is zero.
   __device__ __forceinline__ bool any(uint32_t key) const {
@@ -879,17 +899,22 @@ __device__ __forceinline__ void setup_game(const Cfg& c, Key key, Src& src, Play
     if (placed >= 1) occ = x == p1.x && y == p1.y && (placed >= 2 || !sep);
     if (placed >= 2) {
       occ = occ || (p2.d == p1.d && x == p2.x && y == p2.y);
-      occ = occ || npc.find(pack_xy(x, y)) >= 0;
+      if constexpr (NCAP == kDense) occ = occ || npc.find(pack_xy(x, y)) >= 0;
+      else occ = occ || npc.any(pack_xy(x, y));
     }
     if (occ) continue;
     if (placed == 0) { p1.x = x; p1.y = y; }
     else if (placed == 1) { p2.x = x; p2.y = y; }
-    else if constexpr (NCAP > 0) {
+    else if constexpr (NCAP == kDense) {
       npc.set(placed - 2, pack_xy(x, y));
+      npc.mark_alive(placed - 2);
+    } else if constexpr (NCAP > 0) {
+      npc.push_top(pack_xy(x, y), true);
       npc.mark_alive(placed - 2);
     }
     ++placed;
   }
+  if constexpr (NCAP > 0 && NCAP != kDense) npc.align(placed - 2);
   if (placed < total) err = true;
   p1.hp = c.player_hp;
   p2.hp = c.player_hp;

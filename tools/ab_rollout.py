@@ -43,6 +43,8 @@ def child(arg, large, ticks=50):
         shapes += [(16384, 128, 20, "c5", 2), (131072, 128, 10, "c5", 2)]
     if os.environ.get("AB_SMALL"):   # batches below 64 games per wave: C2, a C3 stream shard
         shapes += [(4096, 128, 40, "c2", 1), (32768, 128, 20, "c3", 1), (16384, 128, 20, "c3", 1)]
+    if os.environ.get("AB_RESETS"):  # C3 with 20-tick episodes: a reset every 20 ticks
+        shapes += [(65536, 128, 20, "c3resets", 1)]
     if os.environ.get("AB_C5SEP"):   # the same with separation damage (sep_period 8)
         shapes += [(16384, 128, 20, "c5sep", 2), (131072, 128, 10, "c5sep", 2)]
     for B, T, reps, cname, pol in shapes:
@@ -50,6 +52,9 @@ def child(arg, large, ticks=50):
             from optimax_rogue_amd.enums import EXT_SEPARATION_DAMAGE
             cfg = EnvConfig.c5()
             cfg.flags, cfg.sep_period = EXT_SEPARATION_DAMAGE, 8
+        elif cname == "c3resets":
+            cfg = EnvConfig.c3()
+            cfg.max_ticks = 20
         else:
             cfg = getattr(EnvConfig, cname)()
         e = BatchedEngine(cfg, B, seed=1, device=dev)
