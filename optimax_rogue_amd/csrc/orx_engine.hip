@@ -2071,7 +2071,13 @@ __device__ __forceinline__ void rollout_tick(const Cfg& c, const orx_state_t& st
     // step) takes the ordered tick
     const bool rpg_ordered = ((c.ext & ORX_EXT_CHARACTER) && desc_meet) ||
                              ((c.ext & ORX_EXT_README_COMBAT) && meet);
-    const bool full0 = (meet & (st1 | st2)) | (st1 & st2) | ext_ordered | rpg_ordered;
+    // an NPC standing on a staircase (left there when an Unused-despawned
+    // depth is regenerated with its staircase elsewhere) is attacked, not
+    // descended through: handle_move tests pos_lookup before the tile
+    // (updater.py:199-207), which the ordered tick follows literally
+    const bool npc_stair = (hit1 & st1) | (hit2 & st2);
+    const bool full0 =
+        (meet & (st1 | st2)) | (st1 & st2) | ext_ordered | rpg_ordered | npc_stair;
     // the games that use the initiative order: the ordered tick, a meet, a
     // descend into the other's depth
     const bool ordered_use = in_progress & (full0 | meet | desc_meet);

@@ -560,6 +560,13 @@ CASES = {
     "separated_unused": dict(cfg=dict(width=7, height=6, max_ticks=120, start_mode=2, despawn=2,
                                       p1_depth=2, p2_depth=0, policy=(1, 2)), seed=8, games=12,
                              ticks=260),
+    # Unused despawn, Separated start: player 1 leaves the NPCs' depth, which
+    # is despawned; player 2 descends into its regeneration, whose staircase
+    # can lie under an NPC -- handle_move attacks it (pos_lookup before the
+    # tile, updater.py:199-207); 21 such attacks in these games
+    "npc_stair_unused_sep": dict(cfg=dict(width=6, height=6, max_ticks=200, start_mode=2,
+                                          despawn=2, p1_depth=1, p2_depth=0, n_npcs=10,
+                                          policy=(2, 2)), seed=15, games=16, ticks=300),
     # C3 shape: 64x64, K=8 NPCs, random
     "c3_npc_64": dict(cfg=dict(width=64, height=64, n_npcs=8), seed=3, games=6, ticks=300),
     # C3 at full episode length: 64x64, K=8, max_ticks 1000, past the first

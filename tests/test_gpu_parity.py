@@ -135,6 +135,13 @@ ORACLE_CASES = {
     # rollout's descend-into-the-other's-depth path in both drawn orders
     "desc_meet_5x4": (dict(width=5, height=4, start_mode=2, p1_depth=2, p2_depth=1,
                            max_ticks=200), (1, 2), 2048, 200, 25),
+    # Unused despawn with a separated start: player 1 leaves the NPCs' depth,
+    # it is despawned, and player 2 descends into its regeneration, whose
+    # staircase may lie under an NPC (attacked, not descended through)
+    "npc_stair_unused_sep": (dict(width=6, height=6, start_mode=2, p1_depth=1, p2_depth=0,
+                                  n_npcs=10, despawn=2, max_ticks=300), (2, 2), 4096, 400, 48),
+    "npc_stair_unused_bank": (dict(width=8, height=7, start_mode=2, p1_depth=1, p2_depth=0,
+                                   n_npcs=9, despawn=2, max_ticks=300), (2, 2), 4096, 400, 49),
     # dense NPCs (K > 16): the occupancy-grid form, from crowded to packed
     "npc_dense_40_16x16": (dict(width=16, height=16, n_npcs=40, npc_health=2, max_ticks=150),
                            (1, 2), 2048, 300, 40),
@@ -168,7 +175,8 @@ ORACLE_CASES = {
 ORACLE_BANKS = {"bank_64_npc": (64, 64, 16, 21, (1,)), "bank_stairs_unused": (12, 10, 5, 22, (1, 3)),
                 "npc_dense_bank": (12, 10, 6, 46, (1, 2)),
                 "bank_big_global": (36, 36, 64, 27, (1, 2)),
-                "stock_bank_separated": (12, 10, 7, 24, (1, 2))}
+                "stock_bank_separated": (12, 10, 7, 24, (1, 2)),
+                "npc_stair_unused_bank": (8, 7, 6, 50, (1, 2))}
 
 
 @pytest.mark.parametrize("name", sorted(ORACLE_CASES))
