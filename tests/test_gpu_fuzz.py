@@ -17,12 +17,16 @@ stays inside the reference's semantics (flags 0); engine-vs-oracle only
 ("parity unpinned") where a build extension is on.  The generator is seeded,
 so a failure names a reproducible case id.
 """
+import os
+
 import numpy as np
 import pytest
 
 from golden_util import compare_state
 
-N_CASES = 96
+# ORX_FUZZ_CASES / ORX_FUZZ_BASE widen or move the sweep for ad-hoc runs
+N_CASES = int(os.environ.get("ORX_FUZZ_CASES", "96"))
+BASE = int(os.environ.get("ORX_FUZZ_BASE", "1000"))
 MANA, HEAL, LEVEL, ITEMS, README = 4, 8, 16, 32, 64
 
 
@@ -49,7 +53,7 @@ def _layouts(rs, W, H):
 
 def _draw(case: int):
     """Configuration, layouts, batch, ticks, seed, offset, bots, lanes of case."""
-    rs = np.random.RandomState(1000 + case)
+    rs = np.random.RandomState(BASE + case)
     W, H = int(rs.randint(4, 40)), int(rs.randint(4, 40))
     if rs.rand() < 0.15:
         W, H = int(rs.choice([64, 96, 128])), int(rs.choice([64, 128]))
@@ -75,9 +79,9 @@ def _draw(case: int):
     elif kind < 0.75:
         K = int(rs.randint(1, 17))
     else:
-        K = int(rs.randint(17, 64))
+        K = int(rs.randint(17, 64 if rs.rand() < 0.8 else 256))
     K = min(K, max(0, room))
-    cfg.update(n_npcs=K, npc_health=int(rs.randint(1, 5)), npc_damage=int(rs.randint(0, 3)),
+    cfg.update(n_npcs=K, npc_health=int(rs.choice([1, 2, 3, 4, 127])), npc_damage=int(rs.randint(0, 3)),
                npc_armor=int(rs.randint(0, 2)))
     flags = 0
     if rs.rand() < 0.5:
@@ -97,7 +101,7 @@ def _draw(case: int):
         cfg["rng"] = 1
     B = int(rs.choice([1, 63, 257, 1000, 1531]))
     T = int(rs.randint(40, 161))
-    pol = (int(rs.randint(1, 3)), int(rs.randint(1, 3)))
+    pol = (int(rs.choice([1, 1, 2, 2, 3])), int(rs.choice([1, 1, 2, 2, 3])))
     lanes = int(rs.choice([0, 0, 64, 32, 16, 8]))
     return cfg, layouts, B, T, int(rs.randint(0, 2 ** 31)), int(rs.randint(0, 5000)), pol, lanes
 
@@ -152,14 +156,21 @@ def test_random_config_vs_oracle(case, oracle_lib, monkeypatch):
         compare_state(e.snapshot(), o.export(), o.K, f"{where} reset")
         return o, e
 
-    # per tick, random actions through orx_step
+    # per tick, random actions through orx_step_events: state, and the update
+    # events of a few games every tick
     ora, eng = pair()
+    ora = oracle_lib.Oracle(cfg, B, seed, off, layouts=layouts, record_events=True)
+    ora.reset(episode=np.zeros(B, np.int32))
     rs = np.random.RandomState(seed % 100003)
     hi = 7 if cfg["flags"] & HEAL else 6
     for t in range(T):
         a = rs.randint(1, hi, size=(B, 2)).astype(np.int8)
         ora.step(a)
-        eng.step(torch.from_numpy(a).to(dev).contiguous())
+        _, ev, nev = eng.step(torch.from_numpy(a).to(dev).contiguous(), events=True)
+        ev, nev = ev.cpu().numpy(), nev.cpu().numpy()
+        for g in rs.randint(0, B, size=3):
+            got = [tuple(int(v) for v in r) for r in ev[g, : nev[g]]]
+            assert got == ora.events(int(g)), f"{where} events t={t + 1} game {g}"
         if t % 40 == 39 or t == T - 1:
             compare_state(eng.snapshot(), ora.export(), ora.K, f"{where} step t={t + 1}")
 
