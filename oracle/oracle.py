@@ -191,6 +191,7 @@ class Oracle:
         return [tuple(int(v) for v in r) for r in buf[:n]]
 
     def entities(self, g: int):
-        buf = np.zeros((64, 7), np.int32)
-        n = lib().oracle_entities(self._h, g, _ptr(buf), 64)
+        cap = 2 + 255 + 1   # both players and up to 255 NPCs (ORX_MAX_NPCS)
+        buf = np.zeros((cap, 7), np.int32)
+        n = lib().oracle_entities(self._h, g, _ptr(buf), cap)
         return [tuple(int(v) for v in r) for r in buf[:n]]

@@ -495,7 +495,10 @@ class Harness:
                 hp[k] = e.health
         rec["npc_pos"] = pos
         rec["npc_health"] = hp
-        rec["npc_alive"] = alive
+        # one 32-bit word per game up to 32 NPCs (the committed fixtures), rows
+        # of 32 alive bits beyond (the engine's dense layout, [words][games])
+        rec["npc_alive"] = alive if K <= 32 else [(alive >> (32 * w)) & 0xFFFFFFFF
+                                                  for w in range((K + 31) // 32)]
         if self.layouts is None:
             rec["world"] = [(d, *gs.world.dungeons[d].staircase()) for d in gs.world.dungeons]
         else:
