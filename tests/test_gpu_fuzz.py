@@ -195,3 +195,64 @@ def test_random_config_vs_oracle(case, oracle_lib, monkeypatch):
         assert np.array_equal(act.cpu().numpy(), np.stack(want_act)), f"{where} actions {c}"
         assert np.array_equal(obs.cpu().numpy(), np.stack(want_obs)), f"{where} obs {c}"
     torch.cuda.synchronize()
+
+
+N_SEQ = int(os.environ.get("ORX_FUZZ_SEQ", "32"))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", range(N_SEQ))
+def test_random_call_sequence_vs_oracle(case, oracle_lib, monkeypatch, tmp_path):
+    """State hand-over between the entry points: a seeded random sequence of
+    orx_step (given actions), orx_policy + orx_step, orx_rollout of 1-40 ticks,
+    masked orx_reset into a chosen episode and checkpoint/resume (save ->
+    load into a new engine) on one random configuration, against the oracle
+    doing the same, compared after every call."""
+    import torch
+    from optimax_rogue_amd import EnvConfig
+    from optimax_rogue_amd.engine import BatchedEngine
+    cfg, layouts, B, T, seed, off, pol, lanes = _draw(7919 + case)
+    where = f"seq {case} {cfg} B={B} lanes={lanes} bank={layouts is not None}"
+    if lanes:
+        monkeypatch.setenv("ORX_ROLLOUT_LANES", str(lanes))
+    dev = torch.device("cuda", 0)
+    ora = oracle_lib.Oracle(cfg, B, seed, off, layouts=layouts)
+    ora.reset(episode=np.zeros(B, np.int32))
+    eng = BatchedEngine(EnvConfig.from_dict(cfg, layouts=layouts), B, seed=seed,
+                        game_offset=off, device=dev)
+    rs = np.random.RandomState(case)
+    hi = 7 if cfg["flags"] & HEAL else 6
+    log = []
+    for j in range(24):
+        op = rs.choice(["step", "policy", "rollout", "reset", "resume"], p=[.25, .2, .35, .12, .08])
+        p = (int(rs.choice([1, 2, 3])), int(rs.choice([1, 2, 3])))
+        if op == "step":
+            a = rs.randint(1, hi, size=(B, 2)).astype(np.int8)
+            ora.step(a)
+            eng.step(torch.from_numpy(a).to(dev).contiguous())
+        elif op == "policy":
+            a = ora.policy(*p)
+            ora.step(a)
+            got = eng.policy(*p)
+            assert np.array_equal(got.cpu().numpy(), a), f"{where} {log} policy"
+            eng.step(got)
+        elif op == "rollout":
+            n = int(rs.randint(1, 41))
+            for _ in range(n):
+                ora.step(ora.policy(*p))
+            eng.rollout(n, *p)
+            op = f"rollout{n}"
+        elif op == "reset":
+            mask = rs.rand(B) < rs.choice([0.1, 0.5, 1.0])
+            ep = rs.randint(0, 1000, size=B).astype(np.int32)
+            cur = eng.snapshot()["episode"]
+            ep = np.where(mask, ep, cur).astype(np.int32)
+            ora.reset(mask=mask, episode=ep)
+            eng.reset(torch.from_numpy(mask), episode=torch.from_numpy(ep))
+        else:
+            path = tmp_path / f"ck{j}.npz"
+            eng.save(path)
+            eng = BatchedEngine.load(path, device=dev)
+        log.append(op)
+        compare_state(eng.snapshot(), ora.export(), ora.K, f"{where} after {log}")
+    torch.cuda.synchronize()
