@@ -186,3 +186,35 @@ def test_known_answer_scenarios(oracle_lib, case):
         got = np.asarray(s[k])
         got = got[:, 0] if got.ndim == 2 else got[0]
         assert np.array_equal(got, np.asarray(v).reshape(got.shape)), (case["name"], k)
+
+
+def test_npc_stair_fixture_attacks_npcs_on_staircases():
+    """npc_stair_unused_sep holds ticks where a player steps onto its depth's
+    staircase while an NPC stands on it (left there by an Unused despawn and
+    regeneration), and the reference resolves each as a combat on that NPC
+    without a descent (handle_move tests pos_lookup first,
+    updater.py:199-207)."""
+    from optimax_rogue_amd.enums import Move, npc_alive_bits
+    fx = Fixture("npc_stair_unused_sep")
+    step = {int(Move.Up): (0, -1), int(Move.Down): (0, 1), int(Move.Right): (1, 0),
+            int(Move.Left): (-1, 0)}
+    d1, n = int(fx.cfg["p1_depth"]), 0
+    for t in range(fx.T):
+        s, s2 = fx.state(t), fx.state(t + 1)
+        live = npc_alive_bits(s["npc_alive"], fx.K)
+        pos = np.asarray(s["npc_pos"]).astype(np.int64)
+        for g in range(fx.G):
+            for p in range(2):
+                d = step.get(int(fx.actions[t, g, p]))
+                if d is None or s["status"][g] != 1 or s["p_depth"][p][g] != d1:
+                    continue
+                tx, ty = s["p_x"][p][g] + d[0], s["p_y"][p][g] + d[1]
+                if (tx, ty) != (s["st_x"][p][g], s["st_y"][p][g]):
+                    continue
+                on = [k for k in range(fx.K) if live[k, g] and pos[k, g] == tx | (ty << 8)]
+                if not on:
+                    continue
+                n += 1
+                assert s2["p_depth"][p][g] == d1 or s2["episode"][g] != s["episode"][g], (t, g, p)
+                assert any(e[0] == 1 for e in fx.events(t, g)), (t, g, p)   # a combat event
+    assert n >= 10, n
