@@ -738,6 +738,9 @@ KAT_SCENARIOS = {
     "npc_both_hit": ((2, 3, 10), (4, 3, 10), [(3, 3, 2), (6, 6, 3)], (2, 4), False),
     "mutual_kill": ((2, 2, 1), (3, 2, 1), [], (2, 4), True),
     "kill_then_step": ((2, 2, 10), (3, 2, 1), [], (2, 1), True),
+    # an NPC standing on the staircase (possible after an Unused despawn
+    # regenerates its depth): stepping onto it is a combat, not a descent
+    "npc_on_stairs": ((4, 5, 10), (2, 2, 10), [(5, 5, 3)], (2, 5), True),
 }
 
 
