@@ -625,6 +625,30 @@ CASES = {
                                   seed=14, games=12, ticks=260),
 }
 
+
+def sweep_case(case, base=1000):
+    """Draw `case` of tests/test_gpu_fuzz.py's random-configuration sweep as a
+    fixture spec (reference semantics only: the players' 10 / 2 / 1, up to 6
+    games) -- the same configuration the GPU sweep runs engine vs oracle."""
+    sys.path.insert(0, os.path.dirname(HERE))
+    from test_gpu_fuzz import _draw
+    cfg, layouts, B, T, seed, off, pol, _ = _draw(case, base)
+    assert not cfg["flags"] and 3 not in pol, "not a reference-semantics draw"
+    cfg = dict(cfg, player_health=10, player_damage=2, player_armor=1, policy=pol,
+               layouts=layouts)
+    return dict(cfg=cfg, seed=seed, games=min(B, 6), ticks=T, offset=off)
+
+
+# random-configuration sweep draws with the most going on (tests/golden/
+# sweep_reference.py checks every such draw; these are kept as fixtures so
+# the GPU golden tests -- step, events, rollout, codec -- run on them too)
+CASES.update({
+    "sweep_94_sep_unused": sweep_case(94),          # 4x27, 158 descents
+    "sweep_151_bank_stock": sweep_case(151),        # 13x6 bank, stock seeding, 302 combats
+    "sweep_174_bank_dense": sweep_case(174),        # 21x24 bank, 106 NPCs, Separated
+    "sweep_196_dense_stock": sweep_case(196),       # 39x33, 227 NPCs, stock, Separated
+})
+
 SNAP_KEYS_I32 = ["p_x", "p_y", "p_depth", "p_health", "st_x", "st_y", "tick", "status",
                  "episode", "ret_sum", "ep_count", "counters", "npc_pos", "npc_health",
                  "npc_alive"]

@@ -51,9 +51,9 @@ def _layouts(rs, W, H):
     return np.stack(out)
 
 
-def _draw(case: int):
+def _draw(case: int, base: int = None):
     """Configuration, layouts, batch, ticks, seed, offset, bots, lanes of case."""
-    rs = np.random.RandomState(BASE + case)
+    rs = np.random.RandomState((BASE if base is None else base) + case)
     W, H = int(rs.randint(4, 40)), int(rs.randint(4, 40))
     if rs.rand() < 0.15:
         W, H = int(rs.choice([64, 96, 128])), int(rs.choice([64, 128]))
