@@ -34,6 +34,7 @@ import argparse
 import json
 import os
 import platform
+import subprocess
 import sys
 import time
 
@@ -149,7 +150,22 @@ def cpu_baseline(cfg_dict: dict, seconds: float) -> dict:
                          f"Updater.update, one process per core for "
                          f"{full['seconds_per_proc']} s each ({full['env_steps']} env-steps); "
                          "tools/ref_cpu_baseline.py -> profiles/ref_cpu_c3.json"}
+    # the pure-Python object-model restatement of the reference (oracle/pyref.py,
+    # bit-exact vs the reference fixtures): the reference's cost profile timed
+    # on THIS host's cores, one process per core (a child interpreter: the
+    # processes fork from it, not from this GPU-initialized one)
+    pyr = None
+    try:
+        r = subprocess.run([sys.executable, "-m", "oracle.pyref", "--bench",
+                            f"--seconds={max(1.0, 0.2 * seconds)}",
+                            f"--single={max(1.0, 0.3 * seconds)}", f"--procs={cores}"],
+                           cwd=ROOT, capture_output=True, text=True, timeout=300)
+        pyr = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else \
+            {"error": r.stderr[-500:]}
+    except (subprocess.SubprocessError, ValueError, IndexError) as e:
+        pyr = {"error": repr(e)}
     return {"value": total / el, "unit": "env-steps/s", "cores": cores, "kind": "port",
+            "python_restatement": pyr,
             "reference_python": ref,
             "per_core": total / el / cores, "single_core": single,
             "sample": f"C oracle (scalar C restatement of Updater.update + RandomBot) on the "
@@ -299,7 +315,13 @@ def main():
     ap.add_argument("--steps", type=int, default=20,
                     help="timed steps; one step = one --chunk-tick rollout launch of every game")
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=65536, help="games per GPU")
+    ap.add_argument("--batch", type=int, default=65536,
+                    help="games per GPU (weak scaling, the default)")
+    ap.add_argument("--strong", action="store_true",
+                    help="strong scaling: a fixed --global-batch split over the ranks by "
+                         "parallel.shard (SURVEY s8(d) C4) instead of --batch games per GPU")
+    ap.add_argument("--global-batch", type=int, default=524288,
+                    help="games of the whole job with --strong (C4: 524,288)")
     ap.add_argument("--chunk", type=int, default=128,
                     help="ticks per step (one rollout launch: the trajectory horizon a learner "
                          "consumes)")
@@ -334,7 +356,8 @@ def main():
     coll_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
 
     cfg = EnvConfig.c3()
-    G = args.batch * world                    # weak scaling: --batch games per GPU
+    # weak scaling: --batch games per GPU; strong: --global-batch games in all
+    G = args.global_batch if args.strong else args.batch * world
     offset, B = shard(G, rank, world)
     chunk = args.chunk
     # the GPU's games as --streams shards on concurrent HIP streams (the
@@ -367,10 +390,18 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    rank_elapsed = elapsed
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    # every rank's shard and its own timed span (rank 0 reports them)
+    mine = {"rank": rank, "offset": offset, "count": B, "elapsed_s": rank_elapsed,
+            "device": str(dev)}
+    ranks = [mine]
+    if world > 1:
+        ranks = [None] * world
+        dist.all_gather_object(ranks, mine)
 
     # dominant kernel: the timed rollout launches, per step (one launch per
     # shard, the shards' launches overlapping on their streams).
@@ -411,8 +442,16 @@ def main():
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(cfg.to_dict(), args.cpu_seconds)
+        if args.strong:
+            metric = (f"env-steps/sec (whole node) at global batch={G}, 64x64 grid; "
+                      "bit-exact vs ref")
+            workload = (f"C4 strong scaling: {G} games in all (fixed), sharded by global id "
+                        f"over {world} GPU(s)")
+        else:
+            metric = "env-steps/sec (whole node) at batch=65536, 64x64 grid; bit-exact vs ref"
+            workload = f"C3: {args.batch} games/GPU"
         result = {
-            "metric": "env-steps/sec (whole node) at batch=65536, 64x64 grid; bit-exact vs ref",
+            "metric": metric,
             "value": value,
             "unit": "env-steps/s",
             "n_gpus": world,
@@ -420,12 +459,12 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.strong else "weak",
             "vs_baseline": None,
             "dtype": "int32",
             "data": "synthetic (Philox-seeded dungeons and RandomBot actions)",
             "config": {
-                "workload": "C3: 65536 games/GPU, 64x64 grid, 8 NPCs/game, 2x RandomBot, "
+                "workload": f"{workload}, 64x64 grid, 8 NPCs/game, 2x RandomBot, "
                             "Unreachable despawn, max_ticks 1000, autoreset; one step = one "
                             f"{chunk}-tick rollout launch of every game, every tick's "
                             "observation + actions written to HBM",
@@ -466,6 +505,8 @@ def main():
             "episodes_finished": episodes,
             "mean_return_p1": mean_ret,
             "returns_gather_ms": gather_ms,
+            "returns_gather_backend": dist.get_backend() if world > 1 else None,
+            "ranks": ranks,
             "extras": extra,
         }
         print(json.dumps(result), flush=True)

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define ORX_ABI_VERSION 3
+#define ORX_ABI_VERSION 4
 
 /* ---- error codes -------------------------------------------------------- */
 #define ORX_OK 0
@@ -89,9 +89,13 @@ extern "C" {
                              (randombot.py:21, updater.py:114,127), numpy for
                              dungeons and spawn cells (worldgen.py:39-40,
                              world.py:62)                                   */
-#define ORX_DSTORE 256    /* stock-seed mode: dungeons remembered per game
-                             (power of two; the depth gap between the two
-                             players it covers under Unreachable)           */
+#define ORX_DSTORE_MIN 256        /* stock-seed mode: the dungeons each player
+                                     remembers (orx_dstore_depths) are the
+                                     smallest power of two >= max(max_ticks,
+                                     ORX_DSTORE_MIN); ORX_DSTORE_UNBOUNDED when
+                                     max_ticks == 0, at most ORX_DSTORE_MAX   */
+#define ORX_DSTORE_UNBOUNDED 4096
+#define ORX_DSTORE_MAX 65536
 
 /* build extensions (orx_cfg_t.flags): mechanics the reference's readme
  * describes but its code does not implement (readme.md:44-48); off = parity.
@@ -290,10 +294,16 @@ typedef struct orx_state {
   /* stock-seed mode (cfg->rng = ORX_RNG_MT19937; NULL otherwise)            */
   uint32_t* mt_py;              /* [625][B] CPython random: mt[624] + index   */
   uint32_t* mt_np;              /* [625][B] numpy RandomState: key[624] + pos */
-  int32_t* dstore;              /* [ORX_DSTORE][2][B] {depth, sx | sy << 8 |
-                                   (layout + 1) << 16} of entered dungeons,
-                                   slot depth % ORX_DSTORE (the staircases a
-                                   keyed stream would regenerate)            */
+  int32_t* dstore;              /* [2][N][2][B], N = orx_dstore_depths(cfg):
+                                   per player, {depth, sx | sy << 8 |
+                                   (layout + 1) << 16} of each dungeon it
+                                   entered, slot (depth - its start depth)
+                                   mod N -- the staircases a keyed stream
+                                   would regenerate.  A player descends at
+                                   most once per tick, so a ring of N >=
+                                   max_ticks depths still holds every depth
+                                   the other player can yet enter from it
+                                   (Unreachable, updater.py:245-257)         */
   /* character mechanics (any ORX_EXT_CHARACTER flag; NULL otherwise)        */
   int32_t* p_rpg;               /* [ORX_RPG_FIELDS][2][B] player attributes   */
   uint16_t* item_pos;           /* [K][B] ORX_EXT_ITEMS: item dropped by NPC
@@ -322,6 +332,16 @@ const char* orx_build_id(void);
  * device a wave; env ORX_ROLLOUT_LANES overrides).  Results do not depend on
  * it.  No reference counterpart (the reference runs one game per process). */
 int orx_rollout_lanes(int64_t n_games);
+
+/* Stock-seed mode: N, the depths each player's dstore ring holds for this
+ * configuration (orx_state_t.dstore is [2][N][2][B] int32), or ORX_EINVAL
+ * for an invalid configuration.  N >= max_ticks, so every game the
+ * reference can play to max_ticks is played; with max_ticks == 0 (no limit)
+ * or max_ticks > ORX_DSTORE_MAX a game whose lagging player still has to
+ * enter a dungeon more than N levels behind the other stops with
+ * ORX_STATUS_RNG_EXHAUSTED instead of inventing a staircase.  Replaces
+ * nothing: the reference keeps World.dungeons in a dict (world.py:101-180). */
+int orx_dstore_depths(const orx_cfg_t* cfg);
 
 /* Message for the last non-zero return on this thread ("" if none). */
 const char* orx_last_error(void);

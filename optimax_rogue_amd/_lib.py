@@ -13,7 +13,7 @@ from .config import OrxCfg
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "liborx.so")
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 
 class OrxState(ctypes.Structure):
@@ -35,7 +35,7 @@ _lib = None
 
 EXPORTS = ("orx_abi_version", "orx_last_error", "orx_validate_cfg", "orx_reset", "orx_step",
            "orx_step_events", "orx_policy", "orx_rollout", "orx_dungeon_stairs",
-           "orx_dungeon_spawn", "orx_seed_mt", "orx_build_id", "orx_rollout_lanes")
+           "orx_dungeon_spawn", "orx_seed_mt", "orx_build_id", "orx_rollout_lanes", "orx_dstore_depths")
 
 
 def load() -> ctypes.CDLL:
@@ -78,6 +78,8 @@ def load() -> ctypes.CDLL:
     L.orx_build_id.argtypes = []
     L.orx_rollout_lanes.restype = ctypes.c_int
     L.orx_rollout_lanes.argtypes = [i64]
+    L.orx_dstore_depths.restype = ctypes.c_int
+    L.orx_dstore_depths.argtypes = [P(OrxCfg)]
     v = L.orx_abi_version()
     if v != ABI_VERSION:
         raise RuntimeError(f"liborx.so ABI {v} != expected {ABI_VERSION}")

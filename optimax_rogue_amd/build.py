@@ -1,6 +1,19 @@
 """Builds the HIP engine in-tree: optimax_rogue_amd/liborx.so for gfx950.
 
     python -m optimax_rogue_amd.build [--force]
+
+Diagnostic variants (results wrong by design; used by tools/ab_*.py and
+tools/stamps.py to attribute time) are built by the same recipe with extra
+preprocessor definitions, into tools/ab_libs/ by default:
+
+    python -m optimax_rogue_amd.build --variant diag16     # -DORX_DIAG=16: no trajectory stores
+    python -m optimax_rogue_amd.build --variant diag32     # -DORX_DIAG=32: trajectory stores only
+    python -m optimax_rogue_amd.build --variant stamps     # -DORX_STAMPS: s_memtime timeline
+    python -m optimax_rogue_amd.build --define ORX_STREAM_AUX=0 --out /tmp/x.so
+
+The definitions are folded into the library's build id (``orx_build_id()``
+= ``source_id(defines)``), so a diagnostic library can never pass for the
+product build (tests/test_gpu_parity.py::test_loaded_library_is_the_trees_kernel).
 """
 from __future__ import annotations
 
@@ -8,6 +21,7 @@ import hashlib
 import os
 import subprocess
 import sys
+from typing import Iterable, Optional
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG_DIR)
@@ -15,6 +29,14 @@ SRC = os.path.join(PKG_DIR, "csrc", "orx_engine.hip")
 HDR = os.path.join(ROOT, "include", "orx.h")
 OUT = os.path.join(PKG_DIR, "liborx.so")
 ARCH = os.environ.get("ORX_OFFLOAD_ARCH", "gfx950")
+AB_LIBS = os.path.join(ROOT, "tools", "ab_libs")
+
+# named diagnostic variants: their -D sets
+VARIANTS = {
+    "diag16": ("ORX_DIAG=16",),   # rollout without its trajectory stores
+    "diag32": ("ORX_DIAG=32",),   # the trajectory stores alone (no tick runs)
+    "stamps": ("ORX_STAMPS",),    # per-wave s_memtime stamps + rare-block counts
+}
 
 
 def hipcc() -> str:
@@ -38,27 +60,58 @@ def built_id(path: str = OUT):
     return out.stdout.strip() if out.returncode == 0 else None
 
 
-def source_id() -> str:
-    """First 16 hex digits of SHA-256(orx_engine.hip || orx.h): the id
-    orx_build_id() of a library built from these sources returns."""
+def source_id(defines: Iterable[str] = ()) -> str:
+    """The id orx_build_id() of a library built from these sources returns:
+    the first 16 hex digits of SHA-256(orx_engine.hip || orx.h), and for a
+    build with extra definitions ``+`` and their sorted list (so the product
+    id is exactly the sources' hash and no diagnostic build shares it)."""
     h = hashlib.sha256()
     for p in (SRC, HDR):
         with open(p, "rb") as f:
             h.update(f.read())
-    return h.hexdigest()[:16]
+    d = sorted(defines)
+    return h.hexdigest()[:16] + ("+" + ",".join(d) if d else "")
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and os.path.exists(OUT) and built_id() == source_id():
-        return OUT
+def build(force: bool = False, verbose: bool = False, defines: Iterable[str] = (),
+          out: Optional[str] = None) -> str:
+    defines = tuple(defines)
+    out = out or (OUT if not defines else os.path.join(AB_LIBS, "custom.so"))
+    sid = source_id(defines)
+    if not force and os.path.exists(out) and built_id(out) == sid:
+        return out
+    os.makedirs(os.path.dirname(out), exist_ok=True)
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC",
-           "-Wall", f'-DORX_BUILD_ID="{source_id()}"', "-o", OUT + ".tmp", SRC]
+           "-Wall", f'-DORX_BUILD_ID="{sid}"'] + [f"-D{d}" for d in defines] + \
+          ["-o", out + ".tmp", SRC]
     if verbose:
         print(" ".join(cmd))
     subprocess.check_call(cmd)
-    os.replace(OUT + ".tmp", OUT)
-    return OUT
+    os.replace(out + ".tmp", out)
+    return out
+
+
+def build_variant(name: str, force: bool = False, verbose: bool = False) -> str:
+    """tools/ab_libs/<name>.so for a named diagnostic variant (VARIANTS)."""
+    return build(force, verbose, VARIANTS[name], os.path.join(AB_LIBS, name + ".so"))
+
+
+def main(argv):
+    force = "--force" in argv
+    defines, out, variants = [], None, []
+    it = iter(argv)
+    for a in it:
+        if a == "--define":
+            defines.append(next(it))
+        elif a == "--out":
+            out = os.path.abspath(next(it))
+        elif a == "--variant":
+            variants.append(next(it))
+    for v in variants:
+        print(build_variant(v, force, verbose=True))
+    if defines or out or not variants:
+        print(build(force, verbose=True, defines=defines, out=out))
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    main(sys.argv[1:])

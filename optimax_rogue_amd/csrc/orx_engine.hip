@@ -210,6 +210,16 @@ __device__ __forceinline__ Player pick(bool c, const Player& a, const Player& b)
   return r;
 }
 
+// Depths each player's dstore ring holds (orx_dstore_depths, include/orx.h):
+// the smallest power of two >= max(max_ticks, ORX_DSTORE_MIN), capped at
+// ORX_DSTORE_MAX; ORX_DSTORE_UNBOUNDED without a tick limit.
+__host__ __device__ inline uint32_t dstore_depths(int32_t max_ticks) {
+  if (max_ticks <= 0) return ORX_DSTORE_UNBOUNDED;
+  uint32_t n = ORX_DSTORE_MIN;
+  while (n < (uint32_t)max_ticks && n < ORX_DSTORE_MAX) n <<= 1;
+  return n;
+}
+
 struct Cfg {  // device copy of orx_cfg_t plus derived constants (all wave-uniform)
   int32_t W, H, despawn, max_ticks, start_mode, d1, d2, K;
   int32_t npc_hp, player_hp, player_dmg_net, autoreset;
@@ -218,6 +228,7 @@ struct Cfg {  // device copy of orx_cfg_t plus derived constants (all wave-unifo
   int32_t player_dmg, player_armor, mana_max, mana_third, mana_regen, mana_pp;
   int32_t xp_kill, xp_level, drop_pct, item_bonus, item_slots, cooldown;
   int32_t ih;        // H - 2 (interior column height)
+  uint32_t dstore_n; // stock-seed mode: depths per player's dstore ring (a power of two)
   // ceil(2^32 / d) for d = ih and d = H: n / d == umulhi(n, magic) for every
   // n < 2^16 (error < n / 2^32 <= 1/d), so set only when the dividends
   // (interior / grid cell indices) stay below 2^16; 0 = divide
@@ -727,8 +738,12 @@ __device__ __forceinline__ uint32_t py_randbelow(S& s, Key key, uint32_t n, bool
 // Where the world-generation words come from.  PhiloxSrc: keyed streams per
 // purpose (dungeons regenerate from their key, nothing stored).  MtSrc: the
 // game's numpy RandomState, consumed in the reference's call order; a
-// dungeon's staircase cannot be regenerated, so entered dungeons are kept in
-// the dstore ring (slot depth % ORX_DSTORE) for the other player to find.
+// dungeon's staircase cannot be regenerated, so every dungeon a player enters
+// is kept in that player's dstore ring (slot (depth - its start depth) mod N,
+// N = orx_dstore_depths >= max_ticks) for the other player to find: the only
+// present dungeon a player looks up is one the other player entered and has
+// since left (Unreachable: other.start <= nd < other.d, updater.py:272-280),
+// fewer than max_ticks of its descents ago.
 struct PhiloxSrc {
   static constexpr bool kMt = false;
   Key key;
@@ -748,22 +763,31 @@ struct PhiloxSrc {
                                           int32_t& sy, int32_t& lay, bool& err) const {
     dungeon_stair<GRID>(c, key, game, ep, depth, gen, sx, sy, lay, err);
   }
-  __device__ __forceinline__ bool recall(int32_t, int32_t&, int32_t&, int32_t&) const {
+  __device__ __forceinline__ bool recall(int32_t, int32_t, int32_t, int32_t&, int32_t&,
+                                         int32_t&) const {
     return false;  // present dungeons are regenerated from their key
   }
-  __device__ __forceinline__ void remember(int32_t, int32_t, int32_t, int32_t) const {}
+  __device__ __forceinline__ void remember(int32_t, int32_t, int32_t, int32_t, int32_t,
+                                           int32_t) const {}
 };
 
 struct MtSrc {
   static constexpr bool kMt = true;
   MtStream py, np;  // CPython random (bots, shuffles), numpy RandomState (world)
-  int32_t* ds;      // this game's dstore column, stride B
-  uint32_t B;
-  __device__ __forceinline__ void open(const orx_state_t& st, uint32_t B_, uint32_t i) {
+  int32_t* ds;      // this game's dstore column, stride B: [2][N][2]
+  uint32_t B, dmask;  // dmask = N - 1 (N a power of two)
+  __device__ __forceinline__ void open(const orx_state_t& st, const Cfg& c, uint32_t B_,
+                                       uint32_t i) {
     py.open(st.mt_py, B_, i);
     np.open(st.mt_np, B_, i);
     ds = st.dstore + i;
     B = B_;
+    dmask = c.dstore_n - 1u;
+  }
+  // row of player `who` (1 or 2) for depth d entered from start depth `start`
+  __device__ __forceinline__ size_t row(int32_t who, int32_t start, int32_t d) const {
+    const size_t k = (size_t)(who == 1 ? 0u : dmask + 1u) + ((uint32_t)(d - start) & dmask);
+    return 2 * k * B;
   }
   __device__ __forceinline__ void close() const { py.close(); np.close(); }
   __device__ __forceinline__ MtStream& init() { return np; }
@@ -773,9 +797,10 @@ struct MtSrc {
                                           int32_t& sy, int32_t& lay, bool& err) {
     dungeon_draw<GRID>(c, np, Key{0, 0}, sx, sy, lay, err);
   }
-  __device__ __forceinline__ bool recall(int32_t depth, int32_t& sx, int32_t& sy,
-                                         int32_t& lay) const {
-    const size_t slot = (size_t)(2 * (depth & (ORX_DSTORE - 1))) * B;
+  // the dungeon at `depth` as player `who` (started at `start`) entered it
+  __device__ __forceinline__ bool recall(int32_t who, int32_t start, int32_t depth, int32_t& sx,
+                                         int32_t& sy, int32_t& lay) const {
+    const size_t slot = row(who, start, depth);
     if (ds[slot] != depth) return false;
     const uint32_t v = (uint32_t)ds[slot + B];
     sx = (int32_t)(v & 0xFFu);
@@ -783,9 +808,9 @@ struct MtSrc {
     lay = (int32_t)(v >> 16) - 1;
     return true;
   }
-  __device__ __forceinline__ void remember(int32_t depth, int32_t sx, int32_t sy,
-                                           int32_t lay) const {
-    const size_t slot = (size_t)(2 * (depth & (ORX_DSTORE - 1))) * B;
+  __device__ __forceinline__ void remember(int32_t who, int32_t start, int32_t depth, int32_t sx,
+                                           int32_t sy, int32_t lay) const {
+    const size_t slot = row(who, start, depth);
     ds[slot] = depth;
     ds[slot + B] = (int32_t)(((uint32_t)sx & 0xFFu) | (((uint32_t)sy & 0xFFu) << 8) |
                              ((uint32_t)(lay + 1) << 16));
@@ -832,13 +857,13 @@ __device__ __forceinline__ void setup_game(const Cfg& c, Key key, Src& src, Play
                                           key), p2.sx, p2.sy);
   }
   if (!drawn1) src.template dungeon<GRID>(c, p1.d, 0, p1.sx, p1.sy, p1.lay, err);
-  src.remember(p1.d, p1.sx, p1.sy, p1.lay);
+  src.remember(1, p1.d, p1.d, p1.sx, p1.sy, p1.lay);
   if (sep) {
     if (!drawn2) src.template dungeon<GRID>(c, p2.d, 0, p2.sx, p2.sy, p2.lay, err);
-    src.remember(p2.d, p2.sx, p2.sy, p2.lay);
   } else {
     p2.sx = p1.sx; p2.sy = p1.sy; p2.lay = p1.lay;
   }
+  src.remember(2, p2.d, p2.d, p2.sx, p2.sy, p2.lay);
   npc.clear();
   auto&& s = src.init();
   const int total = 2 + (NCAP ? c.K : 0);
@@ -974,9 +999,10 @@ __device__ __forceinline__ void descend(const Cfg& c, Key key, Src& src, Player&
   int32_t sx, sy, lay;
   if (present && other.d == nd) {
     sx = other.sx; sy = other.sy; lay = other.lay;
-  } else if (!(present && src.recall(nd, sx, sy, lay))) {
+  } else if (!(present && src.recall(3 - self_iden, other_start, nd, sx, sy, lay))) {
     // keyed: regenerate (present or not); stock-seed: a present dungeon must
-    // be in the ring (a gap beyond ORX_DSTORE stops the game), else draw it
+    // be in the other player's ring (orx_dstore_depths: always, up to
+    // max_ticks), else draw it
     if (Src::kMt && present) err = true;
     bool drawn = false;
     if constexpr (!Src::kMt && !GRID) {  // straight from the stream's first block
@@ -988,7 +1014,7 @@ __device__ __forceinline__ void descend(const Cfg& c, Key key, Src& src, Player&
     }
     if (!drawn) src.template dungeon<GRID>(c, nd, gen, sx, sy, lay, err);
   }
-  src.remember(nd, sx, sy, lay);
+  src.remember(self_iden, self_iden == 1 ? c.d1 : c.d2, nd, sx, sy, lay);
   if (!present) {
     dl.dungeon += 1;
     ev.emit(ORX_EV_DUNGEON, 0, nd, 0);                 // updater.py:278-280
@@ -1755,6 +1781,7 @@ __device__ __forceinline__ Cfg make_cfg(const orx_cfg_t& h, const orx_state_t& s
   c.drop_pct = h.item_drop_pct; c.item_bonus = h.item_bonus; c.item_slots = h.item_slots;
   c.cooldown = h.combat_cooldown;
   c.ih = h.height - 2;
+  c.dstore_n = dstore_depths(h.max_ticks);
   c.ih_magic = (int64_t)(h.width - 2) * (h.height - 2) <= 65536
                    ? (uint32_t)(0xFFFFFFFFu / (uint32_t)c.ih + 1u) : 0u;
   c.h_magic = (int64_t)h.width * h.height <= 65536
@@ -2514,7 +2541,7 @@ __global__ void __launch_bounds__(kRolloutBlock) rollout_kernel(orx_cfg_t hc, or
 // of n) and np.random.seed(n) (numpy mt19937_seed = init_genrand) for
 // n = seed + global game id; both indices at 624 (the first draw twists).
 __global__ void __launch_bounds__(256) mt_seed_kernel(orx_state_t st, uint32_t B, uint64_t seed,
-                                                      uint32_t off) {
+                                                      uint32_t off, uint32_t dstore_n) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= B) return;
   const uint64_t n = seed + off + i;
@@ -2551,7 +2578,7 @@ __global__ void __launch_bounds__(256) mt_seed_kernel(orx_state_t st, uint32_t B
   }
   py[0] = 0x80000000u;
   py[624 * (size_t)B] = 624;
-  for (uint32_t k = 0; k < ORX_DSTORE; ++k) st.dstore[(size_t)(2 * k) * B + i] = -1;
+  for (uint32_t k = 0; k < 2u * dstore_n; ++k) st.dstore[(size_t)(2 * k) * B + i] = -1;
 }
 
 // RandomBot.move = random.choice(list(Move)) = Move(1 + _randbelow(5))
@@ -2587,7 +2614,7 @@ __global__ void __launch_bounds__(256) mt_reset_kernel(orx_cfg_t hc, orx_state_t
   if (mask && !mask[i]) return;
   const Cfg c = make_cfg(hc, st);
   MtSrc src;
-  src.open(st, B, i);
+  src.open(st, c, B, i);
   Player p1, p2;
   Npcs<NCAP> npc;
   npc.bind(st, c, B, i);
@@ -2651,7 +2678,7 @@ __global__ void __launch_bounds__(256) mt_step_kernel(orx_cfg_t hc, orx_state_t 
     if (EV) n_events[i] = 0;
     if (!c.autoreset) return;
     MtSrc src;
-    src.open(st, B, i);
+    src.open(st, c, B, i);
     const uint32_t ep = (uint32_t)st.episode[i] + 1u;
     int32_t tick;
     setup_game<NCAP, GRID>(c, key, src, p1, p2, npc, tick, status);
@@ -2689,7 +2716,7 @@ __global__ void __launch_bounds__(256) mt_step_kernel(orx_cfg_t hc, orx_state_t 
   Events<EV> ev{EV ? events + (size_t)i * ORX_MAX_EVENTS * 4 : nullptr, 0};
   bool err = false;
   MtSrc src;
-  src.open(st, B, i);
+  src.open(st, c, B, i);
   const bool p1_first = mt_shuffles(src.py, npc, err);
   int32_t sep = (c.ext & ORX_EXT_SEPARATION_DAMAGE) ? st.sep_start[i] : -1;
   tick_game<NCAP, EV, GRID>(c, key, src, game, ep, p1_first, p1, p2, npc, items, m, tick, status,
@@ -2731,7 +2758,7 @@ __global__ void __launch_bounds__(256) mt_rollout_kernel(orx_cfg_t hc, orx_state
   int32_t sep = (c.ext & ORX_EXT_SEPARATION_DAMAGE) ? st.sep_start[i] : -1;
   bool stairs_dirty = false, npc_dirty = false;
   MtSrc src;
-  src.open(st, B, i);
+  src.open(st, c, B, i);
   TrajWriter<false> traj(obs, act, B, i);
   for (int32_t t = 0; t < n_ticks; ++t) {
     int32_t a1 = ORX_MOVE_STAY, a2 = ORX_MOVE_STAY;
@@ -2941,6 +2968,27 @@ int device_simds() {
   return 4 * n;
 }
 
+// Dynamic LDS one workgroup may declare on the current device with the
+// opt-in limit raise (160 KiB on gfx950): the opt-in attribute, else the
+// default per-block one, else kMaxLdsBlock; read once per device.
+std::atomic<int> g_lds_block[kMaxDevices];
+
+uint32_t device_lds_per_block() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return kMaxLdsBlock;
+  int n = g_lds_block[dev].load(std::memory_order_relaxed);
+  if (n <= 0) {
+    int optin = 0, plain = 0;
+    if (hipDeviceGetAttribute(&optin, hipDeviceAttributeSharedMemPerBlockOptin, dev) != hipSuccess)
+      optin = 0;
+    if (hipDeviceGetAttribute(&plain, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess)
+      plain = 0;
+    n = optin > 0 ? optin : plain > 0 ? plain : (int)kMaxLdsBlock;
+    g_lds_block[dev].store(n, std::memory_order_relaxed);
+  }
+  return (uint32_t)n;
+}
+
 int lanes_override() {  // read per launch, so a sweep can change it in-process
   const char* e = getenv("ORX_ROLLOUT_LANES");
   const int x = e ? atoi(e) : 0;
@@ -2984,6 +3032,11 @@ int orx_rollout_lanes(int64_t n_games) {
 
 const char* orx_last_error(void) { return g_err; }
 
+int orx_dstore_depths(const orx_cfg_t* cfg) {
+  if (const int r = check_cfg(cfg)) return r;
+  return (int)dstore_depths(cfg->max_ticks);
+}
+
 int orx_validate_cfg(const orx_cfg_t* cfg) {
   int r = check_cfg(cfg);
   if (r == ORX_OK) g_err[0] = 0;
@@ -3000,7 +3053,8 @@ int orx_seed_mt(const orx_cfg_t* cfg, const orx_state_t* st, int64_t n_games, ui
   if (n_games == 0) return ORX_OK;
   if ((r = check_state(cfg, st, false))) return r;
   hipLaunchKernelGGL(mt_seed_kernel, grid_for(n_games), dim3(kBlock), 0, (hipStream_t)stream, *st,
-                     (uint32_t)n_games, seed, (uint32_t)game_offset);
+                     (uint32_t)n_games, seed, (uint32_t)game_offset,
+                     dstore_depths(cfg->max_ticks));
   return launch_status("orx_seed_mt");
 }
 
@@ -3150,11 +3204,15 @@ int orx_rollout(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p1, 
   const uint32_t lds_n = use_lds ? (uint32_t)tiles : 0u;
   uint32_t lds = use_lds ? (uint32_t)((tiles + 15u) & ~15ull) : 0u;
   // dense NPCs: one occupancy bitmap per game of the block after the tiles,
-  // when they fit the CU's LDS (a workgroup may take all 160 KiB on gfx950)
+  // when they fit the device's per-workgroup LDS (a workgroup may take all
+  // 160 KiB on gfx950); the bitmaps are an optimization -- without them the
+  // kernel reads the occupancy grid from HBM -- so a part with less LDS, or
+  // a refused limit raise, launches without them instead of failing
   uint32_t lds_bits = 0;
+  const uint32_t lds_max = device_lds_per_block();
   if (nc == kDense && !getenv("ORX_NO_LDS_BITS")) {
     const uint32_t bb = (uint32_t)((cfg->width * cfg->height + 31) / 32) * 4u;
-    if ((uint64_t)lds + (uint64_t)per_block * bb <= kMaxLdsBlock) {
+    if ((uint64_t)lds + (uint64_t)per_block * bb <= lds_max) {
       lds_bits = bb;
       lds += per_block * bb;
     }
@@ -3163,8 +3221,11 @@ int orx_rollout(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p1, 
   if (nc == N && pm == P && grid == G) {                                                        \
     if (lds > 65536u &&                                                                         \
         hipFuncSetAttribute(reinterpret_cast<const void*>(&rollout_kernel<N, P, G>),            \
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) \
-      return fail(ORX_EIO, "orx_rollout: cannot raise the LDS limit");                          \
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) { \
+      (void)hipGetLastError();                                                                  \
+      if (lds_bits) { lds -= per_block * lds_bits; lds_bits = 0; }                              \
+      if (lds > 65536u) return fail(ORX_EIO, "orx_rollout: cannot raise the LDS limit");        \
+    }                                                                                           \
     hipLaunchKernelGGL((rollout_kernel<N, P, G>), dim3((B + per_block - 1) / per_block),        \
                        dim3(threads), lds, s, *cfg, *st,                                        \
                        policy_p1, policy_p2, n_ticks, obs, act, B, k, off, lanes, lds_n,        \

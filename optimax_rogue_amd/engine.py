@@ -17,7 +17,7 @@ import torch
 
 from . import _lib
 from .config import EnvConfig
-from .enums import (DSTORE, EXT_CHARACTER, EXT_ITEMS, EXT_SEPARATION_DAMAGE, MAX_EVENTS,
+from .enums import (EXT_CHARACTER, EXT_ITEMS, EXT_SEPARATION_DAMAGE, MAX_EVENTS,
                     MAX_REG_NPCS, N_COUNTERS, OBS_FIELDS, RNG_MT19937, RPG_FIELDS, Policy)
 
 STATE_FIELDS = ("p_x", "p_y", "p_depth", "p_health", "st_x", "st_y", "tick", "status", "episode",
@@ -91,12 +91,16 @@ class BatchedEngine:
             self.sep_start = torch.full((B,), -1, dtype=torch.int32, device=device)
             ptrs["sep_start"] = self.sep_start.data_ptr()
         # stock-seed mode: each game's CPython random and numpy RandomState
-        # (MT19937 key words + index, column per game) and its remembered
-        # dungeons (depth, sx | sy << 8 | (layout + 1) << 16) by depth mod DSTORE
+        # (MT19937 key words + index, column per game) and the dungeons each
+        # player entered (depth, sx | sy << 8 | (layout + 1) << 16), a ring of
+        # N = orx_dstore_depths(cfg) >= max_ticks per player, slot (depth -
+        # the player's start depth) mod N
         self.mt_py = self.mt_np = self.dstore = None
         if int(cfg.rng) == RNG_MT19937:
             self.mt_py, self.mt_np = z(625, B), z(625, B)
-            self.dstore = z(DSTORE, 2, B)
+            n = int(self.lib.orx_dstore_depths(ctypes.byref(self._ccfg)))
+            _lib.check("orx_dstore_depths", min(n, 0))
+            self.dstore = z(2, n, 2, B)
             ptrs.update({f: getattr(self, f).data_ptr() for f in ("mt_py", "mt_np", "dstore")})
         # the readme's character mechanics (EXT_CHARACTER flags): player attributes
         # [RPG_FIELDS][2][B]; with EXT_ITEMS and NPCs the items each NPC slot
@@ -406,16 +410,24 @@ class BatchedEngine:
         idx = range(self.B) if indices is None else indices
         extra = {}
         if full_world and self.dstore is not None:
-            # stock-seed mode: the remembered dungeons are the world
+            # stock-seed mode: the remembered dungeons are the world; a depth
+            # no player stands on is in the ring of a player who entered it
             ds = snap["dstore"]
+            n = ds.shape[1]
+            c = self.cfg
+            starts = (int(c.p1_depth), int(c.p2_depth)) if int(c.start_mode) == 2 else (0, 0)
             for i in idx:
                 d1, d2 = int(snap["p_depth"][0][i]), int(snap["p_depth"][1][i])
                 for d in world_depths(self.cfg, d1, d2):
                     if d in (d1, d2):
                         continue
-                    if int(ds[d % DSTORE, 0, i]) != d:
+                    for p, (s0, dp) in enumerate(zip(starts, (d1, d2))):
+                        k = (d - s0) % n
+                        if s0 <= d <= dp and int(ds[p, k, 0, i]) == d:
+                            v = int(ds[p, k, 1, i])
+                            break
+                    else:
                         raise RuntimeError(f"game {i}: depth {d} not in the dungeon store")
-                    v = int(ds[d % DSTORE, 1, i])
                     extra.setdefault(i, {})[d] = (v & 0xFF, (v >> 8) & 0xFF, (v >> 16) - 1)
         elif full_world:
             req = []

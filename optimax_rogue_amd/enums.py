@@ -79,7 +79,8 @@ RPG_FIELDS = ("mana", "xp", "damage", "max_health", "items", "cooldown")
 # EnvConfig.rng (orx_cfg_t.rng, include/orx.h ORX_RNG_*)
 RNG_PHILOX = 0
 RNG_MT19937 = 1
-DSTORE = 256        # ORX_DSTORE: remembered dungeons per game in stock-seed mode
+# stock-seed mode: depths per player's dstore ring (orx_dstore_depths)
+DSTORE_MIN, DSTORE_UNBOUNDED, DSTORE_MAX = 256, 4096, 65536
 
 # per-game event counter rows (include/orx.h ORX_CNT_*)
 CNT_COMBAT, CNT_DESCEND, CNT_DUNGEON, CNT_NPC_DEATH = range(4)

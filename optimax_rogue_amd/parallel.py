@@ -34,11 +34,13 @@ def env_rank() -> Tuple[int, int, int]:
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
-def init(backend: Optional[str] = None, device: Optional[torch.device] = None) -> Tuple[int, int]:
-    """Initializes the default process group if WORLD_SIZE > 1 (nccl = RCCL for
-    GPU tensors, gloo otherwise).  Returns (rank, world)."""
+def init(backend: Optional[str] = None, device: Optional[torch.device] = None,
+         force: bool = False) -> Tuple[int, int]:
+    """Initializes the default process group if WORLD_SIZE > 1, or with
+    ``force`` for any world size (nccl = RCCL for GPU tensors, bound to
+    ``device``; gloo otherwise).  Returns (rank, world)."""
     rank, world, _ = env_rank()
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or force) and not dist.is_initialized():
         if backend is None:
             backend = "nccl" if device is not None and device.type == "cuda" else "gloo"
         kw = {"device_id": device} if backend == "nccl" and device is not None else {}
@@ -51,7 +53,7 @@ def gather_returns(local: torch.Tensor, global_batch: int,
     """All-gathers ``local`` [F, count_r] (e.g. ret_sum / ep_count rows) from every
     rank into [F, global_batch] in global game id order.  Shards may differ in
     size by one game; they are padded to a common width for the collective."""
-    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+    if not dist.is_initialized():
         return local
     world = dist.get_world_size(group)
     width = -(-int(global_batch) // world)

@@ -25,7 +25,7 @@ import torch
 
 from .config import EnvConfig
 from .engine import BatchedEngine
-from .enums import OBS_FIELDS, Policy, UpdateResult
+from .enums import EXT_HEAL, OBS_FIELDS, STATUS_BAD_ACTION, Policy, UpdateResult
 
 _STATUS = OBS_FIELDS.index("status")
 
@@ -52,9 +52,13 @@ class VecEnv:
 
     @staticmethod
     def outcome(before: torch.Tensor, after: torch.Tensor):
-        """(reward, done) of a transition between two status tensors."""
+        """(reward, done) of a transition between two status tensors.  A game
+        that leaves InProgress for an engine stop code (>= 16: a bad action, an
+        exhausted random stream) is done too, with reward 0 -- a truncation:
+        the engine's autoreset starts its next episode on the following step,
+        so the learner must see this one end."""
         done = (before == UpdateResult.InProgress) & (after >= UpdateResult.Player1Win) \
-            & (after <= UpdateResult.Tie)
+            & ((after <= UpdateResult.Tie) | (after >= STATUS_BAD_ACTION))
         reward = torch.where(done, (after == UpdateResult.Player1Win).float()
                              - (after == UpdateResult.Player2Win).float(),
                              torch.zeros((), device=after.device))
@@ -62,18 +66,40 @@ class VecEnv:
 
     # -- reset / step / rollout ----------------------------------------------------
     def reset(self, mask: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """Starts the masked games (all if None) at their next episode's setup."""
-        self.engine.reset(mask)
+        """Starts the masked games (all if None) at their NEXT episode's setup:
+        each game's episode index advances by one, so a truncated game gets a
+        fresh dungeon and fresh draws (randomness is keyed on game, episode
+        and tick), and two resets in a row give different starts.  A truncated
+        episode has no outcome: it does not count in the engine's episode
+        returns (ret_sum / ep_count)."""
+        e = self.engine
+        if mask is not None:
+            mask = mask.to(self.device).bool().reshape(-1)
+            if mask.numel() != self.B:
+                raise ValueError("mask must have n_games elements")
+        e.reset(mask, episode=e.episode + 1)
         return self.observe()
+
+    def _max_move(self) -> int:
+        return 6 if int(self.engine.cfg.flags) & EXT_HEAL else 5
 
     def step(self, actions: torch.Tensor):
         """Plays one tick: ``actions`` int8 [n_games] (player 1; the opponent
-        policy moves player 2) or [n_games, 2] (self-play).  Returns
-        (observation, reward, done, status)."""
+        policy moves player 2) or [n_games, 2] (self-play), Move values 1..5
+        (1..6 with EXT_HEAL; anything else raises ValueError -- checked on the
+        host, so this synchronizes).  Returns (observation, reward, done,
+        status); every tensor is fresh (status is a copy, not the engine's
+        buffer, which the next call overwrites)."""
         e = self.engine
-        a = actions.to(device=self.device, dtype=torch.int8)
-        if tuple(a.shape) not in ((self.B,), (self.B, 2)):   # no silent broadcasting
-            raise ValueError(f"actions must be [n_games] or [n_games, 2], got {tuple(a.shape)}")
+        if tuple(actions.shape) not in ((self.B,), (self.B, 2)):   # no silent broadcasting
+            raise ValueError(f"actions must be [n_games] or [n_games, 2], got "
+                             f"{tuple(actions.shape)}")
+        a = actions.to(device=self.device)
+        hi = self._max_move()
+        if bool(((a < 1) | (a > hi)).any()):   # before the int8 cast: 257 must not wrap to 1
+            raise ValueError(f"actions must be Move values 1..{hi} (an argmax over logits is "
+                             "0-based: add 1)")
+        a = a.to(torch.int8)
         if a.dim() == 1:
             if self.opponent is None:
                 raise ValueError("self-play (opponent=None) takes [n_games, 2] actions")
@@ -82,7 +108,7 @@ class VecEnv:
         else:
             e.actions.copy_(a)
         before = e.status.clone()
-        status = e.step(e.actions)
+        status = e.step(e.actions).clone()
         reward, done = self.outcome(before, status)
         return self.observe(), reward, done, status
 

@@ -606,6 +606,14 @@ CASES = {
                                             policy=(2, 2), n_npcs=2,
                                             layouts=make_layouts(8, 9, 3, 104, n_stairs=(1, 2))),
                                    seed=4000, games=12, ticks=320),
+    # stock-seed mode with a depth gap beyond 256 (player 2 starts 260 levels
+    # down): player 1's StaircaseBot creates depths 1..259, then enters the
+    # depths player 2's RandomBot created and left -- each a dungeon the
+    # engine must recall from player 2's dstore ring (the former depth-mod-256
+    # store had overwritten them with player 1's shallow depths)
+    "stock_deep_gap": dict(cfg=dict(rng=1, width=5, height=5, max_ticks=1500, start_mode=2,
+                                    p1_depth=0, p2_depth=260, policy=(2, 1)), seed=5000, games=4,
+                           ticks=1100),
     # a one-layout bank (no dungeon draw), Separated start, both StaircaseBots
     # dense NPCs (more than the engine's 16 register slots: its occupancy-grid
     # form); the reference's updater takes any number of entities

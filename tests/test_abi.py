@@ -39,7 +39,7 @@ def test_library_exports_every_declared_symbol(lib):
     assert decl == sorted(["orx_abi_version", "orx_last_error", "orx_validate_cfg", "orx_reset",
                            "orx_step", "orx_step_events", "orx_policy", "orx_rollout",
                            "orx_dungeon_stairs", "orx_dungeon_spawn", "orx_seed_mt",
-                           "orx_build_id", "orx_rollout_lanes"])
+                           "orx_build_id", "orx_rollout_lanes", "orx_dstore_depths"])
     from optimax_rogue_amd import _lib
     assert sorted(_lib.EXPORTS) == decl
     for name in decl:
@@ -55,6 +55,19 @@ def test_library_is_built_from_the_tree(lib):
     """orx_build_id() is the hash of the tree's own orx_engine.hip + orx.h."""
     from optimax_rogue_amd import _lib, build
     assert _lib.build_id() == build.source_id()
+
+
+def test_diagnostic_builds_carry_their_defines_in_the_build_id():
+    """A -DORX_DIAG / -DORX_STAMPS library (build.VARIANTS, built by the
+    committed recipe) reports an id that differs from the product's, so it can
+    never pass test_library_is_built_from_the_tree."""
+    from optimax_rogue_amd import build
+    prod = build.source_id()
+    ids = {v: build.source_id(d) for v, d in build.VARIANTS.items()}
+    assert len(set(ids.values()) | {prod}) == len(ids) + 1
+    for v, i in ids.items():
+        assert i.startswith(prod + "+") and all(d in i for d in build.VARIANTS[v])
+    assert build.source_id(["B=1", "A=2"]) == build.source_id(["A=2", "B=1"])
 
 
 def test_struct_layouts_match_header():

@@ -260,7 +260,7 @@ def test_vecenv_step_and_rollout(oracle_lib):
     B, dev = 1024, torch.device("cuda", 0)
     env = VecEnv(cfg, B, seed=9, device=dev, opponent=2)     # StaircaseBot opponent
     ora = oracle_lib.Oracle(cfg.to_dict(), B, 9)
-    ora.reset(episode=np.zeros(B, np.int32))
+    ora.reset(episode=np.ones(B, np.int32))   # env.reset(): every game's next episode (1)
     obs = env.reset()
     rs = np.random.RandomState(2)
     rew_sum = np.zeros(B)
@@ -286,3 +286,40 @@ def test_vecenv_step_and_rollout(oracle_lib):
     after = env.engine.episode_returns().cpu().numpy()
     assert np.array_equal(out["reward"].sum(0).cpu().numpy(), after[0] - before[0])
     assert np.array_equal(out["done"].sum(0).cpu().numpy(), after[1] - before[1])
+
+
+def test_vecenv_reset_starts_next_episodes(oracle_lib):
+    """VecEnv.reset(mask) truncates the masked games into their NEXT episode
+    (a fresh dungeon and fresh draws, the oracle's setup of that episode);
+    two resets in a row give different starts; the status step() returns is
+    a copy the next step does not overwrite."""
+    import torch
+    from golden_util import compare_state
+    from optimax_rogue_amd import EnvConfig, VecEnv
+    cfg = EnvConfig.c3()
+    B, dev = 2048, torch.device("cuda", 0)
+    env = VecEnv(cfg, B, seed=4, device=dev)
+    o0 = env.observe().cpu().numpy()
+    o1 = env.reset().cpu().numpy()
+    o2 = env.reset().cpu().numpy()
+    assert (env.engine.episode.cpu().numpy() == 2).all()
+    for a, b in ((o0, o1), (o1, o2)):   # positions/staircases of the new episodes differ
+        assert (a[:, [0, 1, 4, 5, 10, 11]] != b[:, [0, 1, 4, 5, 10, 11]]).any(1).mean() > 0.99
+    ora = oracle_lib.Oracle(cfg.to_dict(), B, 4)
+    ora.reset(episode=np.full(B, 2, np.int32))
+    compare_state(env.engine.snapshot(), ora.export(), cfg.n_npcs, "two resets")
+    # a masked reset advances only the masked games
+    for _ in range(7):
+        _, _, _, st = env.step(torch.randint(1, 6, (B,), dtype=torch.int8, device=dev))
+    st_copy = st.clone()
+    env.step(torch.randint(1, 6, (B,), dtype=torch.int8, device=dev))
+    assert torch.equal(st, st_copy)
+    mask = torch.zeros(B, dtype=torch.bool)
+    mask[::3] = True
+    ep_before = env.engine.episode.cpu().numpy().copy()
+    env.reset(mask)
+    ep = env.engine.episode.cpu().numpy()
+    m = mask.numpy()
+    assert (ep[m] == ep_before[m] + 1).all() and (ep[~m] == ep_before[~m]).all()
+    tick = env.engine.tick.cpu().numpy()
+    assert (tick[m] == 1).all() and (tick[~m] > 1).all()

@@ -85,3 +85,31 @@ def test_c4_eight_shards_equal_whole_batch():
     assert np.array_equal(np.concatenate(rets, axis=1), want_ret)
     assert want_ret[1].sum() >= G   # every game finished at least one episode
     torch.cuda.synchronize()
+
+
+def test_rccl_process_group_on_the_device():
+    """The nccl (= RCCL) path of parallel.init / gather_returns on hardware:
+    a process group bound to cuda:0 (init_process_group's device_id), the
+    all-gather run on device tensors (no host round trip), the result equal
+    to the input in global id order.  One rank: the box has one GPU and RCCL
+    takes one rank per device; the 2/4/8-rank RCCL runs are the driver's
+    SCALE bench, whose code path this is."""
+    code = (
+        "import sys, torch, torch.distributed as dist\n"
+        f"sys.path.insert(0, {os.path.dirname(HERE)!r})\n"
+        "from optimax_rogue_amd.parallel import init, gather_returns\n"
+        "dev = torch.device('cuda', 0)\n"
+        "torch.cuda.set_device(dev)\n"
+        "init('nccl', dev, force=True)\n"
+        "assert dist.get_backend() == 'nccl', dist.get_backend()\n"
+        "x = torch.arange(2 * 1001, dtype=torch.int32, device=dev).reshape(2, 1001)\n"
+        "y = gather_returns(x, 1001)\n"
+        "torch.cuda.synchronize()\n"
+        "assert y.device == dev and torch.equal(x, y)\n"
+        "dist.destroy_process_group()\n"
+        "print('RCCL_OK')\n")
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", RANK="0", WORLD_SIZE="1",
+               LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()))
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                       timeout=110)
+    assert r.returncode == 0 and "RCCL_OK" in r.stdout, (r.stdout + r.stderr)[-3000:]

@@ -393,25 +393,118 @@ def _invariants(s, cfg):
     assert set(np.unique(s["status"]).tolist()) <= {1, 2, 3, 4}
 
 
+def _obs_rows(ex):
+    """The 14-field observation rows (OBS_FIELDS order) of an oracle export:
+    int32 [14, games]."""
+    return np.stack([ex["p_x"][0], ex["p_y"][0], ex["p_depth"][0], ex["p_health"][0],
+                     ex["p_x"][1], ex["p_y"][1], ex["p_depth"][1], ex["p_health"][1],
+                     ex["tick"], ex["status"], ex["st_x"][0], ex["st_y"][0],
+                     ex["st_x"][1], ex["st_y"][1]]).astype(np.int32)
+
+
+def _replay(ora, n_ticks, pol=(1, 1)):
+    """n_ticks of policy + step on the oracle: (act [T, games, 2], obs [T, 14, games])."""
+    acts, obs = [], []
+    for _ in range(n_ticks):
+        a = ora.policy(*pol)
+        ora.step(a)
+        acts.append(a)
+        obs.append(_obs_rows(ora.export()))
+    return np.stack(acts), np.stack(obs)
+
+
 def test_c3_full_size_properties(oracle_lib):
-    """B=65536 at 64x64 with K=8: invariants after 1000 ticks and a sample of
-    games replayed on the oracle by global id."""
+    """B=65536 at 64x64 with K=8, one 1000-tick launch WITH the trajectory
+    outputs (so the PM=1 RandomBot/buffer-store form at 64 games per wave):
+    invariants after it, and a sample of games replayed on the oracle by
+    global id -- every tick's observation row and action pair, and the final
+    state."""
+    import torch
     from optimax_rogue_amd import EnvConfig
+    from optimax_rogue_amd.enums import OBS_FIELDS
     cfg = EnvConfig.c3().to_dict()
     B, T = 65536, 1000
     eng = _engine(cfg, B, 3)
-    eng.rollout(T, 1, 1)
+    obs = torch.empty((T, len(OBS_FIELDS), B), dtype=torch.int32, device=eng.device)
+    act = torch.empty((T, B, 2), dtype=torch.int8, device=eng.device)
+    eng.rollout(T, 1, 1, obs=obs, act=act)
     s = eng.snapshot()
     _invariants(s, cfg)
     assert s["ep_count"].sum() >= B  # max_ticks 1000 -> every game finished once
     rng = np.random.default_rng(0)
-    for gid in rng.choice(B, 48, replace=False):
+    gids = np.sort(rng.choice(B, 48, replace=False))
+    idx = torch.from_numpy(gids).to(eng.device)
+    g_obs = obs.index_select(2, idx).cpu().numpy()
+    g_act = act.index_select(1, idx).cpu().numpy()
+    del obs, act
+    for j, gid in enumerate(gids):
         ora = oracle_lib.Oracle(cfg, 1, 3, int(gid))
         ora.reset(episode=np.zeros(1, np.int32))
-        ora.rollout(1, 1, T)
-        want = ora.export()
+        w_act, w_obs = _replay(ora, T)
+        assert np.array_equal(g_act[:, j:j + 1], w_act), f"gid {gid} actions"
+        assert np.array_equal(g_obs[:, :, j:j + 1], w_obs), f"gid {gid} observation rows"
         got = {k: (v[..., gid:gid + 1]) for k, v in s.items()}
-        compare_state(got, want, 8, f"gid {gid}")
+        compare_state(got, ora.export(), 8, f"gid {gid}")
+
+
+def test_bench_timed_path_vs_oracle(oracle_lib):
+    """bench.py's timed path exactly: StreamShardedEngine(C3, 65,536 games,
+    seed 3, two stream shards of 32,768) launched through rollout_launcher
+    with both trajectory buffers -- rollout_kernel<8, 1, false> (PM=1) at 32
+    games per wave -- for 9 back-to-back 128-tick launches (1,152 ticks: every
+    game crosses the max_ticks-1000 autoreset), as bench.py issues them (fork,
+    launches, join).  128 games -- 16 windows of 8 consecutive global ids,
+    including both ends of each shard -- are replayed on the oracle tick by
+    tick: every tick's 14-field observation row and both actions of every
+    launch, and the whole state after each launch."""
+    import torch
+    from optimax_rogue_amd import EnvConfig
+    from optimax_rogue_amd.engine import StreamShardedEngine
+    cfg = EnvConfig.c3()
+    B, T, L, seed = 65536, 128, 9, 3
+    dev = torch.device("cuda", 0)
+    eng = StreamShardedEngine(cfg, B, seed=seed, game_offset=0, device=dev, n_streams=2)
+    assert [e.B for e in eng.parts] == [32768, 32768]
+    assert [e.game_offset for e in eng.parts] == [0, 32768]
+    assert eng.rollout_lanes() == 32          # the games per wave bench.py times at
+    obs, act = eng.trajectory_buffers(T)
+    launch = eng.rollout_launcher(T, 1, 1, obs=obs, act=act)
+    rng = np.random.default_rng(7)
+    starts = [0, 32760, 32768, 65528] + sorted(
+        int(x) for x in rng.choice(np.arange(8, 65520, 8), 12, replace=False))
+    gids = np.concatenate([np.arange(s, s + 8) for s in starts])
+    oras = []
+    for s in starts:
+        o = oracle_lib.Oracle(cfg.to_dict(), 8, seed, s)
+        o.reset(episode=np.zeros(8, np.int32))
+        oras.append(o)
+    # per shard: which sampled ids it holds, at which local index
+    sel = []
+    for e in eng.parts:
+        loc = gids - e.game_offset
+        m = (loc >= 0) & (loc < e.B)
+        sel.append((np.nonzero(m)[0], torch.from_numpy(loc[m]).to(dev)))
+    for n in range(L):
+        eng.fork()
+        launch()
+        eng.join()
+        torch.cuda.synchronize()
+        g_obs = np.zeros((T, 14, len(gids)), np.int32)
+        g_act = np.zeros((T, len(gids), 2), np.int8)
+        for (pos, li), o, a in zip(sel, obs, act):
+            g_obs[:, :, pos] = o.index_select(2, li).cpu().numpy()
+            g_act[:, pos] = a.index_select(1, li).cpu().numpy()
+        snap = eng.snapshot()
+        for w, (s, ora) in enumerate(zip(starts, oras)):
+            cols = slice(8 * w, 8 * w + 8)
+            w_act, w_obs = _replay(ora, T)
+            where = f"launch {n} ids {s}..{s + 7}"
+            assert np.array_equal(g_act[:, cols], w_act), f"{where}: actions"
+            assert np.array_equal(g_obs[:, :, cols], w_obs), f"{where}: observation rows"
+            got = {k: v[..., s:s + 8] for k, v in snap.items()}
+            compare_state(got, ora.export(), cfg.n_npcs, f"{where}: state")
+    # every sampled game went through the max_ticks autoreset in the timed form
+    assert (snap["ep_count"][gids] >= 1).all() and (snap["episode"][gids] >= 1).all()
 
 
 def test_bad_action_and_no_autoreset():

@@ -9,11 +9,34 @@ def test_vecenv_outcome():
     the step that end in it count; player 1's view."""
     torch = pytest.importorskip("torch")
     from optimax_rogue_amd.vecenv import VecEnv
-    before = torch.tensor([1, 1, 1, 1, 2, 3, 4, 16], dtype=torch.int32)
-    after = torch.tensor([1, 2, 3, 4, 1, 3, 4, 16], dtype=torch.int32)
+    before = torch.tensor([1, 1, 1, 1, 2, 3, 4, 16, 1, 1, 16], dtype=torch.int32)
+    after = torch.tensor([1, 2, 3, 4, 1, 3, 4, 16, 16, 17, 1], dtype=torch.int32)
     reward, done = VecEnv.outcome(before, after)
-    assert done.tolist() == [False, True, True, True, False, False, False, False]
-    assert reward.tolist() == [0.0, 1.0, -1.0, 0.0, 0.0, 0.0, 0.0, 0.0]
+    # an engine stop code (>= 16) ends the episode as a truncation (reward 0):
+    # the autoreset restarts the game on the next step
+    assert done.tolist() == [False, True, True, True, False, False, False, False, True, True,
+                             False]
+    assert reward.tolist() == [0.0, 1.0, -1.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0]
+
+
+@pytest.mark.parametrize("bad", [[0, 1, 2], [1, 6, 2], [1, 2, 257], [-1, 2, 3]])
+def test_vecenv_step_rejects_non_moves(bad):
+    """A learner's 0-based argmax (or any value outside the Move codes) is
+    refused before it reaches the engine, instead of stopping the game with
+    ORX_STATUS_BAD_ACTION and silently autoresetting it."""
+    import torch
+    from optimax_rogue_amd import EnvConfig
+    from optimax_rogue_amd.vecenv import VecEnv
+    env = VecEnv.__new__(VecEnv)
+    env.engine = _bare_engine(EnvConfig(), 3)
+    env.B, env.device, env.opponent = 3, torch.device("cpu"), 1
+    with pytest.raises(ValueError, match="Move values"):
+        env.step(torch.tensor(bad, dtype=torch.int32))
+    with pytest.raises(ValueError, match="Move values"):
+        env.step(torch.tensor([bad, bad, bad], dtype=torch.int64).t().contiguous()[:, :2])
+    # with EXT_HEAL, 6 (a heal) is a valid action
+    env.engine.cfg = EnvConfig(flags=4 | 8)
+    assert env._max_move() == 6
 
 
 def test_npc_alive_bits():

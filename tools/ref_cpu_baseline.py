@@ -82,9 +82,12 @@ def _worker(args):
     t_end = time.perf_counter() + seconds
     while True:
         if mode == "updater":
-            m1, m2 = bots[0].move(gs), bots[1].move(gs)
+            # Updater.update timed alone with pre-generated actions,
+            # a fresh uniform draw over the 5 moves for each player every tick
+            # (the bots' own draw, made outside the timed loop)
+            acts = [(bots[0].move(gs), bots[1].move(gs)) for _ in range(64)]
             t0 = time.perf_counter()
-            for _ in range(64):
+            for m1, m2 in acts:
                 gs.on_tick()
                 res = upd.update(gs, m1, m2)
                 steps += 1
