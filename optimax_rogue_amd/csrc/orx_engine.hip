@@ -2105,9 +2105,11 @@ __device__ __forceinline__ void rollout_tick(const Cfg& c, const orx_state_t& st
     const bool npc_stair = (hit1 & st1) | (hit2 & st2);
     const bool full0 =
         (meet & (st1 | st2)) | (st1 & st2) | ext_ordered | rpg_ordered | npc_stair;
-    // the games that use the initiative order: the ordered tick, a meet, a
-    // descend into the other's depth
-    const bool ordered_use = in_progress & (full0 | meet | desc_meet);
+    // the games that always use the initiative order: the ordered tick and a
+    // meet.  A descend into the other's depth uses it only when its spawn
+    // candidate is one of the other player's two cells (before and after its
+    // move): the descend branch draws it then (first_from_packed)
+    const bool ordered_use = in_progress & (full0 | meet);
     uint32_t pk_shf = tb.a;
     if (need == 0 && ordered_use) pk_shf = tick_block(key, game, ep, tick).a;
     // all sixteen 2-bit shuffle fields rejected (high bits all set): the
@@ -2166,7 +2168,76 @@ __device__ __forceinline__ void rollout_tick(const Cfg& c, const orx_state_t& st
       tick = ft;
       status = end ? ORX_TIE : ORX_IN_PROGRESS;
       dl.eps += end ? 1 : 0;
-      if (!lean & (st1 | st2)) {  // one player descends
+      bool desc_done = false;  // the descend's fast form below finished it
+      if constexpr (!GRID) {
+        if (!lean & (st1 | st2)) {
+#ifdef ORX_STAMPS
+          ORX_CYC_BEGIN(cyf);
+#endif
+          // One player descends, the common case of handle_descend
+          // (updater.py:259-296) on a keyed empty dungeon: the staircase from
+          // the first block of its (episode, depth, generation) stream, or
+          // the other player's when it stands on that depth; the spawn cell
+          // from the first word of the tick's SPAWN stream, taken when that
+          // word is accepted and the cell is neither of the other player's
+          // cells (before and after its move) -- then the initiative order
+          // cannot matter and no clash is possible -- and no NPC lives on the
+          // new depth.  Anything else falls through to the general form.
+          // Field-wise selects, both blocks drawn side by side.
+          const int32_t sd = st1 ? p1.d : p2.d, od = st1 ? p2.d : p1.d;
+          const int32_t o_start = st1 ? c.d2 : c.d1;
+          const int32_t nd = sd + 1;
+          bool present;
+          uint32_t gen = 0;
+          if (c.despawn == ORX_DESPAWN_UNREACHABLE) {
+            present = o_start <= nd && nd <= od;
+          } else {
+            present = od == nd;
+            gen = (!present && o_start <= nd && nd < od) ? 1u : 0u;
+          }
+          const bool other_on = od == nd;
+          W4 wd = philox(game, ep, (uint32_t)nd, tag(PUR_DUNGEON, gen), key);
+          W4 ws = philox(game, ep, (uint32_t)t0, tag(PUR_SPAWN, 0), key);
+          launder_w4(wd);
+          launder_w4(ws);
+          int32_t sx, sy;
+          bool ok = stair_from_block(c, wd, sx, sy);
+          const bool o_stairs = present & other_on;
+          sx = o_stairs ? (st1 ? p2.sx : p1.sx) : sx;
+          sy = o_stairs ? (st1 ? p2.sy : p1.sy) : sy;
+          ok |= o_stairs;
+          const uint32_t v = ws.a & c.ground.mask;
+          int32_t x, y;
+          ground_cell<false>(c, v, -1, sx, sy, x, y);
+          const int32_t ox = st1 ? p2.x : p1.x, oy = st1 ? p2.y : p1.y;      // after its move
+          const int32_t ox0 = st1 ? x2o : x1o, oy0 = st1 ? y2o : y1o;       // before it
+          const bool touch = other_on & (((x == ox) & (y == oy)) | ((x == ox0) & (y == oy0)));
+          const bool npc_depth = NCAP > 0 && nd == c.d1 && npc.any_alive();
+          ok = ok & (c.ground.rng != 0u) & (v <= c.ground.rng) & !touch & !npc_depth;
+          if (ok) {
+            p1.d = st1 ? nd : p1.d;
+            p1.x = st1 ? x : p1.x;
+            p1.y = st1 ? y : p1.y;
+            p1.sx = st1 ? sx : p1.sx;
+            p1.sy = st1 ? sy : p1.sy;
+            p2.d = st1 ? p2.d : nd;
+            p2.x = st1 ? p2.x : x;
+            p2.y = st1 ? p2.y : y;
+            p2.sx = st1 ? p2.sx : sx;
+            p2.sy = st1 ? p2.sy : sy;
+            dl.descend += 1;
+            dl.dungeon += present ? 0 : 1;
+            desc_done = true;
+#ifdef ORX_STAMPS
+            ORX_COUNT(dl.n_desc);
+#endif
+          }
+#ifdef ORX_STAMPS
+          ORX_CYC_END(dl.cy_desc, cyf);
+#endif
+        }
+      }
+      if (!lean & (st1 | st2) & !desc_done) {  // one player descends: the general form
 #ifdef ORX_STAMPS
         ORX_COUNT(dl.n_desc);
         ORX_CYC_BEGIN(cy1);
@@ -2182,8 +2253,8 @@ __device__ __forceinline__ void rollout_tick(const Cfg& c, const orx_state_t& st
         // cell before that player's move, which may then attack it
         bool s_first = false;
         if (desc_meet) {
-          const uint32_t sa = ~(pk_shf >> 1) & 0x55555555u;  // nonzero: all-reject is ordered
-          s_first = (((pk_shf >> __builtin_ctz(sa)) & 1u) != 0) == st1;
+          const uint32_t pk = need > 0 ? pk_shf : tick_block(key, game, ep, t0).a;
+          s_first = first_from_packed(pk, key, game, ep, t0, err) == st1;
         }
         const int32_t ox0 = st1 ? x2o : x1o, oy0 = st1 ? y2o : y1o;
         Player Ot = O;
