@@ -272,9 +272,10 @@ def extras(torch, cfg, dev, B_cfg, K, large_rollout=False):
         go()
         d = timed_launches(torch, go, reps)
         us = sorted(d)[len(d) // 2]
-        lanes = e.rollout_lanes()
+        shape = e.rollout_shape(pol, pol)
         del e, o, a, go
-        return {"games": games, "ticks_per_launch": T, "games_per_wave": lanes,
+        return {"games": games, "ticks_per_launch": T, "games_per_wave": shape["games_per_wave"],
+                "lanes_per_game": shape["lanes_per_game"], "nontemporal": shape["nontemporal"],
                 "us_per_launch": us * 1e6, "env_steps_per_s": games * T / us}
 
     out["c2"] = dict(rollout_rate(EnvConfig.c2(), 4096, 1), policy="2x RandomBot", grid="32x32")

@@ -333,6 +333,21 @@ const char* orx_build_id(void);
  * it.  No reference counterpart (the reference runs one game per process). */
 int orx_rollout_lanes(int64_t n_games);
 
+/* The shape of an orx_rollout launch with these arguments (trajectory:
+ * obs and act both given): games per wave (1..64), lanes per game (2 for the
+ * paired form -- no NPCs, no dungeon bank, two RandomBots or two
+ * StaircaseBots, batches below 64 games per wave: one lane per player) and
+ * whether the trajectory rows are stored nontemporal (whole-line row
+ * segments) or with the default policy.  Results never depend on it.  No
+ * reference counterpart. */
+typedef struct orx_rollout_shape {
+  int32_t games_per_wave;
+  int32_t lanes_per_game;
+  int32_t nontemporal;
+} orx_rollout_shape_t;
+int orx_rollout_shape(const orx_cfg_t* cfg, int32_t policy_p1, int32_t policy_p2,
+                      int64_t n_games, int32_t trajectory, orx_rollout_shape_t* out);
+
 /* Stock-seed mode: N, the depths each player's dstore ring holds for this
  * configuration (orx_state_t.dstore is [2][N][2][B] int32), or ORX_EINVAL
  * for an invalid configuration.  N >= max_ticks, so every game the

@@ -25,6 +25,11 @@ class OrxState(ctypes.Structure):
         "dstore", "p_rpg", "item_pos", "item_mask", "npc_grid")]
 
 
+class OrxRolloutShape(ctypes.Structure):
+    """ctypes mirror of orx_rollout_shape_t."""
+    _fields_ = [(n, ctypes.c_int32) for n in ("games_per_wave", "lanes_per_game", "nontemporal")]
+
+
 class OrxError(RuntimeError):
     def __init__(self, fn: str, code: int, msg: str):
         super().__init__(f"{fn} returned {code}: {msg}")
@@ -35,7 +40,8 @@ _lib = None
 
 EXPORTS = ("orx_abi_version", "orx_last_error", "orx_validate_cfg", "orx_reset", "orx_step",
            "orx_step_events", "orx_policy", "orx_rollout", "orx_dungeon_stairs",
-           "orx_dungeon_spawn", "orx_seed_mt", "orx_build_id", "orx_rollout_lanes", "orx_dstore_depths")
+           "orx_dungeon_spawn", "orx_seed_mt", "orx_build_id", "orx_rollout_lanes", "orx_dstore_depths",
+           "orx_rollout_shape")
 
 
 def load() -> ctypes.CDLL:
@@ -78,8 +84,13 @@ def load() -> ctypes.CDLL:
     L.orx_build_id.argtypes = []
     L.orx_rollout_lanes.restype = ctypes.c_int
     L.orx_rollout_lanes.argtypes = [i64]
-    L.orx_dstore_depths.restype = ctypes.c_int
-    L.orx_dstore_depths.argtypes = [P(OrxCfg)]
+    # (bound only when present: an A/B diagnostic may load an older build)
+    if hasattr(L, "orx_rollout_shape"):
+        L.orx_rollout_shape.restype = ctypes.c_int
+        L.orx_rollout_shape.argtypes = [P(OrxCfg), i32, i32, i64, i32, P(OrxRolloutShape)]
+    if hasattr(L, "orx_dstore_depths"):
+        L.orx_dstore_depths.restype = ctypes.c_int
+        L.orx_dstore_depths.argtypes = [P(OrxCfg)]
     v = L.orx_abi_version()
     if v != ABI_VERSION:
         raise RuntimeError(f"liborx.so ABI {v} != expected {ABI_VERSION}")

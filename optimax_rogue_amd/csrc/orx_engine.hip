@@ -1928,6 +1928,68 @@ __global__ void __launch_bounds__(256) policy_kernel(orx_state_t st, int32_t pol
   out[i] = pack_actions(a1, a2);
 }
 
+// One player descends -- the common case of handle_descend (updater.py:259-296)
+// on a keyed empty dungeon -- as straight-line selects: the staircase from
+// the first block of the new depth's (episode, depth, generation) stream, or
+// the other player's when it stands on that depth; the spawn cell from the
+// first word of the tick's SPAWN stream, taken when that word is accepted and
+// the cell is neither of the other player's cells (before and after its
+// move; then the initiative order cannot matter and no clash is possible)
+// and no NPC lives on the new depth.  Both blocks are drawn side by side.
+// Writes the descender's depth, cell and staircase and returns true; false
+// (nothing written) sends the tick to the general form.  st1: player 1
+// descends.  (ox0, oy0) / (ox1, oy1): the other player's cell before / after
+// its move this tick.
+template <int NCAP>
+__device__ __forceinline__ bool fast_descend(const Cfg& c, Key key, uint32_t game, uint32_t ep,
+                                             int32_t t0, bool st1, Player& p1, Player& p2,
+                                             int32_t ox0, int32_t oy0, int32_t ox1, int32_t oy1,
+                                             const Npcs<NCAP>& npc, Deltas& dl) {
+  const int32_t sd = st1 ? p1.d : p2.d, od = st1 ? p2.d : p1.d;
+  const int32_t o_start = st1 ? c.d2 : c.d1;
+  const int32_t nd = sd + 1;
+  bool present;
+  uint32_t gen = 0;
+  if (c.despawn == ORX_DESPAWN_UNREACHABLE) {
+    present = o_start <= nd && nd <= od;
+  } else {
+    present = od == nd;
+    gen = (!present && o_start <= nd && nd < od) ? 1u : 0u;
+  }
+  const bool other_on = od == nd;
+  W4 wd = philox(game, ep, (uint32_t)nd, tag(PUR_DUNGEON, gen), key);
+  W4 ws = philox(game, ep, (uint32_t)t0, tag(PUR_SPAWN, 0), key);
+  launder_w4(wd);
+  launder_w4(ws);
+  int32_t sx, sy;
+  bool ok = stair_from_block(c, wd, sx, sy);
+  const bool o_stairs = present & other_on;
+  sx = o_stairs ? (st1 ? p2.sx : p1.sx) : sx;
+  sy = o_stairs ? (st1 ? p2.sy : p1.sy) : sy;
+  ok |= o_stairs;
+  const uint32_t v = ws.a & c.ground.mask;
+  int32_t x, y;
+  ground_cell<false>(c, v, -1, sx, sy, x, y);
+  const bool touch = other_on & (((x == ox1) & (y == oy1)) | ((x == ox0) & (y == oy0)));
+  const bool npc_depth = NCAP > 0 && nd == c.d1 && npc.any_alive();
+  ok = ok & (c.ground.rng != 0u) & (v <= c.ground.rng) & !touch & !npc_depth;
+  if (ok) {
+    p1.d = st1 ? nd : p1.d;
+    p1.x = st1 ? x : p1.x;
+    p1.y = st1 ? y : p1.y;
+    p1.sx = st1 ? sx : p1.sx;
+    p1.sy = st1 ? sy : p1.sy;
+    p2.d = st1 ? p2.d : nd;
+    p2.x = st1 ? p2.x : x;
+    p2.y = st1 ? p2.y : y;
+    p2.sx = st1 ? p2.sx : sx;
+    p2.sy = st1 ? p2.sy : sy;
+    dl.descend += 1;
+    dl.dungeon += present ? 0 : 1;
+  }
+  return ok;
+}
+
 // updater.py:150-162 over the max_ticks result the rollout's common path set,
 // after a combat or separation damage there (the ordered path has its own
 // chain; a double death is a Tie: ORX_EXT_RANDOM_DOUBLE_DEATH is ordered).
@@ -1940,6 +2002,253 @@ __device__ __forceinline__ void deaths_over(const Player& p1, const Player& p2, 
     dl.ret += (s == ORX_PLAYER1_WIN ? 1 : 0) - (s == ORX_PLAYER2_WIN ? 1 : 0);
     status = s;
   }
+}
+
+// The rare block of a rollout tick (rollout_tick's comment lists its cases),
+// from the pre-tick state: finishes the game's tick in place and returns
+// whether it ran the ordered tick (which applies its own extensions).  Also
+// the paired rollout's rare path (pair_rollout_kernel), where both lanes of a
+// game run it on the same rebuilt pair of players.
+template <int NCAP, bool GRID, class M>
+__device__ __forceinline__ bool rare_tick(const Cfg& c, const orx_state_t& st, uint32_t B,
+                                          uint32_t i, Key key, uint32_t game, uint32_t& ep,
+                                          Player& p1, Player& p2, Npcs<NCAP>& npc,
+                                          Items<NCAP>& items, M& hp, int32_t& tick,
+                                          int32_t& status, Deltas& dl, int32_t& sep,
+                                          bool& restarted, const W4& tb, int need, int32_t t1x,
+                                          int32_t t1y, int32_t t2x, int32_t t2y,
+                                          bool ext_ordered) {
+  launder(t1x, t1y, t2x, t2y);
+  launder(p1.x, p1.y, p2.x, p2.y);
+  launder(p1.d, p2.d, p1.sx, p1.sy);
+  launder(p2.sx, p2.sy, status, tick);
+  const bool in_progress = status == ORX_IN_PROGRESS;
+  const bool meet = ((uint32_t)(p1.d ^ p2.d) |
+                     min((uint32_t)(t1x ^ p2.x) | (uint32_t)(t1y ^ p2.y),
+                         min((uint32_t)(t2x ^ p1.x) | (uint32_t)(t2y ^ p1.y),
+                             (uint32_t)(t1x ^ t2x) | (uint32_t)(t1y ^ t2y)))) == 0u;
+  const uint32_t k1 = (uint32_t)t1x | ((uint32_t)t1y << 8);
+  const uint32_t k2 = (uint32_t)t2x | ((uint32_t)t2y << 8);
+  const bool hit1 = NCAP > 0 && (p1.d == c.d1) && npc_on(c, npc, k1);
+  const bool hit2 = NCAP > 0 && (p2.d == c.d1) && npc_on(c, npc, k2);
+  const bool st1 = stair_tile<GRID>(c, p1, t1x, t1y), st2 = stair_tile<GRID>(c, p2, t2x, t2y);
+  const bool desc_meet = (st1 & (p2.d == p1.d + 1)) | (st2 & (p1.d == p2.d + 1));
+  // the character mechanics (ORX_EXT_RPG) keep the common path's rules:
+  // each attacker's own mana and damage, NPC hits and the kill credit in the
+  // drawn order, steps onto items; a descend-meet (whose clash would undo a
+  // step) takes the ordered tick
+  const bool rpg_ordered = ((c.ext & ORX_EXT_CHARACTER) && desc_meet) ||
+                           ((c.ext & ORX_EXT_README_COMBAT) && meet);
+  // an NPC standing on a staircase (left there when an Unused-despawned
+  // depth is regenerated with its staircase elsewhere) is attacked, not
+  // descended through: handle_move tests pos_lookup before the tile
+  // (updater.py:199-207), which the ordered tick follows literally
+  const bool npc_stair = (hit1 & st1) | (hit2 & st2);
+  const bool full0 =
+      (meet & (st1 | st2)) | (st1 & st2) | ext_ordered | rpg_ordered | npc_stair;
+  // the games that always use the initiative order: the ordered tick and a
+  // meet.  A descend into the other's depth uses it only when its spawn
+  // candidate is one of the other player's two cells (before and after its
+  // move): the descend branch draws it then (first_from_packed)
+  const bool ordered_use = in_progress & (full0 | meet);
+  uint32_t pk_shf = tb.a;
+  if (need == 0 && ordered_use) pk_shf = tick_block(key, game, ep, tick).a;
+  // all sixteen 2-bit shuffle fields rejected (high bits all set): the
+  // SHUFFLE stream fallback and its cap, in the ordered tick
+  const bool shf_reject = ordered_use & ((pk_shf | 0x55555555u) == 0xFFFFFFFFu);
+  const bool full = full0 | shf_reject;
+  const bool took_ordered = in_progress & full;
+  const int32_t t0 = tick, ft = tick + 1;
+  const bool end = c.max_ticks && ft >= c.max_ticks;
+  if (!in_progress) {
+    if (c.autoreset) {  // the next episode (worldgen.py:77-87, 124-135)
+#ifdef ORX_STAMPS
+      ORX_COUNT(dl.n_reset);
+      ORX_CYC_BEGIN(cy1);
+#endif
+      ep += 1;
+      setup_game<NCAP, GRID>(c, key, game, ep, p1, p2, npc, tick, status);
+      items.clear();
+      if constexpr (NCAP > 0) {
+        if constexpr (NCAP == kDense) {
+          store_new_npcs(st, c, B, i, npc, true);  // health rows in HBM
+        } else {
+          store_new_npcs(st, c, B, i, npc, false);  // health: from hp at the end
+          hp.fill(c.npc_hp);
+        }
+      }
+      restarted = true;
+      sep = -1;
+#ifdef ORX_STAMPS
+      ORX_CYC_END(dl.cy_reset, cy1);
+#endif
+    }
+  } else if (full) {  // the ordered tick
+#ifdef ORX_STAMPS
+    ORX_COUNT(dl.n_ordered);
+    ORX_CYC_BEGIN(cy1);
+#endif
+    bool err = false;
+    const bool p1_first = first_from_packed(pk_shf, key, game, ep, t0, err);
+    Events<false> ev{nullptr, 0};
+    tick_game<NCAP, false, GRID>(c, key, game, ep, p1_first, p1, p2, npc, items, hp, tick,
+                                 status, err, dl, ev, sep);
+#ifdef ORX_STAMPS
+    ORX_CYC_END(dl.cy_ordered, cy1);
+#endif
+  } else {
+    // the common path's rules, then the one-sided events: a player that
+    // hits an NPC, descends or meets the other does not move freely
+    const bool lean = meet;
+    const bool s1 = !lean & !hit1 & !st1, s2 = !lean & !hit2 & !st2;
+    const int32_t x1o = p1.x, y1o = p1.y, x2o = p2.x, y2o = p2.y;  // for a descend-meet
+    p1.x = s1 ? t1x : p1.x;
+    p1.y = s1 ? t1y : p1.y;
+    p2.x = s2 ? t2x : p2.x;
+    p2.y = s2 ? t2y : p2.y;
+    tick = ft;
+    status = end ? ORX_TIE : ORX_IN_PROGRESS;
+    dl.eps += end ? 1 : 0;
+    bool desc_done = false;  // fast_descend finished it
+    if constexpr (!GRID) {
+      if (!lean & (st1 | st2)) {
+#ifdef ORX_STAMPS
+        ORX_CYC_BEGIN(cyf);
+#endif
+        // the other player has made its move above
+        desc_done = fast_descend<NCAP>(c, key, game, ep, t0, st1, p1, p2,
+                                       st1 ? x2o : x1o, st1 ? y2o : y1o,
+                                       st1 ? p2.x : p1.x, st1 ? p2.y : p1.y, npc, dl);
+#ifdef ORX_STAMPS
+        if (desc_done) ORX_COUNT(dl.n_desc);
+        ORX_CYC_END(dl.cy_desc, cyf);
+#endif
+      }
+    }
+    if (!lean & (st1 | st2) & !desc_done) {  // one player descends: the general form
+#ifdef ORX_STAMPS
+      ORX_COUNT(dl.n_desc);
+      ORX_CYC_BEGIN(cy1);
+#endif
+      PhiloxSrc src{key, game, ep};
+      auto spawn = src.spawn(t0);
+      Events<false> ev{nullptr, 0};
+      bool err = false;
+      Player S = pick(st1, p1, p2);
+      Player O = pick(st1, p2, p1);  // after its own move
+      // into the other's depth (desc_meet), the drawn order matters: moving
+      // first, the descender's spawn cell is tested against the other's
+      // cell before that player's move, which may then attack it
+      bool s_first = false;
+      if (desc_meet) {
+        const uint32_t pk = need > 0 ? pk_shf : tick_block(key, game, ep, t0).a;
+        s_first = first_from_packed(pk, key, game, ep, t0, err) == st1;
+      }
+      const int32_t ox0 = st1 ? x2o : x1o, oy0 = st1 ? y2o : y1o;
+      Player Ot = O;
+      Ot.x = s_first ? ox0 : O.x;
+      Ot.y = s_first ? oy0 : O.y;
+      descend<NCAP, false, GRID>(c, key, src, S, Ot, st1 ? c.d2 : c.d1, npc, spawn, dl, err,
+                                 st1 ? 1 : 2, ev);
+      const bool clash = s_first & ((O.x != ox0) | (O.y != oy0)) & (O.x == S.x) & (O.y == S.y);
+      O.x = clash ? ox0 : O.x;
+      O.y = clash ? oy0 : O.y;
+      S.hp -= (clash && c.player_dmg_net > 0) ? c.player_dmg_net : 0;
+      dl.combat += clash ? 1 : 0;
+      p1 = pick(st1, S, O);
+      p2 = pick(st1, O, S);
+      if (err) {  // an exhausted spawn stream stops the game (never observed)
+        dl.eps -= end ? 1 : 0;
+        status = ORX_STATUS_RNG_EXHAUSTED;
+      }
+      if (clash) deaths_over(p1, p2, end, status, dl);
+#ifdef ORX_STAMPS
+      ORX_CYC_END(dl.cy_desc, cy1);
+#endif
+    }
+    bool kc1 = false, kc2 = false;  // ORX_EXT_LEVELING: each player's kill this tick
+    if (NCAP > 0 && (hit1 | hit2)) {  // NPCs are swept after both moves
+#ifdef ORX_STAMPS
+      ORX_COUNT(dl.n_hits);
+#endif
+      Events<false> ev{nullptr, 0};
+      dl.combat += (hit1 ? 1 : 0) + (hit2 ? 1 : 0);
+      int32_t d1 = c.player_dmg_net > 0 ? c.player_dmg_net : 0, d2 = d1;
+      if (c.ext & ORX_EXT_RPG) {  // each attacker's own damage and mana
+        d1 = hit1 ? rpg_attack(c, p1) : 0;
+        d2 = hit2 ? rpg_attack(c, p2) : 0;
+      }
+      const int h1 = hit1 ? npc.find(k1) : -1, h2 = hit2 ? npc.find(k2) : -1;
+      if (c.ext & ORX_EXT_RPG) {
+        // hits in the drawn order: one NPC hit by both (a meet) credits the
+        // hit that takes it to zero
+        bool sw = false;
+        if (lean) {
+          const uint32_t sa = ~(pk_shf >> 1) & 0x55555555u;
+          sw = ((pk_shf >> __builtin_ctz(sa)) & 1u) == 0;
+        }
+        bool ka = false, kb = false;
+        npc_hits(c, npc, hp, sw ? h2 : h1, sw ? h1 : h2, sw ? d2 : d1, sw ? d1 : d2, dl, ev,
+                 ka, kb, sw ? k2 : k1, sw ? k1 : k2);
+        kc1 = sw ? kb : ka;
+        kc2 = sw ? ka : kb;
+        if ((c.ext & ORX_EXT_ITEMS) && kc1) drop_item(c, key, game, ep, t0, h1, k1, npc, items);
+        if ((c.ext & ORX_EXT_ITEMS) && kc2) drop_item(c, key, game, ep, t0, h2, k2, npc, items);
+      } else {
+        // two hits are then order-free: only the health left matters
+        npc_hits(c, npc, hp, h1, h2, d1, d2, dl, ev, kc1, kc2, k1, k2);
+      }
+    }
+    if (lean) {  // a meet: the two moves in the drawn order
+#ifdef ORX_STAMPS
+      ORX_COUNT(dl.n_meet);
+#endif
+      const uint32_t sa = ~(pk_shf >> 1) & 0x55555555u;  // nonzero: all-reject is ordered
+      const bool p1_first = ((pk_shf >> __builtin_ctz(sa)) & 1u) != 0;
+      const int32_t ax = p1_first ? t1x : t2x, ay = p1_first ? t1y : t2y;
+      const int32_t bx = p1_first ? t2x : t1x, by = p1_first ? t2y : t1y;
+      const int32_t fx0 = p1_first ? p1.x : p2.x, fy0 = p1_first ? p1.y : p2.y;
+      const int32_t sx0 = p1_first ? p2.x : p1.x, sy0 = p1_first ? p2.y : p1.y;
+      const bool hf = p1_first ? hit1 : hit2, hs = p1_first ? hit2 : hit1;
+      const bool occf = (ax == sx0) & (ay == sy0);
+      const int32_t fx = (occf | hf) ? fx0 : ax, fy = (occf | hf) ? fy0 : ay;
+      const bool occs = (bx == fx) & (by == fy);
+      const int32_t sx = (occs | hs) ? sx0 : bx, sy = (occs | hs) ? sy0 : by;
+      const int32_t dmg = c.player_dmg_net > 0 ? c.player_dmg_net : 0;
+      p1.x = p1_first ? fx : sx;
+      p1.y = p1_first ? fy : sy;
+      p2.x = p1_first ? sx : fx;
+      p2.y = p1_first ? sy : fy;
+      if (NCAP > 0 && (c.ext & ORX_EXT_ITEMS)) {  // the meet's steps onto items (a
+        // health item may save a player hit in the tick: before the win check)
+        if ((p1.d == c.d1) & ((p1.x != x1o) | (p1.y != y1o))) pick_up(c, p1, npc, items);
+        if ((p2.d == c.d1) & ((p2.x != x2o) | (p2.y != y2o))) pick_up(c, p2, npc, items);
+      }
+      if (c.ext & ORX_EXT_RPG) {  // each attacker's own damage and mana
+        const bool a1 = p1_first ? occf : occs, a2 = p1_first ? occs : occf;
+        const int32_t e1 = a1 ? rpg_attack(c, p1) : 0, e2 = a2 ? rpg_attack(c, p2) : 0;
+        p2.hp -= e1;
+        p1.hp -= e2;
+      } else {
+        p1.hp -= (p1_first ? occs : occf) ? dmg : 0;
+        p2.hp -= (p1_first ? occf : occs) ? dmg : 0;
+      }
+      dl.combat += (occf ? 1 : 0) + (occs ? 1 : 0);
+      deaths_over(p1, p2, end, status, dl);
+    }
+    // the sweep's experience after every combat of the tick: a player the
+    // other killed in a meet is not refilled
+    if (NCAP > 0 && (c.ext & ORX_EXT_LEVELING)) {
+      if (kc1) gain_xp(c, p1);
+      if (kc2) gain_xp(c, p2);
+    }
+    if (NCAP > 0 && (c.ext & ORX_EXT_ITEMS) && !lean) {  // a step onto an item takes it
+      // (readme.md:44; a meet's steps were taken above)
+      if (!st1 & (p1.d == c.d1) & ((p1.x != x1o) | (p1.y != y1o))) pick_up(c, p1, npc, items);
+      if (!st2 & (p2.d == c.d1) & ((p2.x != x2o) | (p2.y != y2o))) pick_up(c, p2, npc, items);
+    }
+  }
+  return took_ordered;
 }
 
 // One rollout tick of one game (the hot loop of server/main.py:110-113,
@@ -2077,289 +2386,9 @@ __device__ __forceinline__ void rollout_tick(const Cfg& c, const orx_state_t& st
     ORX_COUNT(dl.n_rare);
     ORX_CYC_BEGIN(cy0);
 #endif
-    launder(t1x, t1y, t2x, t2y);
-    launder(p1.x, p1.y, p2.x, p2.y);
-    launder(p1.d, p2.d, p1.sx, p1.sy);
-    launder(p2.sx, p2.sy, status, tick);
-    const bool in_progress = status == ORX_IN_PROGRESS;
-    const bool meet = ((uint32_t)(p1.d ^ p2.d) |
-                       min((uint32_t)(t1x ^ p2.x) | (uint32_t)(t1y ^ p2.y),
-                           min((uint32_t)(t2x ^ p1.x) | (uint32_t)(t2y ^ p1.y),
-                               (uint32_t)(t1x ^ t2x) | (uint32_t)(t1y ^ t2y)))) == 0u;
-    const uint32_t k1 = (uint32_t)t1x | ((uint32_t)t1y << 8);
-    const uint32_t k2 = (uint32_t)t2x | ((uint32_t)t2y << 8);
-    const bool hit1 = NCAP > 0 && (p1.d == c.d1) && npc_on(c, npc, k1);
-    const bool hit2 = NCAP > 0 && (p2.d == c.d1) && npc_on(c, npc, k2);
-    const bool st1 = stair_tile<GRID>(c, p1, t1x, t1y), st2 = stair_tile<GRID>(c, p2, t2x, t2y);
-    const bool desc_meet = (st1 & (p2.d == p1.d + 1)) | (st2 & (p1.d == p2.d + 1));
-    // the character mechanics (ORX_EXT_RPG) keep the common path's rules:
-    // each attacker's own mana and damage, NPC hits and the kill credit in the
-    // drawn order, steps onto items; a descend-meet (whose clash would undo a
-    // step) takes the ordered tick
-    const bool rpg_ordered = ((c.ext & ORX_EXT_CHARACTER) && desc_meet) ||
-                             ((c.ext & ORX_EXT_README_COMBAT) && meet);
-    // an NPC standing on a staircase (left there when an Unused-despawned
-    // depth is regenerated with its staircase elsewhere) is attacked, not
-    // descended through: handle_move tests pos_lookup before the tile
-    // (updater.py:199-207), which the ordered tick follows literally
-    const bool npc_stair = (hit1 & st1) | (hit2 & st2);
-    const bool full0 =
-        (meet & (st1 | st2)) | (st1 & st2) | ext_ordered | rpg_ordered | npc_stair;
-    // the games that always use the initiative order: the ordered tick and a
-    // meet.  A descend into the other's depth uses it only when its spawn
-    // candidate is one of the other player's two cells (before and after its
-    // move): the descend branch draws it then (first_from_packed)
-    const bool ordered_use = in_progress & (full0 | meet);
-    uint32_t pk_shf = tb.a;
-    if (need == 0 && ordered_use) pk_shf = tick_block(key, game, ep, tick).a;
-    // all sixteen 2-bit shuffle fields rejected (high bits all set): the
-    // SHUFFLE stream fallback and its cap, in the ordered tick
-    const bool shf_reject = ordered_use & ((pk_shf | 0x55555555u) == 0xFFFFFFFFu);
-    const bool full = full0 | shf_reject;
-    took_ordered = in_progress & full;
-    const int32_t t0 = tick, ft = tick + 1;
-    const bool end = c.max_ticks && ft >= c.max_ticks;
-    if (!in_progress) {
-      if (c.autoreset) {  // the next episode (worldgen.py:77-87, 124-135)
-#ifdef ORX_STAMPS
-        ORX_COUNT(dl.n_reset);
-        ORX_CYC_BEGIN(cy1);
-#endif
-        ep += 1;
-        setup_game<NCAP, GRID>(c, key, game, ep, p1, p2, npc, tick, status);
-        items.clear();
-        if constexpr (NCAP > 0) {
-          if constexpr (NCAP == kDense) {
-            store_new_npcs(st, c, B, i, npc, true);  // health rows in HBM
-          } else {
-            store_new_npcs(st, c, B, i, npc, false);  // health: from hp at the end
-            hp.fill(c.npc_hp);
-          }
-        }
-        restarted = true;
-        sep = -1;
-#ifdef ORX_STAMPS
-        ORX_CYC_END(dl.cy_reset, cy1);
-#endif
-      }
-    } else if (full) {  // the ordered tick
-#ifdef ORX_STAMPS
-      ORX_COUNT(dl.n_ordered);
-      ORX_CYC_BEGIN(cy1);
-#endif
-      bool err = false;
-      const bool p1_first = first_from_packed(pk_shf, key, game, ep, t0, err);
-      Events<false> ev{nullptr, 0};
-      tick_game<NCAP, false, GRID>(c, key, game, ep, p1_first, p1, p2, npc, items, hp, tick,
-                                   status, err, dl, ev, sep);
-#ifdef ORX_STAMPS
-      ORX_CYC_END(dl.cy_ordered, cy1);
-#endif
-    } else {
-      // the common path's rules, then the one-sided events: a player that
-      // hits an NPC, descends or meets the other does not move freely
-      const bool lean = meet;
-      const bool s1 = !lean & !hit1 & !st1, s2 = !lean & !hit2 & !st2;
-      const int32_t x1o = p1.x, y1o = p1.y, x2o = p2.x, y2o = p2.y;  // for a descend-meet
-      p1.x = s1 ? t1x : p1.x;
-      p1.y = s1 ? t1y : p1.y;
-      p2.x = s2 ? t2x : p2.x;
-      p2.y = s2 ? t2y : p2.y;
-      tick = ft;
-      status = end ? ORX_TIE : ORX_IN_PROGRESS;
-      dl.eps += end ? 1 : 0;
-      bool desc_done = false;  // the descend's fast form below finished it
-      if constexpr (!GRID) {
-        if (!lean & (st1 | st2)) {
-#ifdef ORX_STAMPS
-          ORX_CYC_BEGIN(cyf);
-#endif
-          // One player descends, the common case of handle_descend
-          // (updater.py:259-296) on a keyed empty dungeon: the staircase from
-          // the first block of its (episode, depth, generation) stream, or
-          // the other player's when it stands on that depth; the spawn cell
-          // from the first word of the tick's SPAWN stream, taken when that
-          // word is accepted and the cell is neither of the other player's
-          // cells (before and after its move) -- then the initiative order
-          // cannot matter and no clash is possible -- and no NPC lives on the
-          // new depth.  Anything else falls through to the general form.
-          // Field-wise selects, both blocks drawn side by side.
-          const int32_t sd = st1 ? p1.d : p2.d, od = st1 ? p2.d : p1.d;
-          const int32_t o_start = st1 ? c.d2 : c.d1;
-          const int32_t nd = sd + 1;
-          bool present;
-          uint32_t gen = 0;
-          if (c.despawn == ORX_DESPAWN_UNREACHABLE) {
-            present = o_start <= nd && nd <= od;
-          } else {
-            present = od == nd;
-            gen = (!present && o_start <= nd && nd < od) ? 1u : 0u;
-          }
-          const bool other_on = od == nd;
-          W4 wd = philox(game, ep, (uint32_t)nd, tag(PUR_DUNGEON, gen), key);
-          W4 ws = philox(game, ep, (uint32_t)t0, tag(PUR_SPAWN, 0), key);
-          launder_w4(wd);
-          launder_w4(ws);
-          int32_t sx, sy;
-          bool ok = stair_from_block(c, wd, sx, sy);
-          const bool o_stairs = present & other_on;
-          sx = o_stairs ? (st1 ? p2.sx : p1.sx) : sx;
-          sy = o_stairs ? (st1 ? p2.sy : p1.sy) : sy;
-          ok |= o_stairs;
-          const uint32_t v = ws.a & c.ground.mask;
-          int32_t x, y;
-          ground_cell<false>(c, v, -1, sx, sy, x, y);
-          const int32_t ox = st1 ? p2.x : p1.x, oy = st1 ? p2.y : p1.y;      // after its move
-          const int32_t ox0 = st1 ? x2o : x1o, oy0 = st1 ? y2o : y1o;       // before it
-          const bool touch = other_on & (((x == ox) & (y == oy)) | ((x == ox0) & (y == oy0)));
-          const bool npc_depth = NCAP > 0 && nd == c.d1 && npc.any_alive();
-          ok = ok & (c.ground.rng != 0u) & (v <= c.ground.rng) & !touch & !npc_depth;
-          if (ok) {
-            p1.d = st1 ? nd : p1.d;
-            p1.x = st1 ? x : p1.x;
-            p1.y = st1 ? y : p1.y;
-            p1.sx = st1 ? sx : p1.sx;
-            p1.sy = st1 ? sy : p1.sy;
-            p2.d = st1 ? p2.d : nd;
-            p2.x = st1 ? p2.x : x;
-            p2.y = st1 ? p2.y : y;
-            p2.sx = st1 ? p2.sx : sx;
-            p2.sy = st1 ? p2.sy : sy;
-            dl.descend += 1;
-            dl.dungeon += present ? 0 : 1;
-            desc_done = true;
-#ifdef ORX_STAMPS
-            ORX_COUNT(dl.n_desc);
-#endif
-          }
-#ifdef ORX_STAMPS
-          ORX_CYC_END(dl.cy_desc, cyf);
-#endif
-        }
-      }
-      if (!lean & (st1 | st2) & !desc_done) {  // one player descends: the general form
-#ifdef ORX_STAMPS
-        ORX_COUNT(dl.n_desc);
-        ORX_CYC_BEGIN(cy1);
-#endif
-        PhiloxSrc src{key, game, ep};
-        auto spawn = src.spawn(t0);
-        Events<false> ev{nullptr, 0};
-        bool err = false;
-        Player S = pick(st1, p1, p2);
-        Player O = pick(st1, p2, p1);  // after its own move
-        // into the other's depth (desc_meet), the drawn order matters: moving
-        // first, the descender's spawn cell is tested against the other's
-        // cell before that player's move, which may then attack it
-        bool s_first = false;
-        if (desc_meet) {
-          const uint32_t pk = need > 0 ? pk_shf : tick_block(key, game, ep, t0).a;
-          s_first = first_from_packed(pk, key, game, ep, t0, err) == st1;
-        }
-        const int32_t ox0 = st1 ? x2o : x1o, oy0 = st1 ? y2o : y1o;
-        Player Ot = O;
-        Ot.x = s_first ? ox0 : O.x;
-        Ot.y = s_first ? oy0 : O.y;
-        descend<NCAP, false, GRID>(c, key, src, S, Ot, st1 ? c.d2 : c.d1, npc, spawn, dl, err,
-                                   st1 ? 1 : 2, ev);
-        const bool clash = s_first & ((O.x != ox0) | (O.y != oy0)) & (O.x == S.x) & (O.y == S.y);
-        O.x = clash ? ox0 : O.x;
-        O.y = clash ? oy0 : O.y;
-        S.hp -= (clash && c.player_dmg_net > 0) ? c.player_dmg_net : 0;
-        dl.combat += clash ? 1 : 0;
-        p1 = pick(st1, S, O);
-        p2 = pick(st1, O, S);
-        if (err) {  // an exhausted spawn stream stops the game (never observed)
-          dl.eps -= end ? 1 : 0;
-          status = ORX_STATUS_RNG_EXHAUSTED;
-        }
-        if (clash) deaths_over(p1, p2, end, status, dl);
-#ifdef ORX_STAMPS
-        ORX_CYC_END(dl.cy_desc, cy1);
-#endif
-      }
-      bool kc1 = false, kc2 = false;  // ORX_EXT_LEVELING: each player's kill this tick
-      if (NCAP > 0 && (hit1 | hit2)) {  // NPCs are swept after both moves
-#ifdef ORX_STAMPS
-        ORX_COUNT(dl.n_hits);
-#endif
-        Events<false> ev{nullptr, 0};
-        dl.combat += (hit1 ? 1 : 0) + (hit2 ? 1 : 0);
-        int32_t d1 = c.player_dmg_net > 0 ? c.player_dmg_net : 0, d2 = d1;
-        if (c.ext & ORX_EXT_RPG) {  // each attacker's own damage and mana
-          d1 = hit1 ? rpg_attack(c, p1) : 0;
-          d2 = hit2 ? rpg_attack(c, p2) : 0;
-        }
-        const int h1 = hit1 ? npc.find(k1) : -1, h2 = hit2 ? npc.find(k2) : -1;
-        if (c.ext & ORX_EXT_RPG) {
-          // hits in the drawn order: one NPC hit by both (a meet) credits the
-          // hit that takes it to zero
-          bool sw = false;
-          if (lean) {
-            const uint32_t sa = ~(pk_shf >> 1) & 0x55555555u;
-            sw = ((pk_shf >> __builtin_ctz(sa)) & 1u) == 0;
-          }
-          bool ka = false, kb = false;
-          npc_hits(c, npc, hp, sw ? h2 : h1, sw ? h1 : h2, sw ? d2 : d1, sw ? d1 : d2, dl, ev,
-                   ka, kb, sw ? k2 : k1, sw ? k1 : k2);
-          kc1 = sw ? kb : ka;
-          kc2 = sw ? ka : kb;
-          if ((c.ext & ORX_EXT_ITEMS) && kc1) drop_item(c, key, game, ep, t0, h1, k1, npc, items);
-          if ((c.ext & ORX_EXT_ITEMS) && kc2) drop_item(c, key, game, ep, t0, h2, k2, npc, items);
-        } else {
-          // two hits are then order-free: only the health left matters
-          npc_hits(c, npc, hp, h1, h2, d1, d2, dl, ev, kc1, kc2, k1, k2);
-        }
-      }
-      if (lean) {  // a meet: the two moves in the drawn order
-#ifdef ORX_STAMPS
-        ORX_COUNT(dl.n_meet);
-#endif
-        const uint32_t sa = ~(pk_shf >> 1) & 0x55555555u;  // nonzero: all-reject is ordered
-        const bool p1_first = ((pk_shf >> __builtin_ctz(sa)) & 1u) != 0;
-        const int32_t ax = p1_first ? t1x : t2x, ay = p1_first ? t1y : t2y;
-        const int32_t bx = p1_first ? t2x : t1x, by = p1_first ? t2y : t1y;
-        const int32_t fx0 = p1_first ? p1.x : p2.x, fy0 = p1_first ? p1.y : p2.y;
-        const int32_t sx0 = p1_first ? p2.x : p1.x, sy0 = p1_first ? p2.y : p1.y;
-        const bool hf = p1_first ? hit1 : hit2, hs = p1_first ? hit2 : hit1;
-        const bool occf = (ax == sx0) & (ay == sy0);
-        const int32_t fx = (occf | hf) ? fx0 : ax, fy = (occf | hf) ? fy0 : ay;
-        const bool occs = (bx == fx) & (by == fy);
-        const int32_t sx = (occs | hs) ? sx0 : bx, sy = (occs | hs) ? sy0 : by;
-        const int32_t dmg = c.player_dmg_net > 0 ? c.player_dmg_net : 0;
-        p1.x = p1_first ? fx : sx;
-        p1.y = p1_first ? fy : sy;
-        p2.x = p1_first ? sx : fx;
-        p2.y = p1_first ? sy : fy;
-        if (NCAP > 0 && (c.ext & ORX_EXT_ITEMS)) {  // the meet's steps onto items (a
-          // health item may save a player hit in the tick: before the win check)
-          if ((p1.d == c.d1) & ((p1.x != x1o) | (p1.y != y1o))) pick_up(c, p1, npc, items);
-          if ((p2.d == c.d1) & ((p2.x != x2o) | (p2.y != y2o))) pick_up(c, p2, npc, items);
-        }
-        if (c.ext & ORX_EXT_RPG) {  // each attacker's own damage and mana
-          const bool a1 = p1_first ? occf : occs, a2 = p1_first ? occs : occf;
-          const int32_t e1 = a1 ? rpg_attack(c, p1) : 0, e2 = a2 ? rpg_attack(c, p2) : 0;
-          p2.hp -= e1;
-          p1.hp -= e2;
-        } else {
-          p1.hp -= (p1_first ? occs : occf) ? dmg : 0;
-          p2.hp -= (p1_first ? occf : occs) ? dmg : 0;
-        }
-        dl.combat += (occf ? 1 : 0) + (occs ? 1 : 0);
-        deaths_over(p1, p2, end, status, dl);
-      }
-      // the sweep's experience after every combat of the tick: a player the
-      // other killed in a meet is not refilled
-      if (NCAP > 0 && (c.ext & ORX_EXT_LEVELING)) {
-        if (kc1) gain_xp(c, p1);
-        if (kc2) gain_xp(c, p2);
-      }
-      if (NCAP > 0 && (c.ext & ORX_EXT_ITEMS) && !lean) {  // a step onto an item takes it
-        // (readme.md:44; a meet's steps were taken above)
-        if (!st1 & (p1.d == c.d1) & ((p1.x != x1o) | (p1.y != y1o))) pick_up(c, p1, npc, items);
-        if (!st2 & (p2.d == c.d1) & ((p2.x != x2o) | (p2.y != y2o))) pick_up(c, p2, npc, items);
-      }
-    }
+    took_ordered = rare_tick<NCAP, GRID>(c, st, B, i, key, game, ep, p1, p2, npc, items, hp,
+                                         tick, status, dl, sep, restarted, tb, need, t1x,
+                                         t1y, t2x, t2y, ext_ordered);
 #ifdef ORX_STAMPS
     ORX_CYC_END(dl.cy_rare, cy0);
 #endif
@@ -2425,7 +2454,13 @@ constexpr int32_t kBufferDword3 = 0x00020000;  // gfx9 raw buffer, 32-bit elemen
 #define ORX_STREAM_AUX 2
 #endif
 constexpr int32_t kStreamAux = ORX_STREAM_AUX;  // cache policy: nt (measured)
-template <bool FAST>
+// ... for rows whose per-wave segments are whole 128-B lines.  Narrower
+// segments (fewer than 32 games per wave) are partial lines, which several
+// waves complete: there nt stores cost up to 2x (C5 at 8 games per wave: 165
+// us per launch with nt, 79 plain), so those launches store with the default
+// policy (kPartialAux)
+constexpr int32_t kPartialAux = 0;
+template <bool FAST, int AUX = kStreamAux>
 struct TrajWriter {
   int32_t* obs;
   int8_t* act;
@@ -2457,9 +2492,9 @@ struct TrajWriter {
                                                         kBufferDword3);
 #pragma unroll
       for (int f = 0; f < ORX_OBS_FIELDS; ++f)
-        __builtin_amdgcn_raw_buffer_store_b32(vals[f], ro, (int32_t)vo[f], 0, kStreamAux);
+        __builtin_amdgcn_raw_buffer_store_b32(vals[f], ro, (int32_t)vo[f], 0, AUX);
       const auto ra = __builtin_amdgcn_make_buffer_rsrc(act, 0, (int32_t)(B * 2u), kBufferDword3);
-      __builtin_amdgcn_raw_buffer_store_b16(pack_actions(a1, a2), ra, (int32_t)va, 0, kStreamAux);
+      __builtin_amdgcn_raw_buffer_store_b16(pack_actions(a1, a2), ra, (int32_t)va, 0, AUX);
       obs += (size_t)ORX_OBS_FIELDS * B;
       act += (size_t)2 * B;
     } else {
@@ -2483,7 +2518,7 @@ struct TrajWriter {
 // "enemies + items": mana, experience and items, heal optional).  The
 // specialized forms carry no per-tick uniform branches on policy codes or
 // pointers and write the trajectory with buffer stores.
-template <int NCAP, int PM, bool GRID>
+template <int NCAP, int PM, bool GRID, int AUX = kStreamAux>
 __global__ void __launch_bounds__(kRolloutBlock) rollout_kernel(orx_cfg_t hc, orx_state_t st,
                                                                 int32_t pol1_,
                                                       int32_t pol2_, int32_t n_ticks,
@@ -2555,7 +2590,7 @@ __global__ void __launch_bounds__(kRolloutBlock) rollout_kernel(orx_cfg_t hc, or
   Deltas dl = {0, 0, 0, 0, 0, 0};
   int32_t sep = (c.ext & ORX_EXT_SEPARATION_DAMAGE) ? st.sep_start[i] : -1;
   bool restarted = false;
-  TrajWriter<kTraj> traj(obs, act, B, i);
+  TrajWriter<kTraj, AUX> traj(obs, act, B, i);
 #ifdef ORX_STAMPS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
@@ -2584,6 +2619,315 @@ __global__ void __launch_bounds__(kRolloutBlock) rollout_kernel(orx_cfg_t hc, or
       if (restarted || dl.combat) hp.store(st.npc_health, c.K, B, i);
   }
   flush_deltas(st, B, i, dl);
+#ifdef ORX_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+  ORX_STAMP(4);
+#ifdef ORX_STAMPS
+  uint32_t r[10] = {dl.n_rare, dl.n_ordered, dl.n_hits, dl.n_desc, dl.n_meet, dl.n_reset,
+                    dl.cy_rare, dl.cy_reset, dl.cy_ordered, dl.cy_desc};
+#pragma unroll
+  for (int j = 0; j < 10; ++j)
+    for (int o = 32; o > 0; o >>= 1) r[j] += __shfl_xor(r[j], o);
+  if ((threadIdx.x & 63) == 0) {
+    const size_t w = (size_t)((blockIdx.x * blockDim.x + threadIdx.x) >> 6) * 16;
+#pragma unroll
+    for (int j = 0; j < 10; ++j) g_stamps[w + 5 + j] = r[j];
+  }
+#endif
+}
+
+// ---------------------------------------------------------------------------
+// Paired rollout: two lanes per game
+// ---------------------------------------------------------------------------
+// A batch too small to fill the chip runs at most 32 games per wave (lanes =
+// orx_rollout_lanes < 64), and a lone wave per SIMD pays per instruction, not
+// per lane (a wave whose exec mask lies in its low 32 lanes issues each VALU
+// instruction in one pass: DESIGN.md s7).  Without NPCs and dungeon banks
+// (C5's StaircaseBots, C2's RandomBots) those idle lanes take the second
+// player: lane 2j is player 1 of game j, lane 2j+1 its player 2, so the
+// per-player half of the tick -- the bot's move, the target and its clamp,
+// the staircase test, the common move, and half of the observation row's
+// stores -- is ONE instruction stream for both players.  The pair exchanges
+// the other player's cell, depth and target through DPP (quad_perm
+// [1,0,3,2]: one VALU op each) for the meet test, which is symmetric, so both
+// lanes reach the same decision.  A rare tick rebuilds the game's two Player
+// records in BOTH lanes and runs rollout_tick's scalar rare block (rare_tick)
+// redundantly -- the same instructions in two lanes cost what one lane costs
+// -- so every rare case keeps the single-lane form's exact semantics; each
+// lane then keeps its own player.  Game-level state (tick, status, episode,
+// separation timer, counters) is identical in both lanes; lane 2j writes it.
+__device__ __forceinline__ int32_t pair_swap(int32_t v) {
+  return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);  // quad_perm [1, 0, 3, 2]
+}
+
+// One tick's trajectory rows from a pair of lanes: each lane stores its own
+// player's x, y, depth, health and staircase (rows f and f + 4, 10/11 and
+// 12/13), lane 2j the tick and lane 2j+1 the status (rows 8 and 9), and its
+// own action byte: 7 dword stores and one byte store per tick, each covering
+// two rows, instead of 14 and a 16-bit store.
+template <int AUX>
+struct PairWriter {
+  int32_t* obs;
+  int8_t* act;
+  uint32_t B;
+  uint32_t vo[7], va;
+  __device__ __forceinline__ PairWriter(int32_t* o, int8_t* a, uint32_t B_, uint32_t i,
+                                        uint32_t who)
+      : obs(o), act(a), B(B_) {
+    const uint32_t rows[7] = {0u + 4u * who, 1u + 4u * who, 2u + 4u * who, 3u + 4u * who,
+                              (uint32_t)ORX_OBS_TICK + who, (uint32_t)ORX_OBS_P1_STAIR_X + 2u * who,
+                              (uint32_t)ORX_OBS_P1_STAIR_Y + 2u * who};
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      vo[k] = (rows[k] * B + i) * 4u;
+      asm volatile("" : "+v"(vo[k]));
+    }
+    va = 2u * i + who;
+    asm volatile("" : "+v"(va));
+  }
+  __device__ __forceinline__ void write(const Player& me, int32_t ts, int32_t move) {
+    const int32_t vals[7] = {me.x, me.y, me.d, me.hp, ts, me.sx, me.sy};
+    const auto ro = __builtin_amdgcn_make_buffer_rsrc(obs, 0, (int32_t)(ORX_OBS_FIELDS * B * 4u),
+                                                      kBufferDword3);
+#pragma unroll
+    for (int k = 0; k < 7; ++k)
+      __builtin_amdgcn_raw_buffer_store_b32(vals[k], ro, (int32_t)vo[k], 0, AUX);
+    const auto ra = __builtin_amdgcn_make_buffer_rsrc(act, 0, (int32_t)(B * 2u), kBufferDword3);
+    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)move, ra, (int32_t)va, 0, AUX);
+    obs += (size_t)ORX_OBS_FIELDS * B;
+    act += (size_t)2 * B;
+  }
+};
+
+// PM 1: both players RandomBot (no extension flags); PM 2: both StaircaseBot
+// (at most separation damage).  NCAP 0, empty dungeons, obs and act given.
+template <int PM, int AUX>
+__global__ void __launch_bounds__(kRolloutBlock) pair_rollout_kernel(orx_cfg_t hc, orx_state_t st,
+                                                                     int32_t n_ticks,
+                                                                     int32_t* __restrict__ obs,
+                                                                     int8_t* __restrict__ act,
+                                                                     uint32_t B, Key key,
+                                                                     uint32_t off, uint32_t lanes) {
+  const uint32_t lane = threadIdx.x & 63u;
+  if (lane >= 2u * lanes) return;  // uniform per wave
+  const uint32_t i = ((blockIdx.x * blockDim.x + threadIdx.x) >> 6) * lanes + (lane >> 1);
+  if (i >= B) return;              // both lanes of a game together
+  const uint32_t who = lane & 1u;  // 0: player 1, 1: player 2
+  const bool isB = who != 0u;
+  Cfg c = make_cfg(hc, st);
+  if (PM == 1) c.ext = 0;
+  if (PM == 2) c.ext &= ORX_EXT_SEPARATION_DAMAGE;
+  const uint32_t game = off + i;
+  ORX_STAMP(0);
+  Player me;
+  me.x = st.p_x[who * B + i];
+  me.y = st.p_y[who * B + i];
+  me.d = st.p_depth[who * B + i];
+  me.hp = st.p_health[who * B + i];
+  me.sx = st.st_x[who * B + i];
+  me.sy = st.st_y[who * B + i];
+  me.lay = -1;
+  me.move = ORX_MOVE_STAY;
+  me.tx = me.ty = 0;
+  me.mana = me.xp = me.dmg = me.mhp = me.nitems = me.cool = me.heal = me.hd = 0;
+  int32_t tick = st.tick[i];
+  int32_t status = st.status[i];
+  uint32_t ep = (uint32_t)st.episode[i];
+  int32_t sep = (c.ext & ORX_EXT_SEPARATION_DAMAGE) ? st.sep_start[i] : -1;
+  Npcs<0> npc;
+  npc.clear();
+  Items<0> items;
+  items.clear();
+  NpcHpRegs<0> hp;
+  Deltas dl = {0, 0, 0, 0, 0, 0};
+  bool restarted = false;
+  constexpr int need = PM == 1 ? 2 : 0;
+  PairWriter<AUX> traj(obs, act, B, i, who);
+#ifdef ORX_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+  ORX_STAMP(1);
+  int32_t t = 0;
+  do {
+    // the bot's move (randombot.py:20-21 / staircasebot.py:9-21)
+    W4 tb = {0u, 0u, 0u, 0u};
+    int32_t move;
+    if constexpr (PM == 1) {
+      // the tick block in both lanes; player 1 takes the first accepted 3-bit
+      // field of word b, player 2 the second (as rollout_tick)
+      tb = tick_block(key, game, ep, tick);
+      const uint32_t acc = accepted3(tb.b);
+      const uint32_t acc2 = acc & (acc - 1u);
+      move = (int32_t)((tb.b >> (ffbl(isB ? acc2 : acc) & 31u)) & 7u) + 1;
+      if (ORX_UNLIKELY(acc2 == 0u)) {  // the game's word b holds fewer than two
+        int32_t r0 = ORX_MOVE_STAY, r1 = ORX_MOVE_STAY;
+        bool err = false;
+        moves_from_block(tb, 2, key, game, ep, tick, r0, r1, err);
+        move = isB ? r1 : r0;
+      }
+    } else {
+      const int32_t dx = me.sx - me.x, dy = me.sy - me.y;
+      const int32_t adx = dx < 0 ? -dx : dx, ady = dy < 0 ? -dy : dy;
+      move = adx > ady ? (dx > 0 ? ORX_MOVE_RIGHT : ORX_MOVE_LEFT)
+                       : (dy > 0 ? ORX_MOVE_DOWN : ORX_MOVE_UP);
+    }
+    me.move = move;
+    const bool in_progress = status == ORX_IN_PROGRESS;
+    // effective target (own cell when blocked: the border, clamped)
+    int32_t tx, ty;
+    calc_pos(me.x, me.y, move, tx, ty);
+    tx = med3_i32(tx, 1, c.W - 2);
+    ty = med3_i32(ty, 1, c.H - 2);
+    // the other player of the pair
+    const int32_t ox = pair_swap(me.x), oy = pair_swap(me.y), od = pair_swap(me.d);
+    const int32_t otx = pair_swap(tx), oty = pair_swap(ty);
+    const bool st_me = (tx == me.sx) & (ty == me.sy);
+    const int32_t st_o = pair_swap(st_me ? 1 : 0);
+    const uint32_t e_mo = (uint32_t)(tx ^ ox) | (uint32_t)(ty ^ oy);
+    const uint32_t e_om = (uint32_t)(otx ^ me.x) | (uint32_t)(oty ^ me.y);
+    const uint32_t e_tt = (uint32_t)(tx ^ otx) | (uint32_t)(ty ^ oty);
+    const bool meet = ((uint32_t)(me.d ^ od) | min(e_mo, min(e_om, e_tt))) == 0u;
+    const bool rare = !in_progress | meet | st_me | (st_o != 0);
+    const int32_t ft = tick + 1;
+    const bool end = c.max_ticks && ft >= c.max_ticks;
+    bool took_ordered = false;
+    if (ORX_UNLIKELY(rare)) {
+#ifdef ORX_STAMPS
+      ORX_COUNT(dl.n_rare);
+      ORX_CYC_BEGIN(cy0);
+#endif
+      // One player descends (C5's common rare tick; StaircaseBots only),
+      // fast_descend's rules split over the pair: the descender's lane draws the tick's SPAWN
+      // block, the other lane the new depth's DUNGEON block -- one Philox
+      // instruction stream for both -- and the lanes swap them.
+      bool fast = false;
+      const int32_t osx = pair_swap(me.sx), osy = pair_swap(me.sy);
+      if (PM == 2 && (in_progress & !meet & (st_me != (st_o != 0)))) {
+#ifdef ORX_STAMPS
+        ORX_CYC_BEGIN(cyf);
+#endif
+        const bool dIsB = st_me ? isB : !isB;       // the descender is player 2
+        const int32_t sd = st_me ? me.d : od, odep = st_me ? od : me.d;
+        const int32_t o_start = dIsB ? c.d1 : c.d2;
+        const int32_t nd = sd + 1;
+        bool present;
+        uint32_t gen = 0;
+        if (c.despawn == ORX_DESPAWN_UNREACHABLE) {
+          present = o_start <= nd && nd <= odep;
+        } else {
+          present = odep == nd;
+          gen = (!present && o_start <= nd && nd < odep) ? 1u : 0u;
+        }
+        const bool other_on = odep == nd;
+        W4 w = philox(game, ep, st_me ? (uint32_t)tick : (uint32_t)nd,
+                      st_me ? tag(PUR_SPAWN, 0) : tag(PUR_DUNGEON, gen), key);
+        const W4 wo = {(uint32_t)pair_swap((int32_t)w.a), (uint32_t)pair_swap((int32_t)w.b),
+                       (uint32_t)pair_swap((int32_t)w.c), (uint32_t)pair_swap((int32_t)w.d)};
+        const W4 ws = st_me ? w : wo, wd = st_me ? wo : w;
+        int32_t sx, sy;
+        bool ok = stair_from_block(c, wd, sx, sy);
+        const bool o_stairs = present & other_on;
+        sx = o_stairs ? (st_me ? osx : me.sx) : sx;  // the other player's staircase
+        sy = o_stairs ? (st_me ? osy : me.sy) : sy;
+        ok |= o_stairs;
+        const uint32_t v = ws.a & c.ground.mask;
+        int32_t x, y;
+        ground_cell<false>(c, v, -1, sx, sy, x, y);
+        // the other player's cell before and after its move
+        const int32_t ox0 = st_me ? ox : me.x, oy0 = st_me ? oy : me.y;
+        const int32_t ox1 = st_me ? otx : tx, oy1 = st_me ? oty : ty;
+        const bool touch = other_on & (((x == ox1) & (y == oy1)) | ((x == ox0) & (y == oy0)));
+        ok = ok & (c.ground.rng != 0u) & (v <= c.ground.rng) & !touch;
+        if (ok) {
+          me.d = st_me ? nd : me.d;
+          me.x = st_me ? x : tx;
+          me.y = st_me ? y : ty;
+          me.sx = st_me ? sx : me.sx;
+          me.sy = st_me ? sy : me.sy;
+          dl.descend += 1;
+          dl.dungeon += present ? 0 : 1;
+          dl.eps += end ? 1 : 0;
+          tick = ft;
+          status = end ? ORX_TIE : ORX_IN_PROGRESS;
+          fast = true;
+#ifdef ORX_STAMPS
+          ORX_COUNT(dl.n_desc);
+#endif
+        }
+#ifdef ORX_STAMPS
+        ORX_CYC_END(dl.cy_desc, cyf);
+#endif
+      }
+      if (!fast) {
+        // both lanes rebuild the game's players and run the scalar rare block
+        Player o = me;
+        o.x = ox;
+        o.y = oy;
+        o.d = od;
+        o.hp = pair_swap(me.hp);
+        o.sx = osx;
+        o.sy = osy;
+        o.move = pair_swap(move);
+        Player p1 = pick(isB, o, me), p2 = pick(isB, me, o);
+        took_ordered = rare_tick<0, false>(c, st, B, i, key, game, ep, p1, p2, npc, items, hp,
+                                          tick, status, dl, sep, restarted, tb, need,
+                                          isB ? otx : tx, isB ? oty : ty, isB ? tx : otx,
+                                          isB ? ty : oty, false);
+        me = pick(isB, p2, p1);
+        me.move = move;
+      }
+#ifdef ORX_STAMPS
+      ORX_CYC_END(dl.cy_rare, cy0);
+#endif
+    }
+    // the common tick: the move to the effective target
+    me.x = rare ? me.x : tx;
+    me.y = rare ? me.y : ty;
+    dl.eps += (!rare & end) ? 1 : 0;
+    status = rare ? status : (end ? ORX_TIE : ORX_IN_PROGRESS);
+    tick = rare ? tick : ft;
+    if (c.ext & ORX_EXT_SEPARATION_DAMAGE) {  // as rollout_tick (readme.md:46-47)
+      const bool base = in_progress & !took_ordered;
+      const int32_t od2 = pair_swap(me.d);
+      if (base) {
+        if (me.d != od2) {
+          const int32_t t0 = ft - 1;
+          if (sep < 0) sep = t0;
+          const int32_t k = t0 - sep + 1;
+          const int32_t dmg = (k + c.sep_period - 1) / c.sep_period;
+          me.hp -= me.d < od2 ? dmg : 0;
+          const int32_t ohp = pair_swap(me.hp);
+          const bool d1 = (isB ? ohp : me.hp) <= 0, d2 = (isB ? me.hp : ohp) <= 0;
+          if ((d1 | d2) && status != ORX_STATUS_RNG_EXHAUSTED) {  // deaths_over
+            const int32_t s = d1 ? (d2 ? ORX_TIE : ORX_PLAYER2_WIN) : ORX_PLAYER1_WIN;
+            dl.eps += end ? 0 : 1;
+            dl.ret += (s == ORX_PLAYER1_WIN ? 1 : 0) - (s == ORX_PLAYER2_WIN ? 1 : 0);
+            status = s;
+          }
+        } else {
+          sep = -1;
+        }
+      }
+    }
+    if (!(ORX_DIAG & 16)) traj.write(me, isB ? status : tick, move);
+  } while (++t < n_ticks);
+  ORX_STAMP(3);
+  st.p_x[who * B + i] = me.x;
+  st.p_y[who * B + i] = me.y;
+  st.p_depth[who * B + i] = me.d;
+  st.p_health[who * B + i] = me.hp;
+  if (restarted || dl.descend != 0) {
+    st.st_x[who * B + i] = me.sx;
+    st.st_y[who * B + i] = me.sy;
+  }
+  if (!isB) {
+    st.tick[i] = tick;
+    st.status[i] = status;
+    st.episode[i] = (int32_t)ep;
+    if (c.ext & ORX_EXT_SEPARATION_DAMAGE) st.sep_start[i] = sep;
+    flush_deltas(st, B, i, dl);
+  }
 #ifdef ORX_STAMPS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
@@ -3060,6 +3404,11 @@ uint32_t device_lds_per_block() {
   return (uint32_t)n;
 }
 
+bool paired_enabled() {  // read per launch (ORX_ROLLOUT_PAIRED=0: the one-lane form)
+  const char* e = getenv("ORX_ROLLOUT_PAIRED");
+  return !(e && e[0] == '0');
+}
+
 int lanes_override() {  // read per launch, so a sweep can change it in-process
   const char* e = getenv("ORX_ROLLOUT_LANES");
   const int x = e ? atoi(e) : 0;
@@ -3085,6 +3434,52 @@ uint32_t rollout_lanes(uint32_t B) {
   return L;
 }
 
+// The policy mode (rollout_kernel's PM) of an orx_rollout launch: the
+// buffer-addressed trajectory forms need both buffers and one tick's obs rows
+// below 2 GiB.
+int rollout_pm(const orx_cfg_t* cfg, int32_t p1, int32_t p2, uint32_t B, bool traj) {
+  const bool traj_fast = traj && (uint64_t)B * ORX_OBS_FIELDS * 4u < (1ull << 31);
+  const bool both_random = p1 == ORX_POLICY_RANDOM && p2 == ORX_POLICY_RANDOM;
+  return !traj_fast ? 0
+         : (cfg->flags == 0 && both_random) ? 1
+         : ((cfg->flags & ~ORX_EXT_SEPARATION_DAMAGE) == 0 && p1 == ORX_POLICY_STAIRCASE &&
+            p2 == ORX_POLICY_STAIRCASE) ? 2
+         : ((cfg->flags | ORX_EXT_HEAL) == ORX_EXT_RPG && both_random) ? 3
+         : 0;
+}
+
+// The form, games per wave and store policy of an orx_rollout launch.
+struct RolloutPlan {
+  bool paired;     // pair_rollout_kernel: two lanes per game
+  uint32_t lanes;  // games per wave
+  bool nt;         // nontemporal trajectory stores (whole-line row segments)
+};
+
+// The paired form: no NPCs, no bank, the RandomBot or StaircaseBot trajectory
+// forms (PM 1 / 2), for batches the one-lane rule leaves below 64 games per
+// wave; its games per wave: two waves per SIMD until the wave holds 32
+// games, at least 8 (C5's 8-GPU share, 16,384 games: 8 per wave, 79 us per
+// launch against 89 at 16 and 112 at 32; C2 at 4,096: 50 against 51).
+// ORX_ROLLOUT_LANES (games per wave) and ORX_ROLLOUT_PAIRED=0 override.
+RolloutPlan plan_rollout(const orx_cfg_t* cfg, int pm, uint32_t B) {
+  RolloutPlan p;
+  p.lanes = rollout_lanes(B);
+  p.paired = ncap_for(cfg->n_npcs) == 0 && cfg->n_layouts == 0 && (pm == 1 || pm == 2) &&
+             p.lanes <= 32u && paired_enabled();
+  if (p.paired) {
+    if (const int o = lanes_override()) {
+      p.lanes = o < 32 ? (uint32_t)o : 32u;
+    } else {
+      const uint64_t simds = (uint64_t)device_simds();
+      uint32_t L = 32;
+      while (L > 8 && (uint64_t)B < 2 * simds * L) L >>= 1;
+      p.lanes = L;
+    }
+  }
+  p.nt = p.lanes * 4u >= 128u;  // a wave's row segment is a whole line
+  return p;
+}
+
 }  // namespace
 
 extern "C" {
@@ -3102,6 +3497,28 @@ int orx_rollout_lanes(int64_t n_games) {
 }
 
 const char* orx_last_error(void) { return g_err; }
+
+int orx_rollout_shape(const orx_cfg_t* cfg, int32_t policy_p1, int32_t policy_p2,
+                      int64_t n_games, int32_t trajectory, orx_rollout_shape_t* out) {
+  int r;
+  if ((r = check_cfg(cfg)) || (r = check_policy(policy_p1)) || (r = check_policy(policy_p2)))
+    return r;
+  if (n_games <= 0 || n_games > 0x7FFFFFFFLL) return fail(ORX_EINVAL, "bad n_games");
+  if (!out) return fail(ORX_EINVAL, "out is NULL");
+  const uint32_t B = (uint32_t)n_games;
+  if (cfg->rng == ORX_RNG_MT19937) {  // mt_rollout_kernel: one game per lane, full waves
+    out->games_per_wave = 64;
+    out->lanes_per_game = 1;
+    out->nontemporal = 1;
+    return ORX_OK;
+  }
+  const int pm = rollout_pm(cfg, policy_p1, policy_p2, B, trajectory != 0);
+  const RolloutPlan p = plan_rollout(cfg, pm, B);
+  out->games_per_wave = (int32_t)p.lanes;
+  out->lanes_per_game = p.paired ? 2 : 1;
+  out->nontemporal = (pm != 0 && !p.nt) ? 0 : 1;
+  return ORX_OK;
+}
 
 int orx_dstore_depths(const orx_cfg_t* cfg) {
   if (const int r = check_cfg(cfg)) return r;
@@ -3258,17 +3675,12 @@ int orx_rollout(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p1, 
 #undef ORX_ROLLOUT
     return launch_status("orx_rollout");
   }
-  const bool traj_fast = obs && act && (uint64_t)B * ORX_OBS_FIELDS * 4u < (1ull << 31);
-  const bool both_random = policy_p1 == ORX_POLICY_RANDOM && policy_p2 == ORX_POLICY_RANDOM;
-  const int pm = !traj_fast ? 0
-                 : (cfg->flags == 0 && both_random) ? 1
-                 : ((cfg->flags & ~ORX_EXT_SEPARATION_DAMAGE) == 0 &&
-                    policy_p1 == ORX_POLICY_STAIRCASE && policy_p2 == ORX_POLICY_STAIRCASE) ? 2
-                 : ((cfg->flags | ORX_EXT_HEAL) == ORX_EXT_RPG && both_random) ? 3
-                 : 0;
-  const uint32_t lanes = rollout_lanes(B);
+  const int pm = rollout_pm(cfg, policy_p1, policy_p2, B, obs && act);
+  const RolloutPlan plan = plan_rollout(cfg, pm, B);
+  const uint32_t lanes = plan.lanes;
   const uint32_t threads = rollout_threads(B, lanes);
   const uint32_t per_block = threads / 64u * lanes;
+  const bool nt = plan.nt;
   // dynamic LDS: the bank's tiles when they fit (rollout_kernel stages them)
   const uint64_t tiles = grid ? (uint64_t)cfg->n_layouts * (uint64_t)(cfg->width * cfg->height) : 0;
   const bool use_lds = tiles && tiles <= kMaxLdsTiles && !getenv("ORX_NO_LDS_TILES");
@@ -3288,20 +3700,38 @@ int orx_rollout(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p1, 
       lds += per_block * bb;
     }
   }
-#define ORX_ROLLOUT(N, P, G)                                                                    \
-  if (nc == N && pm == P && grid == G) {                                                        \
+  // the paired form (two lanes per game, pair_rollout_kernel): no NPCs, no
+  // bank, the RandomBot or StaircaseBot trajectory forms, at most 32 games
+  // per wave (env ORX_ROLLOUT_PAIRED=0 turns it off, for measurements)
+  if (plan.paired) {
+    const dim3 blocks((B + per_block - 1) / per_block);
+#define ORX_PAIR(P, A)                                                                          \
+    if (pm == P && (A == kStreamAux) == nt)                                                     \
+      hipLaunchKernelGGL((pair_rollout_kernel<P, A>), blocks, dim3(threads), 0, s, *cfg, *st,    \
+                         n_ticks, obs, act, B, k, off, lanes);
+    ORX_PAIR(1, kStreamAux) ORX_PAIR(1, kPartialAux) ORX_PAIR(2, kStreamAux) ORX_PAIR(2, kPartialAux)
+#undef ORX_PAIR
+    return launch_status("orx_rollout");
+  }
+#define ORX_ROLLOUT_A(N, P, G, A)                                                               \
+  if (nc == N && pm == P && grid == G && (P == 0 || (A == kStreamAux) == nt)) {                \
     if (lds > 65536u &&                                                                         \
-        hipFuncSetAttribute(reinterpret_cast<const void*>(&rollout_kernel<N, P, G>),            \
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&rollout_kernel<N, P, G, A>),         \
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) { \
       (void)hipGetLastError();                                                                  \
       if (lds_bits) { lds -= per_block * lds_bits; lds_bits = 0; }                              \
       if (lds > 65536u) return fail(ORX_EIO, "orx_rollout: cannot raise the LDS limit");        \
     }                                                                                           \
-    hipLaunchKernelGGL((rollout_kernel<N, P, G>), dim3((B + per_block - 1) / per_block),        \
+    hipLaunchKernelGGL((rollout_kernel<N, P, G, A>), dim3((B + per_block - 1) / per_block),     \
                        dim3(threads), lds, s, *cfg, *st,                                        \
                        policy_p1, policy_p2, n_ticks, obs, act, B, k, off, lanes, lds_n,        \
                        lds_bits);                                                               \
+    return launch_status("orx_rollout");                                                        \
   }
+// the buffer-store forms in both store policies; the generic form (PM 0) in one
+#define ORX_ROLLOUT(N, P, G)                                                                    \
+  ORX_ROLLOUT_A(N, P, G, kStreamAux)                                                            \
+  if (P != 0) { ORX_ROLLOUT_A(N, P, G, kPartialAux) }
   ORX_ROLLOUT(0, 0, false) ORX_ROLLOUT(0, 1, false) ORX_ROLLOUT(0, 2, false)
   ORX_ROLLOUT(8, 0, false) ORX_ROLLOUT(8, 1, false) ORX_ROLLOUT(8, 2, false)
   ORX_ROLLOUT(16, 0, false) ORX_ROLLOUT(16, 1, false) ORX_ROLLOUT(16, 2, false)

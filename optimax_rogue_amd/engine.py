@@ -157,8 +157,21 @@ class BatchedEngine:
         return launch
 
     def rollout_lanes(self) -> int:
-        """Games per wave of this batch's rollout launches (orx_rollout_lanes)."""
+        """Games per wave of this batch's one-lane rollout launches
+        (orx_rollout_lanes); rollout_shape() gives the launch's actual form."""
         return int(self.lib.orx_rollout_lanes(self.B))
+
+    def rollout_shape(self, p1: int = Policy.Random, p2: int = Policy.Random,
+                      trajectory: bool = True) -> dict:
+        """The shape orx_rollout launches these arguments with
+        (orx_rollout_shape): games per wave, lanes per game (2 = the paired
+        form), nontemporal trajectory stores."""
+        out = _lib.OrxRolloutShape()
+        code = self.lib.orx_rollout_shape(self._pcfg, int(p1), int(p2), self.B, int(trajectory),
+                                          ctypes.byref(out))
+        _lib.check("orx_rollout_shape", code)
+        return {"games_per_wave": out.games_per_wave, "lanes_per_game": out.lanes_per_game,
+                "nontemporal": bool(out.nontemporal)}
 
     # -- the C-ABI entry points -------------------------------------------
     def seed_rng(self, seed: Optional[int] = None) -> None:

@@ -39,7 +39,8 @@ def test_library_exports_every_declared_symbol(lib):
     assert decl == sorted(["orx_abi_version", "orx_last_error", "orx_validate_cfg", "orx_reset",
                            "orx_step", "orx_step_events", "orx_policy", "orx_rollout",
                            "orx_dungeon_stairs", "orx_dungeon_spawn", "orx_seed_mt",
-                           "orx_build_id", "orx_rollout_lanes", "orx_dstore_depths"])
+                           "orx_build_id", "orx_rollout_lanes", "orx_dstore_depths",
+                           "orx_rollout_shape"])
     from optimax_rogue_amd import _lib
     assert sorted(_lib.EXPORTS) == decl
     for name in decl:
@@ -76,6 +77,8 @@ def test_struct_layouts_match_header():
     from oracle.oracle import CFG_FIELDS as ORACLE_FIELDS
     assert list(CFG_FIELDS) == struct_fields("orx_cfg") == list(ORACLE_FIELDS)
     assert [f for f, _ in OrxState._fields_] == struct_fields("orx_state")
+    from optimax_rogue_amd._lib import OrxRolloutShape
+    assert [f for f, _ in OrxRolloutShape._fields_] == struct_fields("orx_rollout_shape")
     assert ctypes.sizeof(OrxCfg) == 4 * len(CFG_FIELDS)
     assert ctypes.sizeof(OrxState) == 8 * len(OrxState._fields_)
 
@@ -151,3 +154,31 @@ def test_engine_refuses_cpu():
     from optimax_rogue_amd.engine import BatchedEngine
     with pytest.raises(RuntimeError):
         BatchedEngine(EnvConfig(), 8, device=torch.device("cpu"))
+
+
+def test_rollout_shape_rules(lib):
+    """orx_rollout_shape (no device work; 1,024 SIMDs assumed without a GPU):
+    the paired two-lanes-per-game form for NPC-free RandomBot / StaircaseBot
+    trajectory launches below 64 games per wave, nontemporal stores only for
+    whole-line row segments (32+ games per wave)."""
+    from optimax_rogue_amd import EnvConfig
+    from optimax_rogue_amd._lib import OrxRolloutShape
+
+    def shape(cfg, B, p1=1, p2=1, traj=1):
+        out = OrxRolloutShape()
+        assert lib.orx_rollout_shape(ctypes.byref(cfg.to_c()), p1, p2, B, traj,
+                                     ctypes.byref(out)) == 0
+        return out.games_per_wave, out.lanes_per_game, out.nontemporal
+
+    assert shape(EnvConfig.c5(), 16384, 2, 2) == (8, 2, 0)       # C5's 8-GPU share
+    assert shape(EnvConfig.c2(), 4096) == (8, 2, 0)               # C2
+    assert shape(EnvConfig.c5(), 32768, 2, 2) == (16, 2, 0)
+    assert shape(EnvConfig.c5(), 131072, 2, 2) == (64, 1, 1)      # full waves: one lane per game
+    assert shape(EnvConfig.c3(), 32768) == (32, 1, 1)             # the bench's stream shard
+    assert shape(EnvConfig.c3(), 65536) == (64, 1, 1)
+    assert shape(EnvConfig.c3(), 16384) == (16, 1, 0)             # NPCs: one lane per game
+    assert shape(EnvConfig.c5(), 16384, 2, 1) == (16, 1, 1)       # mixed bots: the generic form
+    assert shape(EnvConfig.c2(), 4096, traj=0) == (16, 1, 1)      # no trajectory buffers
+    bad = OrxRolloutShape()
+    assert lib.orx_rollout_shape(ctypes.byref(EnvConfig.c2().to_c()), 9, 1, 64, 1,
+                                 ctypes.byref(bad)) == -22
