@@ -76,11 +76,17 @@ def bytes_per_game(kernel: str, K: int, ticks: int = 1) -> int:
     return ticks * (OBS_BYTES + ACT_BYTES) + state_in + state_out
 
 
-def rollout_kernel_name(B: int, K: int) -> str:
-    """The kernel orx_rollout launches for this workload: rollout_kernel with
-    the RandomBot + trajectory specialization (PM=1), NPC capacity 0/8/16."""
+def rollout_kernel_name(K: int, shape: dict) -> str:
+    """The kernel orx_rollout launches for this workload, as rocprofv3 names
+    it: the RandomBot + trajectory specialization (PM=1), NPC capacity
+    0/8/16, in the form orx_rollout_shape reports -- pair_rollout_kernel (two
+    lanes per game) or rollout_kernel -- with its store policy (AUX 2 =
+    nontemporal, 0 = default)."""
     ncap = 0 if K == 0 else 8 if K <= 8 else 16
-    return f"rollout_kernel<{ncap}, 1, false>"
+    aux = 2 if shape["nontemporal"] else 0
+    if shape["lanes_per_game"] == 2:
+        return f"pair_rollout_kernel<{ncap}, 1, {aux}>"
+    return f"rollout_kernel<{ncap}, 1, false, {aux}>"
 
 
 def _cpu_model() -> str:
@@ -414,7 +420,8 @@ def main():
     materialized = bytes_per_game("rollout", cfg.n_npcs, chunk) * B
     achieved_gbs = materialized / avg_launch_s / 1e9
     contract_bytes = contract_bytes_per_env_step(cfg.n_npcs) * B * chunk
-    lanes = eng.rollout_lanes()
+    shape = eng.rollout_shape(1, 1)   # the 2x RandomBot trajectory launches timed above
+    lanes = shape["games_per_wave"]
     eng_parts = list(eng.parts)
 
     # the only collective: all-gather of per-game episode returns (RCCL / xGMI)
@@ -472,12 +479,14 @@ def main():
                 "batch_per_gpu": B, "global_batch": G, "grid": "64x64",
                 "n_npcs": cfg.n_npcs, "ticks_per_step": chunk, "streams": len(eng_parts),
                 "env_steps_per_step": G * chunk, "games_per_wave": lanes,
+                "lanes_per_game": shape["lanes_per_game"],
+                "nontemporal_stores": shape["nontemporal"],
                 "parallelism": f"games sharded by global id over {world} GPU(s)",
                 "build_id": _lib.build_id(),
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": rollout_kernel_name(B, cfg.n_npcs),
+                "kernel": rollout_kernel_name(cfg.n_npcs, shape),
                 "achieved": achieved_gbs,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

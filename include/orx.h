@@ -338,15 +338,17 @@ int orx_rollout_lanes(int64_t n_games);
  * paired form -- no NPCs, no dungeon bank, two RandomBots or two
  * StaircaseBots, batches below 64 games per wave: one lane per player) and
  * whether the trajectory rows are stored nontemporal (whole-line row
- * segments) or with the default policy.  Results never depend on it.  No
- * reference counterpart. */
+ * segments) or with the default policy; concurrency as in
+ * orx_rollout_concurrent (1 for orx_rollout).  Results never depend on it.
+ * No reference counterpart. */
 typedef struct orx_rollout_shape {
   int32_t games_per_wave;
   int32_t lanes_per_game;
   int32_t nontemporal;
 } orx_rollout_shape_t;
 int orx_rollout_shape(const orx_cfg_t* cfg, int32_t policy_p1, int32_t policy_p2,
-                      int64_t n_games, int32_t trajectory, orx_rollout_shape_t* out);
+                      int64_t n_games, int32_t trajectory, int32_t concurrency,
+                      orx_rollout_shape_t* out);
 
 /* Stock-seed mode: N, the depths each player's dstore ring holds for this
  * configuration (orx_state_t.dstore is [2][N][2][B] int32), or ORX_EINVAL
@@ -417,6 +419,16 @@ int orx_rollout(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p1,
                 int32_t policy_p2, int32_t n_ticks, int32_t* obs, int8_t* act,
                 int64_t n_games, uint64_t seed, int64_t game_offset,
                 void* stream);
+
+/* orx_rollout as one of `concurrency` (>= 1) launches that run on the device
+ * together -- a GPU's batch split over concurrent streams, as
+ * StreamShardedEngine does: the launch shape (orx_rollout_shape) is chosen
+ * for the device's whole load.  Results do not depend on it; orx_rollout is
+ * concurrency 1.  No reference counterpart. */
+int orx_rollout_concurrent(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p1,
+                           int32_t policy_p2, int32_t n_ticks, int32_t* obs, int8_t* act,
+                           int64_t n_games, uint64_t seed, int64_t game_offset,
+                           int32_t concurrency, void* stream);
 
 /* Staircase (sx[j], sy[j]) of dungeon `depths[j]`, generation `gens[j]`, of
  * episode `episodes[j]` of global game `game_ids[j]`: the keyed

@@ -41,7 +41,7 @@ _lib = None
 EXPORTS = ("orx_abi_version", "orx_last_error", "orx_validate_cfg", "orx_reset", "orx_step",
            "orx_step_events", "orx_policy", "orx_rollout", "orx_dungeon_stairs",
            "orx_dungeon_spawn", "orx_seed_mt", "orx_build_id", "orx_rollout_lanes", "orx_dstore_depths",
-           "orx_rollout_shape")
+           "orx_rollout_shape", "orx_rollout_concurrent")
 
 
 def load() -> ctypes.CDLL:
@@ -87,7 +87,11 @@ def load() -> ctypes.CDLL:
     # (bound only when present: an A/B diagnostic may load an older build)
     if hasattr(L, "orx_rollout_shape"):
         L.orx_rollout_shape.restype = ctypes.c_int
-        L.orx_rollout_shape.argtypes = [P(OrxCfg), i32, i32, i64, i32, P(OrxRolloutShape)]
+        L.orx_rollout_shape.argtypes = [P(OrxCfg), i32, i32, i64, i32, i32, P(OrxRolloutShape)]
+    if hasattr(L, "orx_rollout_concurrent"):
+        L.orx_rollout_concurrent.restype = ctypes.c_int
+        L.orx_rollout_concurrent.argtypes = [P(OrxCfg), P(OrxState), i32, i32, i32, vp, vp, i64,
+                                             u64, i64, i32, vp]
     if hasattr(L, "orx_dstore_depths"):
         L.orx_dstore_depths.restype = ctypes.c_int
         L.orx_dstore_depths.argtypes = [P(OrxCfg)]

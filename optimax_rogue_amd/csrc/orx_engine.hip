@@ -545,6 +545,26 @@ __device__ __forceinline__ void npc_any2(const Npcs<NCAP>& npc, uint32_t k1, uin
   }
 }
 
+// One key against every slot (the paired rollout's per-player test): the
+// zero-halfword test of npc_any2 on (slots ^ key:key), the two halves of the
+// running minimum folded at the end.
+template <int NCAP>
+__device__ __forceinline__ bool npc_any1(const Npcs<NCAP>& npc, uint32_t k) {
+  if constexpr (NCAP == 0) {
+    return false;
+  } else if constexpr (NCAP == kDense) {
+    return npc.any(k);
+  } else {
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    const uint32_t KK = k | (k << 16);
+    u16x2 m = __builtin_bit_cast(u16x2, npc.rd(0) ^ KK);
+#pragma unroll
+    for (int r = 1; r < Npcs<NCAP>::kRegs; ++r)
+      m = __builtin_elementwise_min(m, __builtin_bit_cast(u16x2, npc.rd(r) ^ KK));
+    return __builtin_elementwise_min(m, m.yx).x == 0;
+  }
+}
+
 __device__ __forceinline__ uint32_t pack_xy(int32_t x, int32_t y) {
   return (uint32_t)(x & 0xFF) | ((uint32_t)(y & 0xFF) << 8);
 }
@@ -2702,7 +2722,7 @@ struct PairWriter {
 
 // PM 1: both players RandomBot (no extension flags); PM 2: both StaircaseBot
 // (at most separation damage).  NCAP 0, empty dungeons, obs and act given.
-template <int PM, int AUX>
+template <int NCAP, int PM, int AUX>
 __global__ void __launch_bounds__(kRolloutBlock) pair_rollout_kernel(orx_cfg_t hc, orx_state_t st,
                                                                      int32_t n_ticks,
                                                                      int32_t* __restrict__ obs,
@@ -2735,11 +2755,15 @@ __global__ void __launch_bounds__(kRolloutBlock) pair_rollout_kernel(orx_cfg_t h
   int32_t status = st.status[i];
   uint32_t ep = (uint32_t)st.episode[i];
   int32_t sep = (c.ext & ORX_EXT_SEPARATION_DAMAGE) ? st.sep_start[i] : -1;
-  Npcs<0> npc;
-  npc.clear();
-  Items<0> items;
+  // NPCs (register slots): the game's in both lanes, kept identical -- every
+  // change to them happens in the rare block, which both lanes run
+  Npcs<NCAP> npc;
+  npc.bind(st, c, B, i);
+  load_npcs(st, c, B, i, npc);
+  NpcHpRegs<NCAP> hp;
+  if constexpr (NCAP > 0) hp.load(st.npc_health, c.K, B, i);
+  Items<NCAP> items;
   items.clear();
-  NpcHpRegs<0> hp;
   Deltas dl = {0, 0, 0, 0, 0, 0};
   bool restarted = false;
   constexpr int need = PM == 1 ? 2 : 0;
@@ -2788,7 +2812,14 @@ __global__ void __launch_bounds__(kRolloutBlock) pair_rollout_kernel(orx_cfg_t h
     const uint32_t e_om = (uint32_t)(otx ^ me.x) | (uint32_t)(oty ^ me.y);
     const uint32_t e_tt = (uint32_t)(tx ^ otx) | (uint32_t)(ty ^ oty);
     const bool meet = ((uint32_t)(me.d ^ od) | min(e_mo, min(e_om, e_tt))) == 0u;
-    const bool rare = !in_progress | meet | st_me | (st_o != 0);
+    // an NPC on the own target (NPC keys x | y << 8; all NPCs on depth d1)
+    bool hit_me = false;
+    int32_t hit_o = 0;
+    if constexpr (NCAP > 0) {
+      hit_me = (me.d == c.d1) & npc_any1(npc, (uint32_t)tx | ((uint32_t)ty << 8));
+      hit_o = pair_swap(hit_me ? 1 : 0);
+    }
+    const bool rare = !in_progress | meet | st_me | (st_o != 0) | hit_me | (hit_o != 0);
     const int32_t ft = tick + 1;
     const bool end = c.max_ticks && ft >= c.max_ticks;
     bool took_ordered = false;
@@ -2803,7 +2834,7 @@ __global__ void __launch_bounds__(kRolloutBlock) pair_rollout_kernel(orx_cfg_t h
       // instruction stream for both -- and the lanes swap them.
       bool fast = false;
       const int32_t osx = pair_swap(me.sx), osy = pair_swap(me.sy);
-      if (PM == 2 && (in_progress & !meet & (st_me != (st_o != 0)))) {
+      if (PM == 2 && (in_progress & !meet & (st_me != (st_o != 0)) & !hit_me & (hit_o == 0))) {
 #ifdef ORX_STAMPS
         ORX_CYC_BEGIN(cyf);
 #endif
@@ -2838,7 +2869,8 @@ __global__ void __launch_bounds__(kRolloutBlock) pair_rollout_kernel(orx_cfg_t h
         const int32_t ox0 = st_me ? ox : me.x, oy0 = st_me ? oy : me.y;
         const int32_t ox1 = st_me ? otx : tx, oy1 = st_me ? oty : ty;
         const bool touch = other_on & (((x == ox1) & (y == oy1)) | ((x == ox0) & (y == oy0)));
-        ok = ok & (c.ground.rng != 0u) & (v <= c.ground.rng) & !touch;
+        const bool npc_depth = NCAP > 0 && nd == c.d1 && npc.any_alive();
+        ok = ok & (c.ground.rng != 0u) & (v <= c.ground.rng) & !touch & !npc_depth;
         if (ok) {
           me.d = st_me ? nd : me.d;
           me.x = st_me ? x : tx;
@@ -2870,7 +2902,7 @@ __global__ void __launch_bounds__(kRolloutBlock) pair_rollout_kernel(orx_cfg_t h
         o.sy = osy;
         o.move = pair_swap(move);
         Player p1 = pick(isB, o, me), p2 = pick(isB, me, o);
-        took_ordered = rare_tick<0, false>(c, st, B, i, key, game, ep, p1, p2, npc, items, hp,
+        took_ordered = rare_tick<NCAP, false>(c, st, B, i, key, game, ep, p1, p2, npc, items, hp,
                                           tick, status, dl, sep, restarted, tb, need,
                                           isB ? otx : tx, isB ? oty : ty, isB ? tx : otx,
                                           isB ? ty : oty, false);
@@ -2926,6 +2958,10 @@ __global__ void __launch_bounds__(kRolloutBlock) pair_rollout_kernel(orx_cfg_t h
     st.status[i] = status;
     st.episode[i] = (int32_t)ep;
     if (c.ext & ORX_EXT_SEPARATION_DAMAGE) st.sep_start[i] = sep;
+    if constexpr (NCAP > 0) {
+      if (restarted || dl.npc_death) npc.store_alive(st.npc_alive, B, i);
+      if (restarted || dl.combat) hp.store(st.npc_health, c.K, B, i);
+    }
     flush_deltas(st, B, i, dl);
   }
 #ifdef ORX_STAMPS
@@ -3457,14 +3493,17 @@ struct RolloutPlan {
 
 // The paired form: no NPCs, no bank, the RandomBot or StaircaseBot trajectory
 // forms (PM 1 / 2), for batches the one-lane rule leaves below 64 games per
-// wave; its games per wave: two waves per SIMD until the wave holds 32
-// games, at least 8 (C5's 8-GPU share, 16,384 games: 8 per wave, 79 us per
-// launch against 89 at 16 and 112 at 32; C2 at 4,096: 50 against 51).
+// wave; its games per wave: two waves per SIMD -- counting the `concurrency`
+// launches that share the device (StreamShardedEngine's shards) -- until the
+// wave holds 32 games, at least 8 (C5's 8-GPU share, 16,384 games: 8 per
+// wave, 79 us per launch against 89 at 16 and 112 at 32; C2 at 4,096: 50
+// against 51; the bench's two 32,768-game C3 shards: 32 per wave, 96.6 us
+// per step against 158 at 16, four waves per SIMD where 156 VGPRs fit three).
 // ORX_ROLLOUT_LANES (games per wave) and ORX_ROLLOUT_PAIRED=0 override.
-RolloutPlan plan_rollout(const orx_cfg_t* cfg, int pm, uint32_t B) {
+RolloutPlan plan_rollout(const orx_cfg_t* cfg, int pm, uint32_t B, uint32_t concurrency) {
   RolloutPlan p;
   p.lanes = rollout_lanes(B);
-  p.paired = ncap_for(cfg->n_npcs) == 0 && cfg->n_layouts == 0 && (pm == 1 || pm == 2) &&
+  p.paired = ncap_for(cfg->n_npcs) != kDense && cfg->n_layouts == 0 && (pm == 1 || pm == 2) &&
              p.lanes <= 32u && paired_enabled();
   if (p.paired) {
     if (const int o = lanes_override()) {
@@ -3472,7 +3511,7 @@ RolloutPlan plan_rollout(const orx_cfg_t* cfg, int pm, uint32_t B) {
     } else {
       const uint64_t simds = (uint64_t)device_simds();
       uint32_t L = 32;
-      while (L > 8 && (uint64_t)B < 2 * simds * L) L >>= 1;
+      while (L > 8 && (uint64_t)B * concurrency < 2 * simds * L) L >>= 1;
       p.lanes = L;
     }
   }
@@ -3499,8 +3538,10 @@ int orx_rollout_lanes(int64_t n_games) {
 const char* orx_last_error(void) { return g_err; }
 
 int orx_rollout_shape(const orx_cfg_t* cfg, int32_t policy_p1, int32_t policy_p2,
-                      int64_t n_games, int32_t trajectory, orx_rollout_shape_t* out) {
+                      int64_t n_games, int32_t trajectory, int32_t concurrency,
+                      orx_rollout_shape_t* out) {
   int r;
+  if (concurrency < 1) return fail(ORX_EINVAL, "concurrency must be >= 1");
   if ((r = check_cfg(cfg)) || (r = check_policy(policy_p1)) || (r = check_policy(policy_p2)))
     return r;
   if (n_games <= 0 || n_games > 0x7FFFFFFFLL) return fail(ORX_EINVAL, "bad n_games");
@@ -3513,7 +3554,7 @@ int orx_rollout_shape(const orx_cfg_t* cfg, int32_t policy_p1, int32_t policy_p2
     return ORX_OK;
   }
   const int pm = rollout_pm(cfg, policy_p1, policy_p2, B, trajectory != 0);
-  const RolloutPlan p = plan_rollout(cfg, pm, B);
+  const RolloutPlan p = plan_rollout(cfg, pm, B, (uint32_t)concurrency);
   out->games_per_wave = (int32_t)p.lanes;
   out->lanes_per_game = p.paired ? 2 : 1;
   out->nontemporal = (pm != 0 && !p.nt) ? 0 : 1;
@@ -3650,7 +3691,16 @@ int orx_policy(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p1, i
 int orx_rollout(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p1, int32_t policy_p2,
                 int32_t n_ticks, int32_t* obs, int8_t* act, int64_t n_games, uint64_t seed,
                 int64_t game_offset, void* stream) {
+  return orx_rollout_concurrent(cfg, st, policy_p1, policy_p2, n_ticks, obs, act, n_games, seed,
+                                game_offset, 1, stream);
+}
+
+int orx_rollout_concurrent(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p1,
+                           int32_t policy_p2, int32_t n_ticks, int32_t* obs, int8_t* act,
+                           int64_t n_games, uint64_t seed, int64_t game_offset,
+                           int32_t concurrency, void* stream) {
   int r;
+  if (concurrency < 1) return fail(ORX_EINVAL, "concurrency must be >= 1");
   if ((r = check_cfg(cfg)) || (r = check_sizes(n_games, game_offset)) ||
       (r = check_policy(policy_p1)) || (r = check_policy(policy_p2)))
     return r;
@@ -3676,7 +3726,7 @@ int orx_rollout(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p1, 
     return launch_status("orx_rollout");
   }
   const int pm = rollout_pm(cfg, policy_p1, policy_p2, B, obs && act);
-  const RolloutPlan plan = plan_rollout(cfg, pm, B);
+  const RolloutPlan plan = plan_rollout(cfg, pm, B, (uint32_t)concurrency);
   const uint32_t lanes = plan.lanes;
   const uint32_t threads = rollout_threads(B, lanes);
   const uint32_t per_block = threads / 64u * lanes;
@@ -3705,11 +3755,15 @@ int orx_rollout(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p1, 
   // per wave (env ORX_ROLLOUT_PAIRED=0 turns it off, for measurements)
   if (plan.paired) {
     const dim3 blocks((B + per_block - 1) / per_block);
-#define ORX_PAIR(P, A)                                                                          \
-    if (pm == P && (A == kStreamAux) == nt)                                                     \
-      hipLaunchKernelGGL((pair_rollout_kernel<P, A>), blocks, dim3(threads), 0, s, *cfg, *st,    \
+#define ORX_PAIR(N, P, A)                                                                       \
+    if (nc == N && pm == P && (A == kStreamAux) == nt)                                          \
+      hipLaunchKernelGGL((pair_rollout_kernel<N, P, A>), blocks, dim3(threads), 0, s, *cfg, *st, \
                          n_ticks, obs, act, B, k, off, lanes);
-    ORX_PAIR(1, kStreamAux) ORX_PAIR(1, kPartialAux) ORX_PAIR(2, kStreamAux) ORX_PAIR(2, kPartialAux)
+#define ORX_PAIRS(N)                                                                            \
+    ORX_PAIR(N, 1, kStreamAux) ORX_PAIR(N, 1, kPartialAux)                                      \
+    ORX_PAIR(N, 2, kStreamAux) ORX_PAIR(N, 2, kPartialAux)
+    ORX_PAIRS(0) ORX_PAIRS(8) ORX_PAIRS(16)
+#undef ORX_PAIRS
 #undef ORX_PAIR
     return launch_status("orx_rollout");
   }

@@ -55,6 +55,9 @@ class BatchedEngine:
         self.K = int(cfg.n_npcs)
         self.seed = int(seed)
         self.game_offset = int(game_offset)
+        # launches sharing the device with this batch's rollouts (orx_rollout_concurrent):
+        # StreamShardedEngine sets it to its stream count
+        self.concurrency = 1
         B, K = self.B, self.K
         z = lambda *shape, dt=torch.int32: torch.zeros(shape, dtype=dt, device=device)
         self.p_x, self.p_y, self.p_depth, self.p_health = z(2, B), z(2, B), z(2, B), z(2, B)
@@ -146,14 +149,14 @@ class BatchedEngine:
         act)`` on the current stream of this moment, its C arguments bound once
         (a timed loop then pays one ctypes call per launch, nothing else)."""
         self._check_traj(n_ticks, obs, act)
-        fn, check = self.lib.orx_rollout, _lib.check
+        fn, check = self.lib.orx_rollout_concurrent, _lib.check
         args = (self._pcfg, self._pst, int(p1), int(p2), int(n_ticks), _ptr(obs), _ptr(act),
-                self.B, self.seed, self.game_offset, self._stream())
+                self.B, self.seed, self.game_offset, int(self.concurrency), self._stream())
 
         def launch():
             code = fn(*args)
             if code:
-                check("orx_rollout", code)
+                check("orx_rollout_concurrent", code)
         return launch
 
     def rollout_lanes(self) -> int:
@@ -168,7 +171,7 @@ class BatchedEngine:
         form), nontemporal trajectory stores."""
         out = _lib.OrxRolloutShape()
         code = self.lib.orx_rollout_shape(self._pcfg, int(p1), int(p2), self.B, int(trajectory),
-                                          ctypes.byref(out))
+                                          int(self.concurrency), ctypes.byref(out))
         _lib.check("orx_rollout_shape", code)
         return {"games_per_wave": out.games_per_wave, "lanes_per_game": out.lanes_per_game,
                 "nontemporal": bool(out.nontemporal)}
@@ -237,8 +240,8 @@ class BatchedEngine:
         [n_ticks, len(OBS_FIELDS), n_games]) and ``act`` (int8 [n_ticks,
         n_games, 2]) receive every tick's observation and actions."""
         self._check_traj(n_ticks, obs, act)
-        self._call("orx_rollout", int(p1), int(p2), int(n_ticks), _ptr(obs), _ptr(act), self.B,
-                   self.seed, self.game_offset, self._stream())
+        self._call("orx_rollout_concurrent", int(p1), int(p2), int(n_ticks), _ptr(obs), _ptr(act),
+                   self.B, self.seed, self.game_offset, int(self.concurrency), self._stream())
 
     def _check_actions(self, a: torch.Tensor, what: str) -> None:
         # the kernels index [n_games, 2] blindly: a wrong buffer would be an
@@ -494,6 +497,7 @@ class StreamShardedEngine:
             with torch.cuda.stream(s):
                 self.parts.append(BatchedEngine(cfg, cnt, seed=seed, game_offset=game_offset + off,
                                                 device=self.device))
+                self.parts[-1].concurrency = n_streams
         for s in self.streams:
             cur.wait_stream(s)
 
@@ -538,6 +542,11 @@ class StreamShardedEngine:
 
     def rollout_lanes(self) -> int:
         return self.parts[0].rollout_lanes()
+
+    def rollout_shape(self, p1: int = Policy.Random, p2: int = Policy.Random,
+                      trajectory: bool = True) -> dict:
+        """The shape each shard's concurrent rollout launch takes (the first shard's)."""
+        return self.parts[0].rollout_shape(p1, p2, trajectory)
 
     def episode_returns(self) -> torch.Tensor:
         """(ret_sum, ep_count) int32 [2, n_games] in global id order (device)."""

@@ -40,7 +40,7 @@ def test_library_exports_every_declared_symbol(lib):
                            "orx_step", "orx_step_events", "orx_policy", "orx_rollout",
                            "orx_dungeon_stairs", "orx_dungeon_spawn", "orx_seed_mt",
                            "orx_build_id", "orx_rollout_lanes", "orx_dstore_depths",
-                           "orx_rollout_shape"])
+                           "orx_rollout_shape", "orx_rollout_concurrent"])
     from optimax_rogue_amd import _lib
     assert sorted(_lib.EXPORTS) == decl
     for name in decl:
@@ -159,14 +159,15 @@ def test_engine_refuses_cpu():
 def test_rollout_shape_rules(lib):
     """orx_rollout_shape (no device work; 1,024 SIMDs assumed without a GPU):
     the paired two-lanes-per-game form for NPC-free RandomBot / StaircaseBot
-    trajectory launches below 64 games per wave, nontemporal stores only for
+    trajectory launches below 64 games per wave (counting the launches that
+    share the device), nontemporal stores only for
     whole-line row segments (32+ games per wave)."""
     from optimax_rogue_amd import EnvConfig
     from optimax_rogue_amd._lib import OrxRolloutShape
 
-    def shape(cfg, B, p1=1, p2=1, traj=1):
+    def shape(cfg, B, p1=1, p2=1, traj=1, conc=1):
         out = OrxRolloutShape()
-        assert lib.orx_rollout_shape(ctypes.byref(cfg.to_c()), p1, p2, B, traj,
+        assert lib.orx_rollout_shape(ctypes.byref(cfg.to_c()), p1, p2, B, traj, conc,
                                      ctypes.byref(out)) == 0
         return out.games_per_wave, out.lanes_per_game, out.nontemporal
 
@@ -174,11 +175,14 @@ def test_rollout_shape_rules(lib):
     assert shape(EnvConfig.c2(), 4096) == (8, 2, 0)               # C2
     assert shape(EnvConfig.c5(), 32768, 2, 2) == (16, 2, 0)
     assert shape(EnvConfig.c5(), 131072, 2, 2) == (64, 1, 1)      # full waves: one lane per game
-    assert shape(EnvConfig.c3(), 32768) == (32, 1, 1)             # the bench's stream shard
-    assert shape(EnvConfig.c3(), 65536) == (64, 1, 1)
-    assert shape(EnvConfig.c3(), 16384) == (16, 1, 0)             # NPCs: one lane per game
+    assert shape(EnvConfig.c3(), 32768, conc=2) == (32, 2, 1)     # the bench's two stream shards
+    assert shape(EnvConfig.c3(), 32768) == (16, 2, 0)             # one such launch alone
+    assert shape(EnvConfig.c3(), 65536) == (64, 1, 1)             # full waves: one lane per game
+    assert shape(EnvConfig(n_npcs=40), 4096) == (16, 1, 0)        # LDS NPC table: one lane per game
     assert shape(EnvConfig.c5(), 16384, 2, 1) == (16, 1, 1)       # mixed bots: the generic form
     assert shape(EnvConfig.c2(), 4096, traj=0) == (16, 1, 1)      # no trajectory buffers
     bad = OrxRolloutShape()
-    assert lib.orx_rollout_shape(ctypes.byref(EnvConfig.c2().to_c()), 9, 1, 64, 1,
+    assert lib.orx_rollout_shape(ctypes.byref(EnvConfig.c2().to_c()), 9, 1, 64, 1, 1,
+                                 ctypes.byref(bad)) == -22
+    assert lib.orx_rollout_shape(ctypes.byref(EnvConfig.c2().to_c()), 1, 1, 64, 1, 0,
                                  ctypes.byref(bad)) == -22

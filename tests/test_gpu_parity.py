@@ -466,7 +466,8 @@ def test_bench_timed_path_vs_oracle(oracle_lib):
     eng = StreamShardedEngine(cfg, B, seed=seed, game_offset=0, device=dev, n_streams=2)
     assert [e.B for e in eng.parts] == [32768, 32768]
     assert [e.game_offset for e in eng.parts] == [0, 32768]
-    assert eng.rollout_lanes() == 32          # the games per wave bench.py times at
+    assert eng.rollout_shape(1, 1) == {"games_per_wave": 32, "lanes_per_game": 2,
+                                       "nontemporal": True}   # the form bench.py times
     obs, act = eng.trajectory_buffers(T)
     launch = eng.rollout_launcher(T, 1, 1, obs=obs, act=act)
     rng = np.random.default_rng(7)

@@ -21,7 +21,8 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-f
   -- python3 $R/bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_under_trace.json 2> $O/trace.err
 f=$(find $O/trace -name "run_kernel_trace.csv" | head -1)
 python3 $R/tools/ktrace_summary.py $f > $O/kernel_trace_summary.txt
-python3 $R/tools/ktrace_summary.py --span $f "rollout_kernel<8, 1, false>" 65536 2 >> $O/kernel_trace_summary.txt
+KNAME=$(python3 -c "import json,sys; print(json.load(open(sys.argv[1]))['roofline']['kernel'])" $O/bench.json)
+python3 $R/tools/ktrace_summary.py --span $f "$KNAME" 65536 2 >> $O/kernel_trace_summary.txt
 cp $(find $O/trace -name "run_kernel_stats.csv" | head -1) $O/kernel_stats.csv
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $O/fetch -o pmc --output-format csv \
   -- python3 $R/bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_under_fetch.json 2> $O/fetch.err

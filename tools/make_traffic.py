@@ -7,12 +7,14 @@ command itself (tools/gpu_profile.sh):
 
 HBM bytes per launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024: FETCH_SIZE is
 doubled per MI355X_MICROARCH.md (gfx950 tallies 128-B read requests at 64 B).
-Only the dispatches of the headline kernel at the headline grid are averaged
+Only the dispatches of the headline kernel (the form orx_rollout_shape gives
+for bench.py's concurrent stream shards) at its most-dispatched grid are averaged
 (bench.py launches that kernel at no other shape by default); a bench step is
 one dispatch per stream shard, so bytes per step = shards x the average.  The entry is
 stamped with the library's build id: bench.py uses it only for that build.
 """
 import collections
+import ctypes
 import csv
 import glob
 import json
@@ -36,13 +38,23 @@ def load(d, counter):
 
 def main(fetch_dir, write_dir, out_path=None, batch=65536, ticks=128, streams=2):
     import bench
-    from optimax_rogue_amd import _lib
+    from optimax_rogue_amd import EnvConfig, _lib
     fe, wr = load(fetch_dir, "FETCH_SIZE"), load(write_dir, "WRITE_SIZE")
     K = 8
-    kname = bench.rollout_kernel_name(batch, K)
     part = batch // streams                      # bench.py's stream shards (equal here)
-    lanes = _lib.load().orx_rollout_lanes(part)
-    grid = -(-part // (4 * lanes)) * 256         # 256-thread blocks of 4 waves
+    shape = _lib.OrxRolloutShape()
+    lib = _lib.load()
+    assert lib.orx_rollout_shape(ctypes.byref(EnvConfig.c3().to_c()), 1, 1, part, 1, streams,
+                                 ctypes.byref(shape)) == 0
+    shape = {"games_per_wave": shape.games_per_wave, "lanes_per_game": shape.lanes_per_game,
+             "nontemporal": bool(shape.nontemporal)}
+    kname = bench.rollout_kernel_name(K, shape)
+    lanes = shape["games_per_wave"]
+    # the headline kernel's grid: the dispatch shape it was profiled at most
+    grids = [g for (n, g) in fe if n == kname]
+    if not grids:
+        raise SystemExit(f"no dispatches of {kname}: {sorted(fe)}")
+    grid = max(grids, key=lambda g: fe[(kname, g)][1])
     out = {"_source": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over "
                       "`python3 bench.py --gpus 1 --steps 20 --warmup 5` (MI355X, ROCm 7.2), "
                       "written by tools/make_traffic.py. hbm_bytes = (2 * FETCH_SIZE + "
@@ -55,7 +67,8 @@ def main(fetch_dir, write_dir, out_path=None, batch=65536, ticks=128, streams=2)
     alg = bench.bytes_per_game("rollout", K, ticks) * batch
     per_step = streams * (2 * f[0] + w[0]) * 1024
     out["rollout"] = {"kernel": kname, "batch": batch, "ticks": ticks, "streams": streams,
-                      "grid": grid, "games_per_wave": lanes, "dispatches": [f[1], w[1]],
+                      "grid": grid, "games_per_wave": lanes,
+                      "lanes_per_game": shape["lanes_per_game"], "dispatches": [f[1], w[1]],
                       "fetch_kb_per_dispatch": round(f[0], 1),
                       "write_kb_per_dispatch": round(w[0], 1),
                       "hbm_bytes_per_step": int(per_step),
