@@ -2436,6 +2436,8 @@ __device__ __forceinline__ void rollout_tick(const Cfg& c, const orx_state_t& st
   if (c.ext & ORX_EXT_SEPARATION_DAMAGE) {  // build extension (readme.md:46-47), C5's ladder
     // base: the in-progress games whose tick took the common path's rules
     // (free moves, or a hit, a descend or a meet in the rare block)
+    // base: the in-progress games whose tick took the common path's rules
+    // (free moves, or a hit, a descend or a meet in the rare block)
     const bool base = in_progress & !took_ordered;
     if (base) {
       if (p1.d != p2.d) {
@@ -2722,8 +2724,12 @@ struct PairWriter {
 
 // PM 1: both players RandomBot (no extension flags); PM 2: both StaircaseBot
 // (at most separation damage).  NCAP 0, empty dungeons, obs and act given.
-template <int NCAP, int PM, int AUX>
-__global__ void __launch_bounds__(kRolloutBlock) pair_rollout_kernel(orx_cfg_t hc, orx_state_t st,
+// (diagnostic builds may add attributes, e.g. an occupancy target)
+#ifndef ORX_PAIR_ATTR
+#define ORX_PAIR_ATTR
+#endif
+template <int NCAP, int PM, int AUX, bool SEP>
+__global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kernel(orx_cfg_t hc, orx_state_t st,
                                                                      int32_t n_ticks,
                                                                      int32_t* __restrict__ obs,
                                                                      int8_t* __restrict__ act,
@@ -2736,8 +2742,7 @@ __global__ void __launch_bounds__(kRolloutBlock) pair_rollout_kernel(orx_cfg_t h
   const uint32_t who = lane & 1u;  // 0: player 1, 1: player 2
   const bool isB = who != 0u;
   Cfg c = make_cfg(hc, st);
-  if (PM == 1) c.ext = 0;
-  if (PM == 2) c.ext &= ORX_EXT_SEPARATION_DAMAGE;
+  c.ext = SEP ? ORX_EXT_SEPARATION_DAMAGE : 0;  // PM 1: none; PM 2: at most this one
   const uint32_t game = off + i;
   ORX_STAMP(0);
   Player me;
@@ -2754,7 +2759,7 @@ __global__ void __launch_bounds__(kRolloutBlock) pair_rollout_kernel(orx_cfg_t h
   int32_t tick = st.tick[i];
   int32_t status = st.status[i];
   uint32_t ep = (uint32_t)st.episode[i];
-  int32_t sep = (c.ext & ORX_EXT_SEPARATION_DAMAGE) ? st.sep_start[i] : -1;
+  int32_t sep = SEP ? st.sep_start[i] : -1;
   // NPCs (register slots): the game's in both lanes, kept identical -- every
   // change to them happens in the rare block, which both lanes run
   Npcs<NCAP> npc;
@@ -2919,7 +2924,7 @@ __global__ void __launch_bounds__(kRolloutBlock) pair_rollout_kernel(orx_cfg_t h
     dl.eps += (!rare & end) ? 1 : 0;
     status = rare ? status : (end ? ORX_TIE : ORX_IN_PROGRESS);
     tick = rare ? tick : ft;
-    if (c.ext & ORX_EXT_SEPARATION_DAMAGE) {  // as rollout_tick (readme.md:46-47)
+    if constexpr (SEP) {  // as rollout_tick (readme.md:46-47)
       const bool base = in_progress & !took_ordered;
       const int32_t od2 = pair_swap(me.d);
       if (base) {
@@ -2957,7 +2962,7 @@ __global__ void __launch_bounds__(kRolloutBlock) pair_rollout_kernel(orx_cfg_t h
     st.tick[i] = tick;
     st.status[i] = status;
     st.episode[i] = (int32_t)ep;
-    if (c.ext & ORX_EXT_SEPARATION_DAMAGE) st.sep_start[i] = sep;
+    if constexpr (SEP) st.sep_start[i] = sep;
     if constexpr (NCAP > 0) {
       if (restarted || dl.npc_death) npc.store_alive(st.npc_alive, B, i);
       if (restarted || dl.combat) hp.store(st.npc_health, c.K, B, i);
@@ -3755,13 +3760,15 @@ int orx_rollout_concurrent(const orx_cfg_t* cfg, const orx_state_t* st, int32_t 
   // per wave (env ORX_ROLLOUT_PAIRED=0 turns it off, for measurements)
   if (plan.paired) {
     const dim3 blocks((B + per_block - 1) / per_block);
-#define ORX_PAIR(N, P, A)                                                                       \
-    if (nc == N && pm == P && (A == kStreamAux) == nt)                                          \
-      hipLaunchKernelGGL((pair_rollout_kernel<N, P, A>), blocks, dim3(threads), 0, s, *cfg, *st, \
-                         n_ticks, obs, act, B, k, off, lanes);
+    const bool sepd = pm == 2 && (cfg->flags & ORX_EXT_SEPARATION_DAMAGE) != 0;
+#define ORX_PAIR(N, P, A, S)                                                                    \
+    if (nc == N && pm == P && (A == kStreamAux) == nt && S == sepd)                             \
+      hipLaunchKernelGGL((pair_rollout_kernel<N, P, A, S>), blocks, dim3(threads), 0, s, *cfg,  \
+                         *st, n_ticks, obs, act, B, k, off, lanes);
 #define ORX_PAIRS(N)                                                                            \
-    ORX_PAIR(N, 1, kStreamAux) ORX_PAIR(N, 1, kPartialAux)                                      \
-    ORX_PAIR(N, 2, kStreamAux) ORX_PAIR(N, 2, kPartialAux)
+    ORX_PAIR(N, 1, kStreamAux, false) ORX_PAIR(N, 1, kPartialAux, false)                        \
+    ORX_PAIR(N, 2, kStreamAux, false) ORX_PAIR(N, 2, kPartialAux, false)                        \
+    ORX_PAIR(N, 2, kStreamAux, true) ORX_PAIR(N, 2, kPartialAux, true)
     ORX_PAIRS(0) ORX_PAIRS(8) ORX_PAIRS(16)
 #undef ORX_PAIRS
 #undef ORX_PAIR
