@@ -2839,6 +2839,63 @@ __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kern
       // instruction stream for both -- and the lanes swap them.
       bool fast = false;
       const int32_t osx = pair_swap(me.sx), osy = pair_swap(me.sy);
+      if constexpr (PM == 2 && NCAP == 0) {
+        if (!in_progress & (c.autoreset != 0)) {  // uniform over the pair
+          // The next episode (setup_game's keyed first-block form), its two
+          // starting dungeons split over the pair: each lane draws its own
+          // player's DUNGEON block beside the INIT block, and the lanes swap
+          // staircases (Together: both draw depth 0's).  Anything the first
+          // blocks do not settle takes the general form below.
+          const uint32_t ep1 = ep + 1u;
+          const bool sepm = c.start_mode == ORX_START_SEPARATED;
+          const int32_t dme = sepm ? (isB ? c.d2 : c.d1) : 0;
+          W4 wd = philox(game, ep1, (uint32_t)dme, tag(PUR_DUNGEON, 0), key);
+          W4 wi = philox(game, ep1, 0u, tag(PUR_INIT, 0), key);
+          launder_w4(wd);
+          launder_w4(wi);
+          int32_t sx, sy;
+          const bool okd = stair_from_block(c, wd, sx, sy);
+          const int32_t osx1 = pair_swap(sx), osy1 = pair_swap(sy);
+          const int32_t s1x = isB ? osx1 : sx, s1y = isB ? osy1 : sy;
+          const int32_t s2x = isB ? sx : osx1, s2y = isB ? sy : osy1;
+          // both players from the INIT block's four words, as setup_game
+          const NpBound g = c.ground;
+          int n = 0;
+          int32_t x1 = 0, y1 = 0, x2 = 0, y2 = 0;
+#pragma unroll
+          for (uint32_t j = 0; j < 4; ++j) {
+            const uint32_t word = j == 0 ? wi.a : j == 1 ? wi.b : j == 2 ? wi.c : wi.d;
+            const bool is_p2 = n == 1;
+            const uint32_t v = word & g.mask;
+            int32_t x, y;
+            ground_cell<false>(c, v, -1, is_p2 ? s2x : s1x, is_p2 ? s2y : s1y, x, y);
+            const bool take = n < 2 && v <= g.rng && !(is_p2 && !sepm && x == x1 && y == y1);
+            x1 = (take && n == 0) ? x : x1;
+            y1 = (take && n == 0) ? y : y1;
+            x2 = (take && is_p2) ? x : x2;
+            y2 = (take && is_p2) ? y : y2;
+            n += take ? 1 : 0;
+          }
+          const bool ok = okd & (pair_swap(okd ? 1 : 0) != 0) & (n == 2) & (g.rng != 0u);
+          if (ok) {
+            ep = ep1;
+            me.d = dme;
+            me.sx = sx;
+            me.sy = sy;
+            me.x = isB ? x2 : x1;
+            me.y = isB ? y2 : y1;
+            me.hp = c.player_hp;
+            tick = kStartTick;
+            status = ORX_IN_PROGRESS;
+            sep = -1;
+            restarted = true;
+            fast = true;
+#ifdef ORX_STAMPS
+            ORX_COUNT(dl.n_reset);
+#endif
+          }
+        }
+      }
       if (PM == 2 && (in_progress & !meet & (st_me != (st_o != 0)) & !hit_me & (hit_o == 0))) {
 #ifdef ORX_STAMPS
         ORX_CYC_BEGIN(cyf);

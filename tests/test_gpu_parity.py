@@ -597,3 +597,50 @@ def test_known_answer_scenarios(case):
                 got, want = got[live], want[live]
             assert np.array_equal(got, want), (case["name"], events, k, got, want)
         torch.cuda.synchronize()
+
+
+# The paired rollout form (pair_rollout_kernel: two lanes per game, one per
+# player) on its own: NPC-free StaircaseBot pairs with and without separation
+# damage, Together and Separated starts, both despawn rules, short episodes
+# (the paired reset and descend fast paths and their general fallbacks), and
+# RandomBot pairs with register NPCs -- trajectories and state against the
+# oracle's policy + step, tick by tick.
+PAIRED_CASES = {
+    "stairs_sep_damage": (dict(width=12, height=10, start_mode=2, p1_depth=0, p2_depth=2,
+                               max_ticks=60, flags=1, sep_period=2), (2, 2), 1000, 61),
+    "stairs_sep_damage_unused": (dict(width=9, height=14, despawn=2, max_ticks=40, flags=1,
+                                      sep_period=3, player_health=4), (2, 2), 777, 62),
+    "stairs_sep_period1_frail": (dict(width=7, height=7, start_mode=2, p1_depth=1, p2_depth=0,
+                                      max_ticks=0, flags=1, sep_period=1, player_health=3),
+                                 (2, 2), 1531, 63),
+    "stairs_short_episodes": (dict(width=20, height=20, max_ticks=25), (2, 2), 1531, 64),
+    "stairs_separated_64": (dict(width=64, height=64, start_mode=2, p1_depth=3, p2_depth=1,
+                                 max_ticks=90, despawn=2), (2, 2), 2048, 65),
+    "random_npcs_resets": (dict(width=10, height=10, n_npcs=5, max_ticks=30), (1, 1), 1000, 66),
+    "random_duel_deaths": (dict(width=4, height=5, max_ticks=0, player_health=2), (1, 1), 500,
+                           67),
+}
+
+
+@pytest.mark.parametrize("name", sorted(PAIRED_CASES))
+def test_paired_rollout_vs_oracle(name, oracle_lib):
+    import torch
+    from optimax_rogue_amd.enums import OBS_FIELDS
+    cfg, pol, B, seed = PAIRED_CASES[name]
+    ora = oracle_lib.Oracle(cfg, B, seed, 5)
+    ora.reset(episode=np.zeros(B, np.int32))
+    eng = _engine(cfg, B, seed, 5)
+    assert eng.rollout_shape(*pol)["lanes_per_game"] == 2, name
+    T = 40
+    obs = torch.zeros((T, len(OBS_FIELDS), B), dtype=torch.int32, device=eng.device)
+    act = torch.zeros((T, B, 2), dtype=torch.int8, device=eng.device)
+    episodes = 0
+    for launch in range(4):
+        want_act, want_obs = _replay(ora, T, pol)
+        eng.rollout(T, *pol, obs=obs, act=act)
+        compare_state(eng.snapshot(), ora.export(), ora.K, f"{name} launch {launch}")
+        assert np.array_equal(act.cpu().numpy(), want_act), f"{name} actions {launch}"
+        assert np.array_equal(obs.cpu().numpy(), want_obs), f"{name} obs {launch}"
+    episodes = int(eng.snapshot()["episode"].sum())
+    assert episodes > 0, name   # every case crosses resets
+    torch.cuda.synchronize()
