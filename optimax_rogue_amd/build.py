@@ -107,9 +107,12 @@ def main(argv):
             out = os.path.abspath(next(it))
         elif a == "--variant":
             variants.append(next(it))
-    for v in variants:
-        print(build_variant(v, force, verbose=True))
-    if defines or out or not variants:
+    if len(variants) > 1 and out:
+        raise SystemExit("--out names one library: give one --variant with it")
+    for v in variants:   # --variant NAME [--out PATH]: that variant (plus any --define)
+        print(build(force, True, VARIANTS[v] + tuple(defines),
+                    out or os.path.join(AB_LIBS, v + ".so")))
+    if not variants:
         print(build(force, verbose=True, defines=defines, out=out))
 
 

@@ -2779,6 +2779,11 @@ __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kern
   ORX_STAMP(1);
   int32_t t = 0;
   do {
+    if constexpr ((ORX_DIAG & 32) != 0) {  // diagnostic: the trajectory stores alone
+      tick += 1;
+      traj.write(me, isB ? status : tick, ORX_MOVE_STAY);
+      continue;
+    }
     // the bot's move (randombot.py:20-21 / staircasebot.py:9-21)
     W4 tb = {0u, 0u, 0u, 0u};
     int32_t move;

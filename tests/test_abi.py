@@ -71,6 +71,27 @@ def test_diagnostic_builds_carry_their_defines_in_the_build_id():
     assert build.source_id(["B=1", "A=2"]) == build.source_id(["A=2", "B=1"])
 
 
+def test_build_cli_routes_variants(monkeypatch, tmp_path):
+    """`--variant NAME [--out PATH]` builds that variant's -D set (into PATH
+    when given), never the product build (the compile itself is stubbed)."""
+    from optimax_rogue_amd import build
+    calls = []
+    monkeypatch.setattr(build, "build", lambda force, verbose=False, defines=(), out=None:
+                        calls.append((tuple(defines), out)) or str(out))
+    out = str(tmp_path / "d16.so")
+    build.main(["--variant", "diag16", "--out", out])
+    assert calls == [(("ORX_DIAG=16",), out)]
+    calls.clear()
+    build.main(["--variant", "diag32", "--define", "ORX_STREAM_AUX=0"])
+    assert calls == [(("ORX_DIAG=32", "ORX_STREAM_AUX=0"),
+                      os.path.join(build.AB_LIBS, "diag32.so"))]
+    calls.clear()
+    build.main(["--define", "ORX_DIAG=96", "--out", out])
+    assert calls == [(("ORX_DIAG=96",), out)]
+    with pytest.raises(SystemExit):
+        build.main(["--variant", "diag16", "--variant", "diag32", "--out", out])
+
+
 def test_struct_layouts_match_header():
     from optimax_rogue_amd._lib import OrxState
     from optimax_rogue_amd.config import CFG_FIELDS, OrxCfg
