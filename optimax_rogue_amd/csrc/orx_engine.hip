@@ -2779,6 +2779,9 @@ __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kern
   ORX_STAMP(1);
   int32_t t = 0;
   do {
+#ifdef ORX_STAMPS
+    if (t == 64) { ORX_STAMP(2); }
+#endif
     if constexpr ((ORX_DIAG & 32) != 0) {  // diagnostic: the trajectory stores alone
       tick += 1;
       traj.write(me, isB ? status : tick, ORX_MOVE_STAY);
@@ -2899,6 +2902,34 @@ __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kern
             ORX_COUNT(dl.n_reset);
 #endif
           }
+        }
+      }
+      if constexpr (PM == 1 && NCAP > 0) {
+        // NPC hits without a meet or a staircase (C3's common rare tick): the
+        // attackers stay, the other player moves; both lanes apply both hits
+        // to their identical NPC registers (npc_hits: order-free without the
+        // character mechanics, which PM 1 excludes)
+        if (in_progress & !meet & !st_me & (st_o == 0) & (hit_me | (hit_o != 0))) {
+          const uint32_t kme = (uint32_t)tx | ((uint32_t)ty << 8);
+          const int h_me = hit_me ? npc.find(kme) : -1;
+          const int h_o = pair_swap(h_me);
+          const uint32_t k_o = (uint32_t)pair_swap((int32_t)kme);
+          const int h1 = isB ? h_o : h_me, h2 = isB ? h_me : h_o;
+          const int32_t dmg = c.player_dmg_net > 0 ? c.player_dmg_net : 0;
+          Events<false> ev{nullptr, 0};
+          bool k1 = false, k2 = false;
+          dl.combat += (h1 >= 0 ? 1 : 0) + (h2 >= 0 ? 1 : 0);
+          npc_hits(c, npc, hp, h1, h2, dmg, dmg, dl, ev, k1, k2, isB ? k_o : kme,
+                   isB ? kme : k_o);
+          me.x = hit_me ? me.x : tx;
+          me.y = hit_me ? me.y : ty;
+          dl.eps += end ? 1 : 0;
+          tick = ft;
+          status = end ? ORX_TIE : ORX_IN_PROGRESS;
+          fast = true;
+#ifdef ORX_STAMPS
+          ORX_COUNT(dl.n_hits);
+#endif
         }
       }
       if (PM == 2 && (in_progress & !meet & (st_me != (st_o != 0)) & !hit_me & (hit_o == 0))) {

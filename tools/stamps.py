@@ -44,7 +44,8 @@ def main():
     e.rollout(T, pol, pol, obs=obs, act=act)
     f.record()
     torch.cuda.synchronize()
-    W = -(-B // e.rollout_lanes())    # one game per lane, rollout_lanes() games per wave
+    shape = e.rollout_shape(pol, pol)
+    W = -(-B // shape["games_per_wave"])   # the launch's waves (paired: two lanes per game)
     buf = np.zeros(W * 16, dtype=np.uint64)
     dl = ctypes.CDLL(lib)
     dl.orx_diag_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int64]
@@ -53,7 +54,8 @@ def main():
     t0 = st[:, 0].min()
     st = st - t0
     # s_memtime counts the shader clock; report cycles and the event time
-    out = {"B": B, "ticks": T, "cfg": cname, "lanes": e.rollout_lanes(), "event_us": round(s.elapsed_time(f) * 1e3, 2)}
+    out = {"B": B, "ticks": T, "cfg": cname, "games_per_wave": shape["games_per_wave"],
+           "lanes_per_game": shape["lanes_per_game"], "event_us": round(s.elapsed_time(f) * 1e3, 2)}
     names = ["entry", "loaded", "tick64", "loop_end", "drained"]
     for j, n in enumerate(names):
         v = st[:, j]
