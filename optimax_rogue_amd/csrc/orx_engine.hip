@@ -2932,6 +2932,43 @@ __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kern
 #endif
         }
       }
+      if constexpr (PM == 1) {
+        // a meet without a staircase or an NPC hit: rare_tick's lean meet,
+        // the two moves in the drawn order (the tick block's word a; an
+        // all-reject word takes the ordered tick), from each lane's side
+        const uint32_t sa = ~(tb.a >> 1) & 0x55555555u;
+        if (in_progress & meet & !st_me & (st_o == 0) & !hit_me & (hit_o == 0) & (sa != 0u)) {
+          const bool p1_first = ((tb.a >> __builtin_ctz(sa)) & 1u) != 0;
+          const bool me_first = p1_first != isB;
+          const int32_t ax = me_first ? tx : otx, ay = me_first ? ty : oty;
+          const int32_t bx = me_first ? otx : tx, by = me_first ? oty : ty;
+          const int32_t fx0 = me_first ? me.x : ox, fy0 = me_first ? me.y : oy;
+          const int32_t sx0 = me_first ? ox : me.x, sy0 = me_first ? oy : me.y;
+          const bool occf = (ax == sx0) & (ay == sy0);  // the first attacks the second
+          const int32_t fx = occf ? fx0 : ax, fy = occf ? fy0 : ay;
+          const bool occs = (bx == fx) & (by == fy);    // the second attacks the first
+          me.x = me_first ? fx : (occs ? sx0 : bx);
+          me.y = me_first ? fy : (occs ? sy0 : by);
+          const int32_t dmg = c.player_dmg_net > 0 ? c.player_dmg_net : 0;
+          me.hp -= (me_first ? occs : occf) ? dmg : 0;
+          dl.combat += (occf ? 1 : 0) + (occs ? 1 : 0);
+          dl.eps += end ? 1 : 0;
+          tick = ft;
+          status = end ? ORX_TIE : ORX_IN_PROGRESS;
+          const int32_t ohp = pair_swap(me.hp);
+          const bool d1 = (isB ? ohp : me.hp) <= 0, d2 = (isB ? me.hp : ohp) <= 0;
+          if (d1 | d2) {  // deaths_over
+            const int32_t sw = d1 ? (d2 ? ORX_TIE : ORX_PLAYER2_WIN) : ORX_PLAYER1_WIN;
+            dl.eps += end ? 0 : 1;
+            dl.ret += (sw == ORX_PLAYER1_WIN ? 1 : 0) - (sw == ORX_PLAYER2_WIN ? 1 : 0);
+            status = sw;
+          }
+          fast = true;
+#ifdef ORX_STAMPS
+          ORX_COUNT(dl.n_meet);
+#endif
+        }
+      }
       if (PM == 2 && (in_progress & !meet & (st_me != (st_o != 0)) & !hit_me & (hit_o == 0))) {
 #ifdef ORX_STAMPS
         ORX_CYC_BEGIN(cyf);
