@@ -80,12 +80,12 @@ def rollout_kernel_name(K: int, shape: dict) -> str:
     """The kernel orx_rollout launches for this workload, as rocprofv3 names
     it: the RandomBot + trajectory specialization (PM=1), NPC capacity
     0/8/16, in the form orx_rollout_shape reports -- pair_rollout_kernel (two
-    lanes per game) or rollout_kernel -- with its store policy (AUX 2 =
-    nontemporal, 0 = default)."""
+    lanes per game, separation damage off) or rollout_kernel -- with its
+    store policy (AUX 2 = nontemporal, 0 = default)."""
     ncap = 0 if K == 0 else 8 if K <= 8 else 16
     aux = 2 if shape["nontemporal"] else 0
     if shape["lanes_per_game"] == 2:
-        return f"pair_rollout_kernel<{ncap}, 1, {aux}>"
+        return f"pair_rollout_kernel<{ncap}, 1, {aux}, false>"
     return f"rollout_kernel<{ncap}, 1, false, {aux}>"
 
 

@@ -37,8 +37,9 @@ def span(path, kernel, grid, per_step):
     """Wall span of a kernel's dispatches at one grid size (first start to
     last end) divided by the steps they make (per_step dispatches a step):
     the per-step time of launches that overlap on several streams."""
+    key = kernel.rstrip(">")   # the bench names "k<8, 1, 2>", rocprof "k<8, 1, 2, false>"
     rows = [r for r in csv.DictReader(open(path))
-            if kernel in r["Kernel_Name"] and str(grid) in (r.get("Grid_Size_X"), r.get("Grid_Size"))]
+            if key in r["Kernel_Name"] and str(grid) in (r.get("Grid_Size_X"), r.get("Grid_Size"))]
     t0 = min(int(r["Start_Timestamp"]) for r in rows)
     t1 = max(int(r["End_Timestamp"]) for r in rows)
     steps = len(rows) / per_step
