@@ -137,6 +137,36 @@ __device__ __forceinline__ W4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint
   return W4{c0, c1, c2, c3};
 }
 
+// Words a and b of a Philox block with the last round's other half deferred:
+// words c and d follow from the round-10 inputs (h0, h3) by finish_cd, for the
+// rare cases that read them (the paired rollout's common tick needs a and b).
+__device__ __forceinline__ W4 philox_ab(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                        Key key, uint32_t& h0, uint32_t& h3) {
+  uint32_t k0 = key.k0, k1 = key.k1;
+#pragma unroll
+  for (int r = 0; r < 9; ++r) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+    const uint32_t n0 = __builtin_amdgcn_bitop3_b32((uint32_t)(p1 >> 32), c1, k0, 0x96);
+    const uint32_t n2 = __builtin_amdgcn_bitop3_b32((uint32_t)(p0 >> 32), c3, k1, 0x96);
+    c1 = (uint32_t)p1;
+    c3 = (uint32_t)p0;
+    c0 = n0;
+    c2 = n2;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+  h0 = c0;
+  h3 = c3;
+  return W4{(uint32_t)__builtin_amdgcn_bitop3_b32((uint32_t)(p1 >> 32), c1, k0, 0x96), (uint32_t)p1, 0u, 0u};
+}
+__device__ __forceinline__ void finish_cd(W4& w, uint32_t h0, uint32_t h3, Key key) {
+  const uint64_t p0 = (uint64_t)0xD2511F53u * h0;
+  w.c = (uint32_t)__builtin_amdgcn_bitop3_b32((uint32_t)(p0 >> 32), h3, key.k1 + 9u * 0xBB67AE85u, 0x96);
+  w.d = (uint32_t)p0;
+}
+
 __device__ __forceinline__ uint32_t tag(uint32_t purpose, uint32_t gen) {
   return (purpose << 28) | (gen << 24);
 }
@@ -548,6 +578,24 @@ __device__ __forceinline__ void npc_any2(const Npcs<NCAP>& npc, uint32_t k1, uin
 // One key against every slot (the paired rollout's per-player test): the
 // zero-halfword test of npc_any2 on (slots ^ key:key), the two halves of the
 // running minimum folded at the end.
+// npc_any1 for a register-slot game with the NPC depth folded into the key:
+// dk = 0x80008000 when the player is not on the NPCs' depth (a half no slot
+// holds: live keys keep bit 15 clear, dead slots are 0xFFFF), 0 when it is
+template <int NCAP>
+__device__ __forceinline__ bool npc_any1_dk(const Npcs<NCAP>& npc, uint32_t k, uint32_t dk) {
+  if constexpr (NCAP == 0 || NCAP == kDense) {
+    return false;
+  } else {
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    const uint32_t KK = ((k << 16) | dk) | k;
+    u16x2 m = __builtin_bit_cast(u16x2, npc.rd(0) ^ KK);
+#pragma unroll
+    for (int r = 1; r < Npcs<NCAP>::kRegs; ++r)
+      m = __builtin_elementwise_min(m, __builtin_bit_cast(u16x2, npc.rd(r) ^ KK));
+    return __builtin_elementwise_min(m, m.yx).x == 0;
+  }
+}
+
 template <int NCAP>
 __device__ __forceinline__ bool npc_any1(const Npcs<NCAP>& npc, uint32_t k) {
   if constexpr (NCAP == 0) {
@@ -1104,6 +1152,12 @@ __device__ __forceinline__ W4 tick_block(Key key, uint32_t game, uint32_t ep, in
 __device__ __forceinline__ int32_t med3_i32(int32_t x, int32_t lo, int32_t hi) {
   int32_t r;
   asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(lo), "s"(hi));
+  return r;
+}
+// x clamped to [1, hi] (the interior's lower bound as an inline constant)
+__device__ __forceinline__ int32_t med3_1(int32_t x, int32_t hi) {
+  int32_t r;
+  asm("v_med3_i32 %0, %1, 1, %2" : "=v"(r) : "v"(x), "s"(hi));
   return r;
 }
 
@@ -2683,6 +2737,34 @@ __device__ __forceinline__ int32_t pair_swap(int32_t v) {
   return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);  // quad_perm [1, 0, 3, 2]
 }
 
+// The paired common path's exchange terms, each ONE VOP2 instruction whose
+// DPP source operand reads the other lane (quad_perm [1,0,3,2]) instead of a
+// v_mov_b32_dpp and the op: swap(kp) ^ kt, swap(kt) ^ kp, swap(kt) ^ kt and
+// swap(d) ^ d for the meet test; min(swap(z), z) for the staircase / NPC test.
+// (The compiler fuses such xors into three-input v_bitop3, which takes no DPP
+// operand on gfx950, so they are written out; the leading s_nop 1 gives the
+// two wait states a DPP read needs after a VALU write of its source.)
+__device__ __forceinline__ void meet_terms(uint32_t kp, uint32_t kt, uint32_t d, uint32_t& e_mo,
+                                           uint32_t& e_om, uint32_t& e_tt, uint32_t& e_d) {
+  asm("s_nop 1\n"
+      "v_xor_b32_dpp %0, %4, %5 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+      "v_xor_b32_dpp %1, %5, %4 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+      "v_xor_b32_dpp %2, %5, %5 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+      "v_xor_b32_dpp %3, %6, %6 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf"
+      : "=&v"(e_mo), "=&v"(e_om), "=&v"(e_tt), "=&v"(e_d)
+      : "v"(kp), "v"(kt), "v"(d));
+}
+__device__ __forceinline__ uint32_t min_swapped(uint32_t z) {
+  uint32_t r;
+  asm("s_nop 1\n"
+      "v_min_u32_dpp %0, %1, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf"
+      : "=v"(r) : "v"(z));
+  return r;
+}
+__device__ __forceinline__ uint32_t pack_cell(int32_t x, int32_t y) {
+  return (uint32_t)x | ((uint32_t)y << 8);  // the NPC slots' key form (x, y < 256)
+}
+
 // One tick's trajectory rows from a pair of lanes: each lane stores its own
 // player's x, y, depth, health and staircase (rows f and f + 4, 10/11 and
 // 12/13), lane 2j the tick and lane 2j+1 the status (rows 8 and 9), and its
@@ -2756,6 +2838,8 @@ __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kern
   me.move = ORX_MOVE_STAY;
   me.tx = me.ty = 0;
   me.mana = me.xp = me.dmg = me.mhp = me.nitems = me.cool = me.heal = me.hd = 0;
+  uint32_t kp = pack_cell(me.x, me.y), ks = pack_cell(me.sx, me.sy);  // packed cells
+  uint32_t dk = me.d == c.d1 ? 0u : 0x80008000u;  // off the NPCs' depth (npc_any1_dk)
   int32_t tick = st.tick[i];
   int32_t status = st.status[i];
   uint32_t ep = (uint32_t)st.episode[i];
@@ -2789,17 +2873,21 @@ __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kern
     }
     // the bot's move (randombot.py:20-21 / staircasebot.py:9-21)
     W4 tb = {0u, 0u, 0u, 0u};
+    uint32_t h0 = 0u, h3 = 0u;  // PM 1: the tick block's deferred words c, d
     int32_t move;
     if constexpr (PM == 1) {
       // the tick block in both lanes; player 1 takes the first accepted 3-bit
       // field of word b, player 2 the second (as rollout_tick)
-      tb = tick_block(key, game, ep, tick);
+      tb = philox_ab(game, ep, (uint32_t)tick, tag(PUR_TICK, 0), key, h0, h3);
       const uint32_t acc = accepted3(tb.b);
       const uint32_t acc2 = acc & (acc - 1u);
-      move = (int32_t)((tb.b >> (ffbl(isB ? acc2 : acc) & 31u)) & 7u) + 1;
+      // (v_bfe_u32 reads its offset's low 5 bits: ffbl's 0xFFFFFFFF for an
+      // empty mask needs no mask, the value is then replaced below)
+      move = (int32_t)__builtin_amdgcn_ubfe(tb.b, ffbl(isB ? acc2 : acc), 3u) + 1;
       if (ORX_UNLIKELY(acc2 == 0u)) {  // the game's word b holds fewer than two
         int32_t r0 = ORX_MOVE_STAY, r1 = ORX_MOVE_STAY;
         bool err = false;
+        finish_cd(tb, h0, h3, key);
         moves_from_block(tb, 2, key, game, ep, tick, r0, r1, err);
         move = isB ? r1 : r0;
       }
@@ -2814,25 +2902,22 @@ __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kern
     // effective target (own cell when blocked: the border, clamped)
     int32_t tx, ty;
     calc_pos(me.x, me.y, move, tx, ty);
-    tx = med3_i32(tx, 1, c.W - 2);
-    ty = med3_i32(ty, 1, c.H - 2);
-    // the other player of the pair
-    const int32_t ox = pair_swap(me.x), oy = pair_swap(me.y), od = pair_swap(me.d);
-    const int32_t otx = pair_swap(tx), oty = pair_swap(ty);
-    const bool st_me = (tx == me.sx) & (ty == me.sy);
-    const int32_t st_o = pair_swap(st_me ? 1 : 0);
-    const uint32_t e_mo = (uint32_t)(tx ^ ox) | (uint32_t)(ty ^ oy);
-    const uint32_t e_om = (uint32_t)(otx ^ me.x) | (uint32_t)(oty ^ me.y);
-    const uint32_t e_tt = (uint32_t)(tx ^ otx) | (uint32_t)(ty ^ oty);
-    const bool meet = ((uint32_t)(me.d ^ od) | min(e_mo, min(e_om, e_tt))) == 0u;
-    // an NPC on the own target (NPC keys x | y << 8; all NPCs on depth d1)
+    tx = med3_1(tx, c.W - 2);
+    ty = med3_1(ty, c.H - 2);
+    const uint32_t kt = pack_cell(tx, ty);
+    // The rare test on packed cells (x | y << 8): a meet is both players on
+    // one depth with my target on the other's cell, the other's target on
+    // mine, or one target for both -- symmetric, so both lanes decide alike
+    // -- and either player's target holding its staircase or an NPC (NPC keys
+    // x | y << 8, all NPCs on depth d1).  Each term reads the other lane
+    // through its own DPP source operand.
+    uint32_t e_mo, e_om, e_tt, e_d;
+    meet_terms(kp, kt, (uint32_t)me.d, e_mo, e_om, e_tt, e_d);
+    const uint32_t mt = min(e_mo, min(e_om, e_tt)) | e_d;  // 0: a meet
     bool hit_me = false;
-    int32_t hit_o = 0;
-    if constexpr (NCAP > 0) {
-      hit_me = (me.d == c.d1) & npc_any1(npc, (uint32_t)tx | ((uint32_t)ty << 8));
-      hit_o = pair_swap(hit_me ? 1 : 0);
-    }
-    const bool rare = !in_progress | meet | st_me | (st_o != 0) | hit_me | (hit_o != 0);
+    if constexpr (NCAP > 0) hit_me = npc_any1_dk(npc, kt, dk);
+    const uint32_t z = hit_me ? 0u : (kt ^ ks);  // 0: my staircase or an NPC on my target
+    const bool rare = !in_progress | (min(mt, min_swapped(z)) == 0u);
     const int32_t ft = tick + 1;
     const bool end = c.max_ticks && ft >= c.max_ticks;
     bool took_ordered = false;
@@ -2841,6 +2926,32 @@ __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kern
       ORX_COUNT(dl.n_rare);
       ORX_CYC_BEGIN(cy0);
 #endif
+      if constexpr (PM == 1) {  // the tick block's words c and d (rare_tick's fallbacks)
+        asm volatile("" : "+v"(h0), "+v"(h3));
+        finish_cd(tb, h0, h3, key);
+      }
+      // The pre-tick cell and tick, rebuilt from kp and ft: the common path
+      // then needs neither past its target and the next tick's values take
+      // their registers (no copies at the loop's back edge).
+      {
+        uint32_t k0 = kp;
+        int32_t f0 = ft;
+        asm volatile("" : "+v"(k0), "+v"(f0));
+        me.x = (int32_t)(k0 & 0xFFu);
+        me.y = (int32_t)(k0 >> 8);
+        tick = f0 - 1;
+      }
+      // the terms one by one, from laundered copies (the common path's
+      // swaps stay folded into their ops)
+      int32_t lx = me.x, ly = me.y, ld = me.d, ltx = tx, lty = ty, lsx = me.sx, lsy = me.sy;
+      launder(lx, ly, ld, ltx);
+      asm volatile("" : "+v"(lty), "+v"(lsx), "+v"(lsy));
+      const int32_t ox = pair_swap(lx), oy = pair_swap(ly), od = pair_swap(ld);
+      const int32_t otx = pair_swap(ltx), oty = pair_swap(lty);
+      const bool meet = mt == 0u;
+      const bool st_me = (ltx == lsx) & (lty == lsy);
+      const int32_t st_o = pair_swap(st_me ? 1 : 0);
+      const int32_t hit_o = pair_swap(hit_me ? 1 : 0);
       // One player descends (C5's common rare tick; StaircaseBots only),
       // fast_descend's rules split over the pair: the descender's lane draws the tick's SPAWN
       // block, the other lane the new depth's DUNGEON block -- one Philox
@@ -3044,9 +3155,14 @@ __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kern
         me = pick(isB, p2, p1);
         me.move = move;
       }
+      kp = pack_cell(me.x, me.y);
+      ks = pack_cell(me.sx, me.sy);
+      dk = me.d == c.d1 ? 0u : 0x80008000u;
 #ifdef ORX_STAMPS
       ORX_CYC_END(dl.cy_rare, cy0);
 #endif
+    } else {
+      kp = kt;
     }
     // the common tick: the move to the effective target
     me.x = rare ? me.x : tx;
@@ -3078,7 +3194,7 @@ __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kern
       }
     }
     if (!(ORX_DIAG & 16)) traj.write(me, isB ? status : tick, move);
-  } while (++t < n_ticks);
+    } while (++t < n_ticks);
   ORX_STAMP(3);
   st.p_x[who * B + i] = me.x;
   st.p_y[who * B + i] = me.y;
