@@ -66,8 +66,9 @@ def bytes_per_game(kernel: str, K: int, ticks: int = 1) -> int:
     npc_read = (4 + 2 * K) if K else 0        # alive mask + K packed u16 positions
     if kernel == "step":
         # read: actions 2, players 32, staircases 16, tick/status/episode 12, NPCs
-        # write: players 32, tick 4, status 4
-        return 2 + 32 + 16 + 12 + npc_read + 40
+        # write: positions 16, tick 4 (depth, health and status only where they
+        # changed: a descend, a combat, an episode end -- rare per game-tick)
+        return 2 + 32 + 16 + 12 + npc_read + 20
     if kernel == "policy":
         return 4 + 4 + 2                       # tick, episode -> 2 int8 actions
     # players, staircases, tick/status/episode, NPC positions + alive mask + health
