@@ -1775,21 +1775,22 @@ __device__ __forceinline__ void store_players(const orx_state_t& st, uint32_t B,
   }
 }
 
-// store_players after a tick of step_kernel: depth and health rows are
-// written only by the games whose values changed (a descend, a combat), so
-// the per-tick step moves 16 B less per game on most ticks
+// store_players after a tick of step_kernel: the depth rows (and the
+// staircases) only when a player descended, the health rows only when `hp`
+// (a combat, under the reference's rules; always with extensions, which
+// change health in more ways), so the per-tick step moves 16 B less per game
+// on most ticks
 template <bool GRID = false>
 __device__ __forceinline__ void store_players_tick(const orx_state_t& st, uint32_t B, uint32_t i,
                                                    const Player& p1, const Player& p2,
-                                                   const Player& o1, const Player& o2,
-                                                   bool stairs) {
+                                                   bool descended, bool hp) {
   st.p_x[i] = p1.x;           st.p_x[B + i] = p2.x;
   st.p_y[i] = p1.y;           st.p_y[B + i] = p2.y;
-  if (p1.d != o1.d) st.p_depth[i] = p1.d;
-  if (p2.d != o2.d) st.p_depth[B + i] = p2.d;
-  if (p1.hp != o1.hp) st.p_health[i] = p1.hp;
-  if (p2.hp != o2.hp) st.p_health[B + i] = p2.hp;
-  if (stairs) {
+  if (hp) {
+    st.p_health[i] = p1.hp;   st.p_health[B + i] = p2.hp;
+  }
+  if (descended) {
+    st.p_depth[i] = p1.d;     st.p_depth[B + i] = p2.d;
     st.st_x[i] = p1.sx;       st.st_x[B + i] = p2.sx;
     st.st_y[i] = p1.sy;       st.st_y[B + i] = p2.sy;
     if constexpr (GRID) {
@@ -1933,7 +1934,10 @@ __global__ void __launch_bounds__(256) reset_kernel(orx_cfg_t hc, orx_state_t st
   }
 }
 
-template <int NCAP, bool EV, bool GRID>
+// EXT = false: the reference's rules only (cfg.flags == 0), the extension
+// code compiled out -- fewer registers, so more waves per SIMD hide the
+// state loads (the per-tick drop-in's common case)
+template <int NCAP, bool EV, bool GRID, bool EXT = true>
 __global__ void __launch_bounds__(256) step_kernel(orx_cfg_t hc, orx_state_t st,
                                                    const int8_t* __restrict__ actions, uint32_t B,
                                                    Key key, uint32_t off,
@@ -1941,7 +1945,8 @@ __global__ void __launch_bounds__(256) step_kernel(orx_cfg_t hc, orx_state_t st,
                                                    int32_t* __restrict__ n_events) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= B) return;
-  const Cfg c = make_cfg(hc, st);
+  Cfg c = make_cfg(hc, st);
+  if constexpr (!EXT) c.ext = 0;
   const uint32_t game = off + i;
   int32_t status = st.status[i];
   Npcs<NCAP> npc;
@@ -1978,7 +1983,6 @@ __global__ void __launch_bounds__(256) step_kernel(orx_cfg_t hc, orx_state_t st,
   const uint32_t ep = (uint32_t)st.episode[i];
   int32_t tick = st.tick[i];
   load_players<GRID>(st, B, i, p1, p2);
-  const Player o1 = p1, o2 = p2;  // the pre-tick players (store_players_tick)
   load_npcs(st, c, B, i, npc);
   Items<NCAP> items;
   load_rpg(st, c, B, i, p1, p2, npc, items);
@@ -1992,7 +1996,7 @@ __global__ void __launch_bounds__(256) step_kernel(orx_cfg_t hc, orx_state_t st,
                             dl, ev, sep);
   if (c.ext & ORX_EXT_SEPARATION_DAMAGE) st.sep_start[i] = sep;
   store_rpg(st, c, B, i, p1, p2, npc, items);
-  store_players_tick<GRID>(st, B, i, p1, p2, o1, o2, dl.descend != 0);
+  store_players_tick<GRID>(st, B, i, p1, p2, dl.descend != 0, EXT ? true : dl.combat != 0);
   st.tick[i] = tick;
   if (status != ORX_IN_PROGRESS) st.status[i] = status;  // (it was InProgress)
   if (NCAP > 0 && dl.npc_death) npc.store_alive(st.npc_alive, B, i);
@@ -3909,6 +3913,18 @@ static int launch_step(const orx_cfg_t* cfg, const orx_state_t* st, const int8_t
   const int nc = ncap_for(cfg->n_npcs);
   const bool grid = cfg->n_layouts > 0;
   const bool mt = cfg->rng == ORX_RNG_MT19937;
+  if (!ev && !grid && !mt && cfg->flags == 0 && nc != kDense) {  // the reference's rules
+    if (nc == 0)
+      hipLaunchKernelGGL((step_kernel<0, false, false, false>), grid_for(B), dim3(kBlock), 0, s,
+                         *cfg, *st, actions, B, k, off, events, n_events);
+    else if (nc == 8)
+      hipLaunchKernelGGL((step_kernel<8, false, false, false>), grid_for(B), dim3(kBlock), 0, s,
+                         *cfg, *st, actions, B, k, off, events, n_events);
+    else
+      hipLaunchKernelGGL((step_kernel<16, false, false, false>), grid_for(B), dim3(kBlock), 0, s,
+                         *cfg, *st, actions, B, k, off, events, n_events);
+    return launch_status(name);
+  }
 #define ORX_STEP(NC, E, G)                                                                      \
   if (nc == NC && ev == E && grid == G) {                                                      \
     if (mt)                                                                                     \
