@@ -1,8 +1,12 @@
 #!/usr/bin/env python3
 """bench.py -- env-steps/s of the batched Optimax Rogue tick engine on MI355X.
 
-    python bench.py [--gpus N --steps K --warmup W]          # 1 GPU
+    python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+`--gpus N` outside torchrun starts the N rank processes itself (one per GPU,
+torch.distributed.run on 127.0.0.1, before this process touches the GPU) and
+exits with their code; under torchrun WORLD_SIZE must equal N.
 
 Workload (BASELINE.json configs[2], "C3"): 65,536 games per GPU on a 64x64
 grid with enemies (K = 8 NPCs per game), both players driven by RandomBot,
@@ -147,13 +151,13 @@ def cpu_baseline(cfg_dict: dict, seconds: float) -> dict:
     total = sum(B * n for n, _ in res.values())
     ref = None
     if os.path.exists(REF_CPU_FILE):
-        r = json.load(open(REF_CPU_FILE))
-        full = r["full"]
+        rj = json.load(open(REF_CPU_FILE))
+        full = rj["full"]
         ref = {"value": full["aggregate_env_steps_per_s"], "unit": "env-steps/s",
                "cores": full["procs"], "per_core": full["per_core_env_steps_per_s"],
-               "single_core": full["single_core_env_steps_per_s"], "host": r["host"],
+               "single_core": full["single_core_env_steps_per_s"], "host": rj["host"],
                "where": "build container (the reference cannot run on the GPU box)",
-               "sample": f"{r['workload']}; the reference's RandomBot.move x2 + on_tick + "
+               "sample": f"{rj['workload']}; the reference's RandomBot.move x2 + on_tick + "
                          f"Updater.update, one process per core for "
                          f"{full['seconds_per_proc']} s each ({full['env_steps']} env-steps); "
                          "tools/ref_cpu_baseline.py -> profiles/ref_cpu_c3.json"}
@@ -171,6 +175,17 @@ def cpu_baseline(cfg_dict: dict, seconds: float) -> dict:
             {"error": r.stderr[-500:]}
     except (subprocess.SubprocessError, ValueError, IndexError) as e:
         pyr = {"error": repr(e)}
+    # the restatement's cost relative to the reference's on one host (the
+    # build container, tools/ref_cpu_baseline.py): the reference's own rate on
+    # THIS host's cores, estimated as python_restatement / that ratio
+    if ref is not None and "pyref_vs_reference" in rj and "per_core" in (pyr or {}):
+        ratio = rj["pyref_vs_reference"]
+        ref["pyref_vs_reference"] = {k: ratio[k] for k in ("single_core", "per_core")}
+        pyr["reference_estimate_here"] = {
+            "per_core": pyr["per_core"] / ratio["per_core"],
+            "value": pyr["value"] / ratio["per_core"], "cores": pyr["cores"],
+            "note": "python_restatement / pyref_vs_reference.per_core (both legs measured on "
+                    "one host): the reference updater's estimated rate on this box's cores"}
     return {"value": total / el, "unit": "env-steps/s", "cores": cores, "kind": "port",
             "python_restatement": pyr,
             "reference_python": ref,
@@ -317,6 +332,55 @@ def extras(torch, cfg, dev, B_cfg, K, large_rollout=False):
     return out
 
 
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int, argv, same_device: bool = False) -> int:
+    """`--gpus N` outside torchrun: N rank processes, one per GPU, started
+    before this process touches the GPU (torch.distributed.run on 127.0.0.1,
+    the same form the driver uses), with this script's own arguments; returns
+    their exit code.  Rank 0's JSON line goes straight to this stdout.
+    torch.cuda.device_count() does not initialize the GPU on this image."""
+    import torch
+    if not same_device:
+        have = torch.cuda.device_count()
+        if have < n:
+            raise SystemExit(f"--gpus {n}: only {have} GPU(s) visible (use --same-device to "
+                             "rehearse N ranks on one card)")
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__)] + list(argv)
+    return subprocess.call(cmd, env=env)
+
+
+def launch_check(args) -> None:
+    """--launch-check: the rank plumbing alone, no GPU (a CPU test of
+    launch_ranks): every rank joins a gloo group, rank 0 prints the line's
+    n_gpus and ranks entries."""
+    import torch.distributed as dist
+    from optimax_rogue_amd.parallel import env_rank, init, shard
+    rank, world, local = env_rank()
+    init("gloo" if world > 1 else None)
+    G = args.global_batch if args.strong else args.batch * world
+    offset, count = shard(G, rank, world)
+    mine = {"rank": rank, "local_rank": local, "offset": offset, "count": count}
+    ranks = [mine]
+    if world > 1:
+        ranks = [None] * world
+        dist.all_gather_object(ranks, mine)
+    if rank == 0:
+        print(json.dumps({"n_gpus": world, "global_batch": G, "ranks": ranks}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -344,9 +408,19 @@ def main():
                     help="nccl (= RCCL, default) or gloo (multi-rank rehearsal on one GPU)")
     ap.add_argument("--same-device", action="store_true",
                     help="every rank uses cuda:0 (rehearsing N ranks on a 1-GPU box)")
+    ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
-    if args.steps < 1 or args.chunk < 1 or args.warmup < 0:
-        raise SystemExit("--steps and --chunk must be >= 1, --warmup >= 0")
+    if args.steps < 1 or args.chunk < 1 or args.warmup < 0 or args.gpus < 1:
+        raise SystemExit("--gpus, --steps and --chunk must be >= 1, --warmup >= 0")
+    # --gpus N: under torchrun the world size must be N; outside it this
+    # process starts the N ranks itself (before any GPU call) and waits
+    if "WORLD_SIZE" in os.environ:
+        if int(os.environ["WORLD_SIZE"]) != args.gpus:
+            raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']}")
+    elif args.gpus > 1:
+        raise SystemExit(launch_ranks(args.gpus, sys.argv[1:], args.same_device))
+    if args.launch_check:
+        return launch_check(args)
 
     import torch
     import torch.distributed as dist

@@ -335,8 +335,10 @@ int orx_rollout_lanes(int64_t n_games);
 
 /* The shape of an orx_rollout launch with these arguments (trajectory:
  * obs and act both given): games per wave (1..64), lanes per game (2 for the
- * paired form -- no NPCs, no dungeon bank, two RandomBots or two
- * StaircaseBots, batches below 64 games per wave: one lane per player) and
+ * paired form -- no dense NPCs (n_npcs <= ORX_MAX_REG_NPCS, held in
+ * registers), no dungeon bank, two RandomBots or two StaircaseBots, batches
+ * below 64 games per wave: one lane per player; the bench's C3 shards run
+ * pair_rollout_kernel<8, 1, 2, false>) and
  * whether the trajectory rows are stored nontemporal (whole-line row
  * segments) or with the default policy; concurrency as in
  * orx_rollout_concurrent (1 for orx_rollout).  Results never depend on it.
@@ -356,8 +358,12 @@ int orx_rollout_shape(const orx_cfg_t* cfg, int32_t policy_p1, int32_t policy_p2
  * reference can play to max_ticks is played; with max_ticks == 0 (no limit)
  * or max_ticks > ORX_DSTORE_MAX a game whose lagging player still has to
  * enter a dungeon more than N levels behind the other stops with
- * ORX_STATUS_RNG_EXHAUSTED instead of inventing a staircase.  Replaces
- * nothing: the reference keeps World.dungeons in a dict (world.py:101-180). */
+ * ORX_STATUS_RNG_EXHAUSTED instead of inventing a staircase.  Cost: 16 * N
+ * bytes per game (16 KiB at max_ticks 1000, 64 KiB with no limit, 1 MiB at
+ * the 65,536-depth cap), all of it cleared by orx_seed_mt -- size stock-seed
+ * batches for it (BatchedEngine warns above a quarter of the device's
+ * memory).  Replaces nothing: the reference keeps World.dungeons in a dict
+ * (world.py:101-180). */
 int orx_dstore_depths(const orx_cfg_t* cfg);
 
 /* Message for the last non-zero return on this thread ("" if none). */

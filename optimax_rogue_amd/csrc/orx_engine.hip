@@ -2565,6 +2565,9 @@ constexpr int32_t kStreamAux = ORX_STREAM_AUX;  // cache policy: nt (measured, D
 // us per launch with nt, 79 plain), so those launches store with the default
 // policy (kPartialAux)
 constexpr int32_t kPartialAux = 0;
+// the launch tables pick an instance by (AUX == kStreamAux) == nt: equal
+// policies would leave one store form with no instance
+static_assert(kStreamAux != kPartialAux, "ORX_STREAM_AUX must differ from the partial-line policy");
 template <bool FAST, int AUX = kStreamAux>
 struct TrajWriter {
   int32_t* obs;
@@ -2834,7 +2837,9 @@ struct PairWriter {
 };
 
 // PM 1: both players RandomBot (no extension flags); PM 2: both StaircaseBot
-// (at most separation damage).  NCAP 0, empty dungeons, obs and act given.
+// (at most separation damage).  NCAP 0 / 8 / 16 (register NPCs, no dense
+// grid), empty dungeons, obs and act given.  The bench's C3 shards run
+// pair_rollout_kernel<8, 1, 2, false>.
 // (diagnostic builds may add attributes, e.g. an occupancy target)
 #ifndef ORX_PAIR_ATTR
 #define ORX_PAIR_ATTR
@@ -3760,7 +3765,8 @@ int rollout_pm(const orx_cfg_t* cfg, int32_t p1, int32_t p2, uint32_t B, bool tr
          : (cfg->flags == 0 && both_random) ? 1
          : ((cfg->flags & ~ORX_EXT_SEPARATION_DAMAGE) == 0 && p1 == ORX_POLICY_STAIRCASE &&
             p2 == ORX_POLICY_STAIRCASE) ? 2
-         : ((cfg->flags | ORX_EXT_HEAL) == ORX_EXT_RPG && both_random) ? 3
+         : ((cfg->flags | ORX_EXT_HEAL) == ORX_EXT_RPG && both_random &&
+            ncap_for(cfg->n_npcs) != kDense) ? 3   // (no dense-NPC instance of PM 3)
          : 0;
 }
 
@@ -3771,7 +3777,7 @@ struct RolloutPlan {
   bool nt;         // nontemporal trajectory stores (whole-line row segments)
 };
 
-// The paired form: no NPCs, no bank, the RandomBot or StaircaseBot trajectory
+// The paired form: no dense NPCs (K <= 16), no bank, the RandomBot or StaircaseBot trajectory
 // forms (PM 1 / 2), for batches the one-lane rule leaves below 64 games per
 // wave; its games per wave: two waves per SIMD -- counting the `concurrency`
 // launches that share the device (StreamShardedEngine's shards) -- until the
@@ -4042,16 +4048,19 @@ int orx_rollout_concurrent(const orx_cfg_t* cfg, const orx_state_t* st, int32_t 
       lds += per_block * bb;
     }
   }
-  // the paired form (two lanes per game, pair_rollout_kernel): no NPCs, no
-  // bank, the RandomBot or StaircaseBot trajectory forms, at most 32 games
+  // the paired form (two lanes per game, pair_rollout_kernel): no dense NPCs
+  // (K <= 16 in registers), no bank, the RandomBot or StaircaseBot trajectory
+  // forms, at most 32 games
   // per wave (env ORX_ROLLOUT_PAIRED=0 turns it off, for measurements)
   if (plan.paired) {
     const dim3 blocks((B + per_block - 1) / per_block);
     const bool sepd = pm == 2 && (cfg->flags & ORX_EXT_SEPARATION_DAMAGE) != 0;
 #define ORX_PAIR(N, P, A, S)                                                                    \
-    if (nc == N && pm == P && (A == kStreamAux) == nt && S == sepd)                             \
+    if (nc == N && pm == P && (A == kStreamAux) == nt && S == sepd) {                           \
       hipLaunchKernelGGL((pair_rollout_kernel<N, P, A, S>), blocks, dim3(threads), 0, s, *cfg,  \
-                         *st, n_ticks, obs, act, B, k, off, lanes);
+                         *st, n_ticks, obs, act, B, k, off, lanes);                             \
+      return launch_status("orx_rollout");                                                      \
+    }
 #define ORX_PAIRS(N)                                                                            \
     ORX_PAIR(N, 1, kStreamAux, false) ORX_PAIR(N, 1, kPartialAux, false)                        \
     ORX_PAIR(N, 2, kStreamAux, false) ORX_PAIR(N, 2, kPartialAux, false)                        \
@@ -4059,7 +4068,7 @@ int orx_rollout_concurrent(const orx_cfg_t* cfg, const orx_state_t* st, int32_t 
     ORX_PAIRS(0) ORX_PAIRS(8) ORX_PAIRS(16)
 #undef ORX_PAIRS
 #undef ORX_PAIR
-    return launch_status("orx_rollout");
+    return fail(ORX_EIO, "orx_rollout: no paired kernel instance for this plan");
   }
 #define ORX_ROLLOUT_A(N, P, G, A)                                                               \
   if (nc == N && pm == P && grid == G && (P == 0 || (A == kStreamAux) == nt)) {                \
@@ -4091,7 +4100,7 @@ int orx_rollout_concurrent(const orx_cfg_t* cfg, const orx_state_t* st, int32_t 
   ORX_ROLLOUT(kDense, 0, false) ORX_ROLLOUT(kDense, 1, false) ORX_ROLLOUT(kDense, 2, false)
   ORX_ROLLOUT(kDense, 0, true) ORX_ROLLOUT(kDense, 1, true) ORX_ROLLOUT(kDense, 2, true)
 #undef ORX_ROLLOUT
-  return launch_status("orx_rollout");
+  return fail(ORX_EIO, "orx_rollout: no rollout kernel instance for this plan");
 }
 
 #ifdef ORX_STAMPS

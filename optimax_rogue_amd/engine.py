@@ -103,6 +103,7 @@ class BatchedEngine:
             self.mt_py, self.mt_np = z(625, B), z(625, B)
             n = int(self.lib.orx_dstore_depths(ctypes.byref(self._ccfg)))
             _lib.check("orx_dstore_depths", min(n, 0))
+            self._warn_dstore(n)
             self.dstore = z(2, n, 2, B)
             ptrs.update({f: getattr(self, f).data_ptr() for f in ("mt_py", "mt_np", "dstore")})
         # the readme's character mechanics (EXT_CHARACTER flags): player attributes
@@ -131,6 +132,20 @@ class BatchedEngine:
             self.reset()
 
     # -- plumbing -----------------------------------------------------------
+    def _warn_dstore(self, n_depths: int) -> int:
+        """Stock-seed mode's dungeon store costs 16 * N bytes per game (N =
+        orx_dstore_depths >= max_ticks; orx_seed_mt clears all of it): warns
+        when the batch's store exceeds a quarter of the device's memory.
+        Returns the store's bytes."""
+        import warnings
+        nbytes = 16 * int(n_depths) * self.B
+        total = torch.cuda.get_device_properties(self.device).total_memory
+        if nbytes > total // 4:
+            warnings.warn(f"stock-seed dungeon store: {nbytes / 2**30:.1f} GiB for {self.B} games "
+                          f"({16 * n_depths} B per game at max_ticks {self.cfg.max_ticks}), more "
+                          f"than a quarter of {self.device}'s memory", RuntimeWarning)
+        return nbytes
+
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 

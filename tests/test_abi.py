@@ -179,10 +179,11 @@ def test_engine_refuses_cpu():
 
 def test_rollout_shape_rules(lib):
     """orx_rollout_shape (no device work; 1,024 SIMDs assumed without a GPU):
-    the paired two-lanes-per-game form for NPC-free RandomBot / StaircaseBot
-    trajectory launches below 64 games per wave (counting the launches that
-    share the device), nontemporal stores only for
-    whole-line row segments (32+ games per wave)."""
+    the paired two-lanes-per-game form for RandomBot / StaircaseBot
+    trajectory launches without dense NPCs (K <= 16, register slots) below 64
+    games per wave (counting the launches that share the device; the bench's
+    C3 shards: pair_rollout_kernel<8, 1, 2, false>), nontemporal stores only
+    for whole-line row segments (32+ games per wave)."""
     from optimax_rogue_amd import EnvConfig
     from optimax_rogue_amd._lib import OrxRolloutShape
 

@@ -87,6 +87,28 @@ def test_c4_eight_shards_equal_whole_batch():
     torch.cuda.synchronize()
 
 
+def test_bench_gpus_2_runs_two_ranks():
+    """`python bench.py --gpus 2` (no torchrun around it) starts two ranks by
+    itself: here both on cuda:0 with the gloo gather (--same-device; RCCL takes
+    one rank per device), as the driver's SCALE run does with one GPU each.
+    The line reports n_gpus 2, both ranks' shards and the returns gather."""
+    root = os.path.dirname(HERE)
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="1")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2",
+                        "--same-device", "--dist-backend", "gloo", "--batch", "8192",
+                        "--steps", "2", "--warmup", "1", "--no-extras", "--no-cpu-baseline"],
+                       env=env, capture_output=True, text=True, timeout=110, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["config"]["global_batch"] == 16384
+    assert [(x["rank"], x["offset"], x["count"]) for x in line["ranks"]] == \
+        [(0, 0, 8192), (1, 8192, 8192)]
+    assert line["returns_gather_ms"] is not None and line["returns_gather_backend"] == "gloo"
+    assert line["value"] > 0
+
+
 def test_rccl_process_group_on_the_device():
     """The nccl (= RCCL) path of parallel.init / gather_returns on hardware:
     a process group bound to cuda:0 (init_process_group's device_id), the

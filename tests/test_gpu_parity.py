@@ -447,10 +447,68 @@ def test_c3_full_size_properties(oracle_lib):
         compare_state(got, ora.export(), 8, f"gid {gid}")
 
 
+def _timed_form_vs_oracle(oracle_lib, eng, parts, obs, act, launch, cfg, pol, seed, T, L,
+                          starts):
+    """Runs ``launch`` (a pre-bound rollout launcher over ``parts``, each with
+    its obs/act buffers) L times as bench.py issues it, and replays 8-game
+    windows of consecutive global ids starting at ``starts`` on the oracle
+    tick by tick: every tick's 14-field observation row and both actions of
+    every launch, and the whole state after each launch.  Returns the last
+    snapshot and the sampled global ids."""
+    import torch
+    dev = parts[0].device
+    gids = np.concatenate([np.arange(s, s + 8) for s in starts])
+    oras = []
+    for s in starts:
+        o = oracle_lib.Oracle(cfg.to_dict(), 8, seed, s)
+        o.reset(episode=np.zeros(8, np.int32))
+        oras.append(o)
+    # per shard: which sampled ids it holds, at which local index
+    sel = []
+    for e in parts:
+        loc = gids - e.game_offset
+        m = (loc >= 0) & (loc < e.B)
+        sel.append((np.nonzero(m)[0], torch.from_numpy(loc[m]).to(dev)))
+    sharded = hasattr(eng, "fork")
+    for n in range(L):
+        if sharded:
+            eng.fork()
+        launch()
+        if sharded:
+            eng.join()
+        torch.cuda.synchronize()
+        g_obs = np.zeros((T, 14, len(gids)), np.int32)
+        g_act = np.zeros((T, len(gids), 2), np.int8)
+        for (pos, li), o, a in zip(sel, obs, act):
+            g_obs[:, :, pos] = o.index_select(2, li).cpu().numpy()
+            g_act[:, pos] = a.index_select(1, li).cpu().numpy()
+        snap = eng.snapshot()
+        for w, (s, ora) in enumerate(zip(starts, oras)):
+            cols = slice(8 * w, 8 * w + 8)
+            w_act, w_obs = _replay(ora, T, pol)
+            where = f"launch {n} ids {s}..{s + 7}"
+            assert np.array_equal(g_act[:, cols], w_act), f"{where}: actions"
+            assert np.array_equal(g_obs[:, :, cols], w_obs), f"{where}: observation rows"
+            got = {k: v[..., s:s + 8] for k, v in snap.items()}
+            compare_state(got, ora.export(), cfg.n_npcs, f"{where}: state")
+    return snap, gids
+
+
+def _window_starts(B, shard_size, n_random, seed):
+    """Both ends of every shard plus n_random 8-aligned windows inside."""
+    ends = []
+    for off in range(0, B, shard_size):
+        ends += [off, off + shard_size - 8]
+    rng = np.random.default_rng(seed)
+    pool = np.setdiff1d(np.arange(8, B - 8, 8), ends)
+    return sorted(set(ends) | {int(x) for x in rng.choice(pool, n_random, replace=False)})
+
+
 def test_bench_timed_path_vs_oracle(oracle_lib):
     """bench.py's timed path exactly: StreamShardedEngine(C3, 65,536 games,
     seed 3, two stream shards of 32,768) launched through rollout_launcher
-    with both trajectory buffers -- rollout_kernel<8, 1, false> (PM=1) at 32
+    with both trajectory buffers -- pair_rollout_kernel<8, 1, 2, false> (two
+    lanes per game, register NPCs, RandomBots, nontemporal stores) at 32
     games per wave -- for 9 back-to-back 128-tick launches (1,152 ticks: every
     game crosses the max_ticks-1000 autoreset), as bench.py issues them (fork,
     launches, join).  128 games -- 16 windows of 8 consecutive global ids,
@@ -470,42 +528,59 @@ def test_bench_timed_path_vs_oracle(oracle_lib):
                                        "nontemporal": True}   # the form bench.py times
     obs, act = eng.trajectory_buffers(T)
     launch = eng.rollout_launcher(T, 1, 1, obs=obs, act=act)
-    rng = np.random.default_rng(7)
-    starts = [0, 32760, 32768, 65528] + sorted(
-        int(x) for x in rng.choice(np.arange(8, 65520, 8), 12, replace=False))
-    gids = np.concatenate([np.arange(s, s + 8) for s in starts])
-    oras = []
-    for s in starts:
-        o = oracle_lib.Oracle(cfg.to_dict(), 8, seed, s)
-        o.reset(episode=np.zeros(8, np.int32))
-        oras.append(o)
-    # per shard: which sampled ids it holds, at which local index
-    sel = []
-    for e in eng.parts:
-        loc = gids - e.game_offset
-        m = (loc >= 0) & (loc < e.B)
-        sel.append((np.nonzero(m)[0], torch.from_numpy(loc[m]).to(dev)))
-    for n in range(L):
-        eng.fork()
-        launch()
-        eng.join()
-        torch.cuda.synchronize()
-        g_obs = np.zeros((T, 14, len(gids)), np.int32)
-        g_act = np.zeros((T, len(gids), 2), np.int8)
-        for (pos, li), o, a in zip(sel, obs, act):
-            g_obs[:, :, pos] = o.index_select(2, li).cpu().numpy()
-            g_act[:, pos] = a.index_select(1, li).cpu().numpy()
-        snap = eng.snapshot()
-        for w, (s, ora) in enumerate(zip(starts, oras)):
-            cols = slice(8 * w, 8 * w + 8)
-            w_act, w_obs = _replay(ora, T)
-            where = f"launch {n} ids {s}..{s + 7}"
-            assert np.array_equal(g_act[:, cols], w_act), f"{where}: actions"
-            assert np.array_equal(g_obs[:, :, cols], w_obs), f"{where}: observation rows"
-            got = {k: v[..., s:s + 8] for k, v in snap.items()}
-            compare_state(got, ora.export(), cfg.n_npcs, f"{where}: state")
+    starts = _window_starts(B, 32768, 12, 7)
+    snap, gids = _timed_form_vs_oracle(oracle_lib, eng, eng.parts, obs, act, launch, cfg,
+                                       (1, 1), seed, T, L, starts)
     # every sampled game went through the max_ticks autoreset in the timed form
     assert (snap["ep_count"][gids] >= 1).all() and (snap["episode"][gids] >= 1).all()
+
+
+# bench.py's extras at their timed shapes (bench.extras: rollout_rate, seed 5,
+# one BatchedEngine, 128-tick launches with both trajectory buffers): the
+# form each one launches (lanes per game, nontemporal stores), and 9 launches
+# = 1,152 ticks, past the max_ticks-1000 autoreset
+EXTRAS_FORMS = {
+    # C2: pair_rollout_kernel<0, 1, 0, false>
+    "c2_4096": ("c2", 0, 4096, (1, 1), 2, False),
+    # C5 at its 8-GPU share: pair_rollout_kernel<0, 2, 0, false / true>
+    "c5_16384_sep_off": ("c5", 0, 16384, (2, 2), 2, False),
+    "c5_16384_sep_on": ("c5", 1, 16384, (2, 2), 2, False),
+    # C5 on one GPU: the one-lane rollout_kernel at 64 games per wave, nt stores
+    "c5_131072_sep_off": ("c5", 0, 131072, (2, 2), 1, True),
+    "c5_131072_sep_on": ("c5", 1, 131072, (2, 2), 1, True),
+}
+
+
+@pytest.mark.parametrize("name", sorted(EXTRAS_FORMS))
+def test_bench_extras_timed_forms_vs_oracle(name, oracle_lib):
+    """Each extras line of bench.py in the exact form it is timed (C2's
+    4,096 games on 32x32; C5's 16,384 and 131,072 games on 128x128 with
+    StaircaseBots, separation damage off -- reference semantics -- and on, at
+    bench.py's sep_period 8), 9 back-to-back 128-tick launches: 64-80 sampled
+    games (8-game windows, both batch ends) replayed on the oracle, every
+    tick's observation row, both actions, the state after every launch
+    (updater.py:76-162, staircasebot.py:9-21, randombot.py:20-21)."""
+    import torch
+    from optimax_rogue_amd import EnvConfig
+    from optimax_rogue_amd.engine import BatchedEngine
+    from optimax_rogue_amd.enums import EXT_SEPARATION_DAMAGE, OBS_FIELDS
+    which, sep, B, pol, lanes, nt = EXTRAS_FORMS[name]
+    cfg = getattr(EnvConfig, which)()
+    if sep:
+        cfg.flags, cfg.sep_period = EXT_SEPARATION_DAMAGE, 8
+    T, L, seed = 128, 9, 5
+    eng = BatchedEngine(cfg, B, seed=seed, device=torch.device("cuda", 0))
+    shape = eng.rollout_shape(*pol)
+    assert (shape["lanes_per_game"], shape["nontemporal"]) == (lanes, nt), shape
+    obs = torch.empty((T, len(OBS_FIELDS), B), dtype=torch.int32, device=eng.device)
+    act = torch.empty((T, B, 2), dtype=torch.int8, device=eng.device)
+    launch = eng.rollout_launcher(T, *pol, obs=obs, act=act)
+    starts = _window_starts(B, B, 6, 11)
+    snap, gids = _timed_form_vs_oracle(oracle_lib, eng, [eng], [obs], [act], launch, cfg, pol,
+                                       seed, T, L, starts)
+    assert (snap["ep_count"][gids] >= 1).all()
+    if which == "c5":   # the StaircaseBots went deep
+        assert snap["counters"][1][gids].sum() > 100
 
 
 def test_bad_action_and_no_autoreset():
@@ -619,6 +694,18 @@ PAIRED_CASES = {
     "random_npcs_resets": (dict(width=10, height=10, n_npcs=5, max_ticks=30), (1, 1), 1000, 66),
     "random_duel_deaths": (dict(width=4, height=5, max_ticks=0, player_health=2), (1, 1), 500,
                            67),
+    # the 16-slot register-NPC instances (K 9..16) with RandomBots
+    "random_npcs_k12": (dict(width=9, height=8, n_npcs=12, npc_health=2, max_ticks=45), (1, 1),
+                        1000, 68),
+    "random_npcs_k16_unused": (dict(width=10, height=9, n_npcs=16, max_ticks=35, despawn=2),
+                               (1, 1), 999, 69),
+    # StaircaseBots with register NPCs (rare_tick's general path in the pair):
+    # player 2 starts above the NPCs' depth and descends onto it, where
+    # player 1 walks through them
+    "stairs_npcs_separated": (dict(width=8, height=7, n_npcs=6, start_mode=2, p1_depth=1,
+                                   p2_depth=0, max_ticks=50, npc_health=2), (2, 2), 1000, 70),
+    "stairs_npcs_k14_unused": (dict(width=9, height=9, n_npcs=14, start_mode=2, p1_depth=1,
+                                    p2_depth=0, despawn=2, max_ticks=40), (2, 2), 1024, 71),
 }
 
 
@@ -643,4 +730,31 @@ def test_paired_rollout_vs_oracle(name, oracle_lib):
         assert np.array_equal(obs.cpu().numpy(), want_obs), f"{name} obs {launch}"
     episodes = int(eng.snapshot()["episode"].sum())
     assert episodes > 0, name   # every case crosses resets
+    if cfg.get("n_npcs"):
+        c = eng.snapshot()["counters"]
+        assert c[0].sum() > 0 and c[3].sum() > 0, name   # combats and NPC deaths happened
     torch.cuda.synchronize()
+
+
+def test_dense_npc_character_trajectory_vs_oracle(oracle_lib):
+    """Dense NPCs (K > 16) with the character mechanics and RandomBots, WITH
+    trajectory buffers: the generic rollout form (there is no dense instance
+    of the PM 3 form; before round 4 this launch matched no kernel and
+    returned without running) -- rows, actions and state vs the oracle."""
+    import torch
+    from optimax_rogue_amd.enums import OBS_FIELDS
+    cfg = dict(width=12, height=12, n_npcs=30, npc_health=2, max_ticks=60, flags=4 | 16 | 64,
+               xp_per_level=2)
+    B, T, seed = 1024, 30, 45
+    ora = oracle_lib.Oracle(cfg, B, seed, 0)
+    ora.reset(episode=np.zeros(B, np.int32))
+    eng = _engine(cfg, B, seed)
+    obs = torch.zeros((T, len(OBS_FIELDS), B), dtype=torch.int32, device=eng.device)
+    act = torch.zeros((T, B, 2), dtype=torch.int8, device=eng.device)
+    for launch in range(3):
+        want_act, want_obs = _replay(ora, T, (1, 1))
+        eng.rollout(T, 1, 1, obs=obs, act=act)
+        compare_state(eng.snapshot(), ora.export(), ora.K, f"launch {launch}")
+        assert np.array_equal(act.cpu().numpy(), want_act), f"actions {launch}"
+        assert np.array_equal(obs.cpu().numpy(), want_obs), f"obs {launch}"
+    assert int(eng.snapshot()["episode"].sum()) > 0

@@ -12,7 +12,7 @@ mkdir -p $O
 cd $R
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 if [ "${2:-tests}" = tests ]; then
-  timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 300 \
+  timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 \
     --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
   tail -3 $O/pytest.log
 fi
@@ -22,8 +22,8 @@ if [ "${3:-}" = rehearse ]; then
   for MODE in weak strong; do
     EXTRA=""
     [ $MODE = strong ] && EXTRA="--strong"
-    timeout -k 10 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
-      --master-addr 127.0.0.1 --master-port $((29500 + RANDOM % 1000)) bench.py --gpus 2 \
+    # bench.py starts the two ranks itself (torch.distributed.run underneath)
+    timeout -k 10 300 python3 bench.py --gpus 2 \
       --steps 10 --warmup 3 --dist-backend gloo --same-device $EXTRA \
       > $O/bench_2rank_gloo_$MODE.json 2> $O/bench_2rank_gloo_$MODE.err
     cut -c1-300 $O/bench_2rank_gloo_$MODE.json

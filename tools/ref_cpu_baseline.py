@@ -20,6 +20,13 @@ goes to /dev/null.  Two loops are timed:
   * full: RandomBot.move for both players + on_tick + update (what one
     env-step of the batched engine covers).
 
+Beside them, on the same cores in the same run, `oracle/pyref.py` (the
+pure-Python object-model restatement bench.py times on the GPU box as
+`python_restatement`, where the reference cannot go): `pyref_vs_reference`
+= pyref's env-steps/s / the reference's "full" leg, single core and per core
+of the parallel leg, so the GPU box's python_restatement figure can be read
+as the reference's cost (divide by the ratio).
+
     python tools/ref_cpu_baseline.py [--seconds 10] [--procs N]
 """
 import argparse
@@ -145,6 +152,17 @@ def main():
                      "per_core_env_steps_per_s": sum(s / b for s, b in res) / a.procs,
                      "env_steps": steps, "seconds_per_proc": a.seconds,
                      "wall_s": wall}
+    # the restatement on the same host: one core, then a.procs processes
+    sys.path.insert(0, ROOT)
+    from oracle import pyref
+    pr = pyref.bench(a.seconds, a.procs, a.seconds)
+    full = out["full"]
+    out["pyref"] = {k: pr[k] for k in ("single_core", "per_core", "value", "cores", "sample")}
+    out["pyref_vs_reference"] = {
+        "single_core": pr["single_core"] / full["single_core_env_steps_per_s"],
+        "per_core": pr["per_core"] / full["per_core_env_steps_per_s"],
+        "note": "oracle/pyref.py env-steps/s over the reference's 'full' leg on this host: "
+                "python_restatement (GPU box) / this ratio = the reference's own rate there"}
     json.dump(out, open(a.out, "w"), indent=1)
     print(json.dumps(out, indent=1))
 
