@@ -247,6 +247,32 @@ def extras(torch, cfg, dev, B_cfg, K, large_rollout=False):
                             "note": "orx_policy + orx_step per tick, 50 ticks per HIP graph"}
     del eng, g
     torch.cuda.empty_cache()
+    # (1b) the learner's per-tick path: VecEnv.step (one orx_env_step launch:
+    # int64 learner actions for player 1, RandomBot opponent, observation /
+    # reward / done / status out, no host sync), called eagerly from Python
+    # at the config batch, 400 ticks, wall clock
+    from optimax_rogue_amd import VecEnv
+    env = VecEnv(cfg, B_cfg, seed=3, device=dev, opponent=1)
+    pool = torch.randint(1, 6, (16, B_cfg), dtype=torch.int64, device=dev)
+    for k in range(20):
+        env.step(pool[k % 16])
+    torch.cuda.synchronize()
+    n_ve = 400
+    t0 = time.perf_counter()
+    for k in range(n_ve):
+        env.step(pool[k % 16])
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    ks = timed_launches(torch, lambda: env.step(pool[0]), 30)
+    out["vecenv_step"] = {"value": B_cfg * n_ve / el, "unit": "env-steps/s",
+                          "us_per_tick": el / n_ve * 1e6,
+                          "device_us_per_tick": sorted(ks)[len(ks) // 2] * 1e6,
+                          "note": "VecEnv.step eager from Python (int64 learner actions + "
+                                  "RandomBot opponent -> obs, reward, done, status): one "
+                                  "orx_env_step launch per tick, no host sync; "
+                                  "device_us_per_tick = HIP events around one call"}
+    del env, pool
+    torch.cuda.empty_cache()
     # (2) large batch: the chip full (2^21 games)
     BL = 1 << 21
     eng = BatchedEngine(cfg, BL, seed=3, device=dev)

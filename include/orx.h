@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define ORX_ABI_VERSION 4
+#define ORX_ABI_VERSION 5
 
 /* ---- error codes -------------------------------------------------------- */
 #define ORX_OK 0
@@ -414,6 +414,25 @@ int orx_step_events(const orx_cfg_t* cfg, const orx_state_t* st, const int8_t* a
 int orx_policy(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p1,
                int32_t policy_p2, int8_t* actions, int64_t n_games,
                uint64_t seed, int64_t game_offset, void* stream);
+
+/* A learner's tick in one launch (VecEnv.step): player 1's actions from
+ * `actions` (action_cols 1: [B], player 2 moved by policy_p2 as orx_policy
+ * would; 2: [B][2], both players), elements of action_bytes bytes (1, 2, 4
+ * or 8: int8 .. int64, read at full width -- any value outside the Move
+ * codes, e.g. a 0-based argmax or 257, becomes an invalid move, which stops
+ * that game with ORX_STATUS_BAD_ACTION as orx_step does); the pair played is
+ * written to act[b][2]; then orx_step; then per game the post-step
+ * observation row obs[b * ORX_OBS_FIELDS + f] (the orx_rollout fields), the
+ * status, reward[b] (player 1's view: +1 Player1Win, -1 Player2Win, 0
+ * otherwise, on the tick the episode ends) and done[b] (1 on that tick; an
+ * engine stop code >= 16 ends it as a truncation).  No host sync.  Philox
+ * mode only (stock-seed mode: orx_policy + orx_step).  Replaces the bot
+ * loop's per-tick exchange, optimax_rogue_bots/main.py:118-155, and
+ * server/main.py:110-113 for a learner. */
+int orx_env_step(const orx_cfg_t* cfg, const orx_state_t* st, const void* actions,
+                 int32_t action_bytes, int32_t action_cols, int32_t policy_p2, int8_t* act,
+                 int32_t* obs, float* reward, uint8_t* done, int32_t* status, int64_t n_games,
+                 uint64_t seed, int64_t game_offset, void* stream);
 
 /* Fused rollout: n_ticks x (orx_policy then orx_step) in one launch, state
  * kept in registers between ticks.  If obs != NULL, tick t's post-step

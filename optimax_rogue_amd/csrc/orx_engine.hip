@@ -1937,14 +1937,14 @@ __global__ void __launch_bounds__(256) reset_kernel(orx_cfg_t hc, orx_state_t st
 // EXT = false: the reference's rules only (cfg.flags == 0), the extension
 // code compiled out -- fewer registers, so more waves per SIMD hide the
 // state loads (the per-tick drop-in's common case)
-template <int NCAP, bool EV, bool GRID, bool EXT = true>
-__global__ void __launch_bounds__(256) step_kernel(orx_cfg_t hc, orx_state_t st,
-                                                   const int8_t* __restrict__ actions, uint32_t B,
-                                                   Key key, uint32_t off,
-                                                   int32_t* __restrict__ events,
-                                                   int32_t* __restrict__ n_events) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= B) return;
+// One game's Updater.update (or its autoreset): the per-tick step kernels'
+// body.  get_action() yields the game's packed action pair (player 1 in the
+// low byte); it is called only for a game in progress.
+template <int NCAP, bool EV, bool GRID, bool EXT, class A>
+__device__ __forceinline__ void step_game(const orx_cfg_t& hc, const orx_state_t& st, A get_action,
+                                          uint32_t B, uint32_t i, Key key, uint32_t off,
+                                          int32_t* __restrict__ events,
+                                          int32_t* __restrict__ n_events) {
   Cfg c = make_cfg(hc, st);
   if constexpr (!EXT) c.ext = 0;
   const uint32_t game = off + i;
@@ -1972,7 +1972,7 @@ __global__ void __launch_bounds__(256) step_kernel(orx_cfg_t hc, orx_state_t st,
     }
     return;
   }
-  const uint16_t a = reinterpret_cast<const uint16_t*>(actions)[i];
+  const uint16_t a = get_action();
   p1.move = (int8_t)(a & 0xFF);
   p2.move = (int8_t)(a >> 8);
   if (!valid_move(c, p1.move) || !valid_move(c, p2.move)) {
@@ -2004,6 +2004,19 @@ __global__ void __launch_bounds__(256) step_kernel(orx_cfg_t hc, orx_state_t st,
   if (EV) n_events[i] = ev.n;
 }
 
+template <int NCAP, bool EV, bool GRID, bool EXT = true>
+__global__ void __launch_bounds__(256) step_kernel(orx_cfg_t hc, orx_state_t st,
+                                                   const int8_t* __restrict__ actions, uint32_t B,
+                                                   Key key, uint32_t off,
+                                                   int32_t* __restrict__ events,
+                                                   int32_t* __restrict__ n_events) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B) return;
+  step_game<NCAP, EV, GRID, EXT>(
+      hc, st, [&] { return reinterpret_cast<const uint16_t*>(actions)[i]; }, B, i, key, off,
+      events, n_events);
+}
+
 __global__ void __launch_bounds__(256) policy_kernel(orx_state_t st, int32_t pol1, int32_t pol2,
                                                      int8_t* __restrict__ actions, uint32_t B,
                                                      Key key, uint32_t off) {
@@ -2029,6 +2042,69 @@ __global__ void __launch_bounds__(256) policy_kernel(orx_state_t st, int32_t pol
   const W4 tb = need_rng ? tick_block(key, off + i, ep, tick) : W4{0, 0, 0, 0};
   policy_pair(key, off + i, ep, tick, pol1, pol2, tb, p1, p2, a1, a2);
   out[i] = pack_actions(a1, a2);
+}
+
+// A learner's tick (orx_env_step, VecEnv.step): the learner's actions read at
+// their own width (dsize bytes; anything outside 1..max move becomes 0, which
+// the step turns into ORX_STATUS_BAD_ACTION, so a wrapped int8 never becomes
+// a legal move), player 2's move from policy `pol2` when cols == 1, the
+// pair written to act (the engine's actions buffer), step_game, and the
+// game's observation row [14], status, reward (player 1's view: +1 / -1 on
+// the tick its episode ends in a win / loss) and done (that tick; an engine
+// stop code >= 16 is a truncation) -- VecEnv.outcome on device, no host
+// sync.  The row is read back from the state this thread just wrote.
+template <int NCAP, bool GRID, bool EXT>
+__global__ void __launch_bounds__(256) env_step_kernel(
+    orx_cfg_t hc, orx_state_t st, const void* __restrict__ actions, int32_t dsize, int32_t cols,
+    int32_t pol2, int8_t* __restrict__ act, int32_t* __restrict__ obs, float* __restrict__ reward,
+    uint8_t* __restrict__ done, int32_t* __restrict__ status_out, uint32_t B, Key key,
+    uint32_t off) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B) return;
+  const int32_t before = st.status[i];
+  const int64_t hi = (EXT && (hc.flags & ORX_EXT_HEAL)) ? ORX_MOVE_HEAL : ORX_MOVE_STAY;
+  auto learner = [&](uint32_t k) -> int32_t {
+    int64_t v;
+    if (dsize == 1) v = reinterpret_cast<const int8_t*>(actions)[k];
+    else if (dsize == 2) v = reinterpret_cast<const int16_t*>(actions)[k];
+    else if (dsize == 4) v = reinterpret_cast<const int32_t*>(actions)[k];
+    else v = reinterpret_cast<const int64_t*>(actions)[k];
+    return (v >= ORX_MOVE_UP && v <= hi) ? (int32_t)v : 0;
+  };
+  int32_t a1 = learner(cols == 1 ? i : 2u * i), a2 = ORX_MOVE_STAY;
+  if (cols == 2) {
+    a2 = learner(2u * i + 1u);
+  } else if (pol2 != ORX_POLICY_STAY && pol2 != ORX_POLICY_NONE) {
+    Player p1, p2;
+    p2.x = st.p_x[B + i];
+    p2.y = st.p_y[B + i];
+    p2.sx = st.st_x[B + i];
+    p2.sy = st.st_y[B + i];
+    const uint32_t ep = (uint32_t)st.episode[i];
+    const int32_t tick = st.tick[i];
+    const W4 tb = pol2 == ORX_POLICY_RANDOM ? tick_block(key, off + i, ep, tick)
+                                            : W4{0, 0, 0, 0};
+    int32_t keep = a1;
+    policy_pair(key, off + i, ep, tick, ORX_POLICY_NONE, pol2, tb, p1, p2, keep, a2);
+  } else if (pol2 == ORX_POLICY_NONE) {
+    a2 = (int8_t)(reinterpret_cast<const uint16_t*>(act)[i] >> 8);  // kept from before
+  }
+  const uint16_t a = pack_actions(a1, a2);
+  reinterpret_cast<uint16_t*>(act)[i] = a;
+  step_game<NCAP, false, GRID, EXT>(hc, st, [&] { return a; }, B, i, key, off, nullptr, nullptr);
+  const int32_t after = st.status[i];
+  const int32_t row[ORX_OBS_FIELDS] = {
+      st.p_x[i],      st.p_y[i],     st.p_depth[i],     st.p_health[i],     st.p_x[B + i],
+      st.p_y[B + i],  st.p_depth[B + i], st.p_health[B + i], st.tick[i],   after,
+      st.st_x[i],     st.st_y[i],    st.st_x[B + i],    st.st_y[B + i]};
+#pragma unroll
+  for (int f = 0; f < ORX_OBS_FIELDS; ++f) obs[(size_t)i * ORX_OBS_FIELDS + f] = row[f];
+  const bool ended = before == ORX_IN_PROGRESS && after >= ORX_PLAYER1_WIN &&
+                     (after <= ORX_TIE || after >= ORX_STATUS_BAD_ACTION);
+  done[i] = ended ? 1 : 0;
+  reward[i] = !ended ? 0.0f : after == ORX_PLAYER1_WIN ? 1.0f : after == ORX_PLAYER2_WIN ? -1.0f
+                                                                                         : 0.0f;
+  status_out[i] = after;
 }
 
 // One player descends -- the common case of handle_descend (updater.py:259-296)
@@ -3984,6 +4060,44 @@ int orx_policy(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p1, i
   hipLaunchKernelGGL(policy_kernel, grid_for(B), dim3(kBlock), 0, (hipStream_t)stream, *st,
                      policy_p1, policy_p2, actions, B, make_key(seed), off);
   return launch_status("orx_policy");
+}
+
+int orx_env_step(const orx_cfg_t* cfg, const orx_state_t* st, const void* actions,
+                 int32_t action_bytes, int32_t action_cols, int32_t policy_p2, int8_t* act,
+                 int32_t* obs, float* reward, uint8_t* done, int32_t* status, int64_t n_games,
+                 uint64_t seed, int64_t game_offset, void* stream) {
+  int r;
+  if ((r = check_cfg(cfg)) || (r = check_sizes(n_games, game_offset)) ||
+      (r = check_policy(policy_p2)))
+    return r;
+  if (action_bytes != 1 && action_bytes != 2 && action_bytes != 4 && action_bytes != 8)
+    return fail(ORX_EINVAL, "action_bytes must be 1, 2, 4 or 8");
+  if (action_cols != 1 && action_cols != 2) return fail(ORX_EINVAL, "action_cols must be 1 or 2");
+  if (cfg->rng == ORX_RNG_MT19937)
+    return fail(ORX_EINVAL, "orx_env_step: stock-seed mode draws the bots' moves from the "
+                            "games' own streams; use orx_policy + orx_step");
+  if (n_games == 0) return ORX_OK;
+  if ((r = check_state(cfg, st, true))) return r;
+  if (!actions || !act || !obs || !reward || !done || !status)
+    return fail(ORX_EINVAL, "a pointer is NULL");
+  const uint32_t B = (uint32_t)n_games, off = (uint32_t)game_offset;
+  const hipStream_t s = (hipStream_t)stream;
+  const Key k = make_key(seed);
+  const int nc = ncap_for(cfg->n_npcs);
+  const bool grid = cfg->n_layouts > 0;
+#define ORX_ENV(N, G, X)                                                                        \
+  if (nc == N && grid == G && (cfg->flags == 0 || X)) {                                        \
+    hipLaunchKernelGGL((env_step_kernel<N, G, X>), grid_for(B), dim3(kBlock), 0, s, *cfg, *st,   \
+                       actions, action_bytes, action_cols, policy_p2, act, obs, reward, done,   \
+                       status, B, k, off);                                                      \
+    return launch_status("orx_env_step");                                                      \
+  }
+  ORX_ENV(0, false, false) ORX_ENV(8, false, false) ORX_ENV(16, false, false)
+  ORX_ENV(0, false, true) ORX_ENV(8, false, true) ORX_ENV(16, false, true)
+  ORX_ENV(kDense, false, true) ORX_ENV(0, true, true) ORX_ENV(8, true, true)
+  ORX_ENV(16, true, true) ORX_ENV(kDense, true, true)
+#undef ORX_ENV
+  return fail(ORX_EIO, "orx_env_step: no kernel instance for this configuration");
 }
 
 int orx_rollout(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p1, int32_t policy_p2,

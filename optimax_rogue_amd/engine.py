@@ -240,6 +240,31 @@ class BatchedEngine:
                    self.game_offset, self._stream())
         return self.status, self._ev, self._nev
 
+    _ACTION_BYTES = {torch.int8: 1, torch.int16: 2, torch.int32: 4, torch.int64: 8}
+
+    def env_step(self, actions: torch.Tensor, p2: int, obs: torch.Tensor, reward: torch.Tensor,
+                 done: torch.Tensor, status: torch.Tensor) -> None:
+        """orx_env_step: one learner tick in one launch.  ``actions``: integer
+        [n_games] (player 1; player 2 moved by policy ``p2``) or [n_games, 2],
+        any integer width, contiguous, on the engine's device (values outside
+        the Move codes stop that game with STATUS_BAD_ACTION).  Writes the
+        pair played into ``self.actions``, then obs int32 [n_games, 14],
+        reward float32, done bool and status int32 [n_games]."""
+        nb = self._ACTION_BYTES.get(actions.dtype)
+        if nb is None or tuple(actions.shape) not in ((self.B,), (self.B, 2)) \
+                or not actions.is_contiguous() or actions.device != self.device:
+            raise ValueError(f"actions must be a contiguous integer [n_games] or [n_games, 2] "
+                             f"tensor on {self.device}")
+        for t, dt, shape in ((obs, torch.int32, (self.B, len(OBS_FIELDS))),
+                             (reward, torch.float32, (self.B,)), (done, torch.bool, (self.B,)),
+                             (status, torch.int32, (self.B,))):
+            if t.dtype != dt or tuple(t.shape) != shape or not t.is_contiguous() \
+                    or t.device != self.device:
+                raise ValueError(f"env_step output must be a contiguous {dt} {shape} tensor")
+        self._call("orx_env_step", _ptr(actions), nb, actions.dim(), int(p2), _ptr(self.actions),
+                   _ptr(obs), _ptr(reward), _ptr(done), _ptr(status), self.B, self.seed,
+                   self.game_offset, self._stream())
+
     def policy(self, p1: int = Policy.Random, p2: int = Policy.Random,
                out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """RandomBot / StaircaseBot moves for both players into ``out``."""

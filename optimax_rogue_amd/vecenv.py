@@ -33,7 +33,7 @@ _STATUS = OBS_FIELDS.index("status")
 class VecEnv:
     def __init__(self, cfg: EnvConfig, n_games: int, seed: int = 0, game_offset: int = 0,
                  device: Optional[torch.device] = None,
-                 opponent: Optional[int] = Policy.Random):
+                 opponent: Optional[int] = Policy.Random, check_actions: bool = False):
         if not int(cfg.autoreset):
             raise ValueError("VecEnv needs cfg.autoreset = 1 (finished games restart)")
         self.engine = BatchedEngine(cfg, n_games, seed=seed, game_offset=game_offset,
@@ -41,6 +41,10 @@ class VecEnv:
         self.B = self.engine.B
         self.device = self.engine.device
         self.opponent = None if opponent is None else int(opponent)
+        # True: step() raises ValueError on a non-Move action (a host check, so
+        # every step synchronizes); False (default): the engine stops that game
+        # with STATUS_BAD_ACTION, which step() reports as done (a truncation)
+        self.check_actions = bool(check_actions)
 
     # -- observation -----------------------------------------------------------
     def observe(self) -> torch.Tensor:
@@ -84,25 +88,51 @@ class VecEnv:
         return 6 if int(self.engine.cfg.flags) & EXT_HEAL else 5
 
     def step(self, actions: torch.Tensor):
-        """Plays one tick: ``actions`` int8 [n_games] (player 1; the opponent
+        """Plays one tick: ``actions`` integer [n_games] (player 1; the opponent
         policy moves player 2) or [n_games, 2] (self-play), Move values 1..5
-        (1..6 with EXT_HEAL; anything else raises ValueError -- checked on the
-        host, so this synchronizes).  Returns (observation, reward, done,
-        status); every tensor is fresh (status is a copy, not the engine's
-        buffer, which the next call overwrites)."""
+        (1..6 with EXT_HEAL), any integer dtype.  A value outside them (e.g. a
+        0-based argmax) stops that game with STATUS_BAD_ACTION: it is done
+        with reward 0 this step (a truncation) and restarts on the next one;
+        with ``check_actions=True`` it raises ValueError instead (a host check:
+        that step synchronizes).  One launch (orx_env_step) and no host sync
+        otherwise.  Returns (observation, reward, done, status), all fresh
+        tensors."""
         e = self.engine
         if tuple(actions.shape) not in ((self.B,), (self.B, 2)):   # no silent broadcasting
             raise ValueError(f"actions must be [n_games] or [n_games, 2], got "
                              f"{tuple(actions.shape)}")
-        a = actions.to(device=self.device)
+        if actions.dtype not in BatchedEngine._ACTION_BYTES:
+            raise ValueError(f"actions must be an integer tensor, got {actions.dtype}")
+        if actions.dim() == 1 and self.opponent is None:
+            raise ValueError("self-play (opponent=None) takes [n_games, 2] actions")
+        a = actions if actions.device == self.device else actions.to(self.device)
+        if not a.is_contiguous():
+            a = a.contiguous()
+        if self.check_actions:
+            hi = self._max_move()
+            if bool(((a < 1) | (a > hi)).any()):
+                raise ValueError(f"actions must be Move values 1..{hi} (an argmax over logits is "
+                                 "0-based: add 1)")
+        if e.mt_py is not None:
+            return self._step_stock(a)
+        B = self.B
+        obs = torch.empty((B, len(OBS_FIELDS)), dtype=torch.int32, device=self.device)
+        reward = torch.empty(B, dtype=torch.float32, device=self.device)
+        done = torch.empty(B, dtype=torch.bool, device=self.device)
+        status = torch.empty(B, dtype=torch.int32, device=self.device)
+        e.env_step(a, Policy.NONE if self.opponent is None else self.opponent, obs, reward, done,
+                   status)
+        return obs, reward, done, status
+
+    def _step_stock(self, a: torch.Tensor):
+        """Stock-seed mode (the bots draw from each game's own MT19937 stream):
+        orx_policy + orx_step, invalid values mapped on the device to the
+        invalid move 0 before the int8 cast (257 must not wrap to 1)."""
+        e = self.engine
         hi = self._max_move()
-        if bool(((a < 1) | (a > hi)).any()):   # before the int8 cast: 257 must not wrap to 1
-            raise ValueError(f"actions must be Move values 1..{hi} (an argmax over logits is "
-                             "0-based: add 1)")
-        a = a.to(torch.int8)
+        a = torch.where((a >= 1) & (a <= hi), a, torch.zeros((), dtype=a.dtype,
+                                                             device=a.device)).to(torch.int8)
         if a.dim() == 1:
-            if self.opponent is None:
-                raise ValueError("self-play (opponent=None) takes [n_games, 2] actions")
             e.actions[:, 0].copy_(a)
             e.policy(Policy.NONE, self.opponent)   # player 2's move; player 1's kept
         else:

@@ -323,3 +323,100 @@ def test_vecenv_reset_starts_next_episodes(oracle_lib):
     assert (ep[m] == ep_before[m] + 1).all() and (ep[~m] == ep_before[~m]).all()
     tick = env.engine.tick.cpu().numpy()
     assert (tick[m] == 1).all() and (tick[~m] > 1).all()
+
+
+@pytest.mark.parametrize("case", ["c3_int64", "selfplay_int32", "stairs_opponent", "dense_bank",
+                                  "heal_ext"])
+def test_vecenv_fused_step_equals_policy_step(case):
+    """VecEnv.step (one orx_env_step launch, no host sync) against the
+    unfused engine calls it replaces -- orx_policy for player 2, orx_step,
+    then VecEnv.outcome and observe() on the host side of the comparison --
+    for int8..int64 learner actions, self-play, both opponent policies,
+    register / dense NPCs, a dungeon bank and the character extensions
+    (actions 6 = heal valid)."""
+    import torch
+    from optimax_rogue_amd import DungeonBank, EnvConfig, VecEnv
+    from optimax_rogue_amd.engine import BatchedEngine
+    from optimax_rogue_amd.enums import Policy
+    dev = torch.device("cuda", 0)
+    layouts = None
+    if case == "c3_int64":
+        cfg, opp, dt, hi = EnvConfig(width=64, height=64, n_npcs=8, max_ticks=40), 1, torch.int64, 5
+    elif case == "selfplay_int32":
+        cfg, opp, dt, hi = EnvConfig(width=8, height=7, n_npcs=3, max_ticks=30,
+                                     player_health=3), None, torch.int32, 5
+    elif case == "stairs_opponent":
+        cfg, opp, dt, hi = EnvConfig(width=9, height=9, max_ticks=50, start_mode=2, p1_depth=0,
+                                     p2_depth=1), 2, torch.int8, 5
+    elif case == "dense_bank":
+        bank = DungeonBank.random(12, 10, 4, seed=3, n_stairs=2)
+        layouts = bank.layouts
+        cfg, opp, dt, hi = EnvConfig(width=12, height=10, n_npcs=24, max_ticks=60,
+                                     npc_health=1, layouts=layouts), 1, torch.int16, 5
+    else:
+        cfg, opp, dt, hi = EnvConfig(width=8, height=8, n_npcs=6, max_ticks=50,
+                                     flags=4 | 8 | 16 | 32, player_health=4), 1, torch.int64, 6
+    B, T = 1537, 80
+    env = VecEnv(cfg, B, seed=13, device=dev, opponent=opp)
+    ref = BatchedEngine(cfg, B, seed=13, device=dev)
+    g = torch.Generator(device="cpu").manual_seed(5)
+    dones = 0
+    for t in range(T):
+        shape = (B, 2) if opp is None else (B,)
+        a = torch.randint(1, hi + 1, shape, generator=g).to(dt).to(dev)
+        obs, r, d, st = env.step(a)
+        a8 = a.to(torch.int8)
+        if opp is None:
+            ref.actions.copy_(a8)
+        else:
+            ref.actions[:, 0].copy_(a8)
+            ref.policy(Policy.NONE, opp)
+        before = ref.status.clone()
+        want_st = ref.step(ref.actions).clone()
+        want_r, want_d = VecEnv.outcome(before, want_st)
+        assert torch.equal(env.engine.actions, ref.actions), (case, t)
+        assert torch.equal(st, want_st), (case, t)
+        assert torch.equal(d, want_d) and torch.equal(r, want_r), (case, t)
+        e = ref
+        want_obs = torch.stack([e.p_x[0], e.p_y[0], e.p_depth[0], e.p_health[0], e.p_x[1],
+                                e.p_y[1], e.p_depth[1], e.p_health[1], e.tick, e.status,
+                                e.st_x[0], e.st_y[0], e.st_x[1], e.st_y[1]], dim=1)
+        assert torch.equal(obs, want_obs), (case, t)
+        dones += int(d.sum())
+    assert dones > B // 4, case
+    a, b = env.engine.snapshot(), ref.snapshot()
+    for k in a:
+        assert np.array_equal(a[k], b[k]), (case, k)
+
+
+def test_vecenv_bad_actions_truncate_on_device():
+    """Values outside the Move codes (0, -1, 6 without EXT_HEAL, 257 as
+    int64 -- which an int8 cast would wrap to the legal 1) stop exactly
+    those games with STATUS_BAD_ACTION: done, reward 0, no host sync; the
+    next step starts their next episode.  check_actions=True raises instead."""
+    import torch
+    from optimax_rogue_amd import EnvConfig, VecEnv
+    from optimax_rogue_amd.enums import STATUS_BAD_ACTION
+    dev = torch.device("cuda", 0)
+    B = 512
+    env = VecEnv(EnvConfig(width=10, height=10, max_ticks=100), B, seed=2, device=dev)
+    a = torch.full((B,), 5, dtype=torch.int64, device=dev)
+    bad = {3: 0, 10: -1, 77: 6, 100: 257, 511: 1 << 40}
+    for k, v in bad.items():
+        a[k] = v
+    ep0 = env.engine.episode.clone()
+    obs, r, d, st = env.step(a)
+    idx = torch.tensor(sorted(bad), device=dev)
+    assert (st[idx] == STATUS_BAD_ACTION).all() and d[idx].all() and (r[idx] == 0).all()
+    keep = torch.ones(B, dtype=torch.bool, device=dev)
+    keep[idx] = False
+    assert (st[keep] == 1).all() and not d[keep].any()
+    assert (obs[:, 9] == st).all()
+    obs, r, d, st = env.step(torch.full((B,), 5, dtype=torch.int8, device=dev))
+    assert (st == 1).all() and not d.any()
+    ep = env.engine.episode
+    assert (ep[idx] == ep0[idx] + 1).all() and (ep[keep] == ep0[keep]).all()
+    assert (obs[idx, 8] == 1).all()   # their next episode's first tick
+    strict = VecEnv(EnvConfig(width=10, height=10), 8, seed=2, device=dev, check_actions=True)
+    with pytest.raises(ValueError, match="Move values"):
+        strict.step(torch.tensor([1, 2, 3, 4, 5, 0, 1, 1], device=dev))

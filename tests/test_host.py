@@ -21,15 +21,14 @@ def test_vecenv_outcome():
 
 @pytest.mark.parametrize("bad", [[0, 1, 2], [1, 6, 2], [1, 2, 257], [-1, 2, 3]])
 def test_vecenv_step_rejects_non_moves(bad):
-    """A learner's 0-based argmax (or any value outside the Move codes) is
-    refused before it reaches the engine, instead of stopping the game with
-    ORX_STATUS_BAD_ACTION and silently autoresetting it."""
+    """check_actions=True: a learner's 0-based argmax (or any value outside
+    the Move codes) is refused on the host before it reaches the engine."""
     import torch
     from optimax_rogue_amd import EnvConfig
     from optimax_rogue_amd.vecenv import VecEnv
     env = VecEnv.__new__(VecEnv)
     env.engine = _bare_engine(EnvConfig(), 3)
-    env.B, env.device, env.opponent = 3, torch.device("cpu"), 1
+    env.B, env.device, env.opponent, env.check_actions = 3, torch.device("cpu"), 1, True
     with pytest.raises(ValueError, match="Move values"):
         env.step(torch.tensor(bad, dtype=torch.int32))
     with pytest.raises(ValueError, match="Move values"):
@@ -110,3 +109,32 @@ def test_engine_refuses_snapshots_off_the_grid():
             e._check_snapshot(dict(ok, **{key: val}))
     # a dead NPC's slot is not read: any position passes
     e._check_snapshot(dict(ok, npc_pos=np.array([[200] * 3, [0] * 3]), npc_alive=np.full(3, 2)))
+
+
+@pytest.mark.parametrize("bad", [[0, 1, 2], [1, 2, 257], [-1, 2, 3]])
+def test_vecenv_step_passes_bad_actions_to_the_engine(bad):
+    """check_actions=False (the default): no host check and no sync -- the
+    learner's tensor goes to orx_env_step as it is (full width: 257 is not
+    cast to int8, where it would wrap to a legal 1); the engine stops those
+    games with STATUS_BAD_ACTION and step() reports them done (GPU tests:
+    test_vecenv_bad_actions_truncate_on_device)."""
+    import torch
+    from optimax_rogue_amd import EnvConfig
+    from optimax_rogue_amd.vecenv import VecEnv
+    calls = []
+
+    class Eng:
+        cfg, mt_py = EnvConfig(), None
+
+        def env_step(self, a, p2, obs, reward, done, status):
+            calls.append((a.clone(), p2, obs.shape, reward.dtype, done.dtype, status.dtype))
+
+    env = VecEnv.__new__(VecEnv)
+    env.engine, env.check_actions = Eng(), False
+    env.B, env.device, env.opponent = 3, torch.device("cpu"), 2
+    env.step(torch.tensor(bad, dtype=torch.int64))
+    a, p2, shape, rd, dd, sd = calls[0]
+    assert a.dtype == torch.int64 and a.tolist() == bad and p2 == 2
+    assert shape == (3, 14) and rd == torch.float32 and dd == torch.bool and sd == torch.int32
+    with pytest.raises(ValueError, match="integer"):
+        env.step(torch.tensor([1.0, 2.0, 3.0]))
