@@ -326,6 +326,40 @@ def extras(torch, cfg, dev, B_cfg, K, large_rollout=False):
                 "lanes_per_game": shape["lanes_per_game"], "nontemporal": shape["nontemporal"],
                 "us_per_launch": us * 1e6, "env_steps_per_s": games * T / us}
 
+    # (3a) the headline step with ORX_OBS_COMPACT trajectory rows (24 B per
+    # env-step instead of 56: u8 cells and staircases, int16 healths,
+    # tick | status << 27; the same launches, shards and stream layout)
+    from optimax_rogue_amd.engine import StreamShardedEngine
+    from optimax_rogue_amd.enums import OBS_COMPACT
+    sh = StreamShardedEngine(cfg, B_cfg, seed=3, device=dev, n_streams=2)
+    T = 128
+    co, ca = sh.trajectory_buffers(T, OBS_COMPACT)
+    go = sh.rollout_launcher(T, 1, 1, obs=co, act=ca, obs_format=OBS_COMPACT)
+    sh.fork()
+    for _ in range(3):
+        go()
+    sh.join()
+    reps = 10
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    sh.fork()
+    for _ in range(reps):
+        go()
+    sh.join()
+    e1.record()
+    torch.cuda.synchronize()
+    step_s = e0.elapsed_time(e1) * 1e-3 / reps
+    cb = (bytes_per_game("rollout", K, T) - T * OBS_BYTES + T * 24) * B_cfg
+    out["compact_rows"] = {
+        "games": B_cfg, "ticks_per_step": T, "streams": 2, "us_per_step": step_s * 1e6,
+        "env_steps_per_s": B_cfg * T / step_s, "bytes_per_env_step": cb / (B_cfg * T),
+        "achieved_GBps": cb / step_s / 1e9, "frac": cb / step_s / 1e9 / HBM_PEAK_GBS,
+        "note": "bench step with obs_format=ORX_OBS_COMPACT (6 uint32 rows per tick: cells, "
+                "staircases, healths, depths, tick|status; decode_compact gives the 14 int32 "
+                "fields back bit-exact) -- an opt-in trajectory format, not the headline"}
+    del sh, co, ca, go
+    torch.cuda.empty_cache()
     out["c2"] = dict(rollout_rate(EnvConfig.c2(), 4096, 1), policy="2x RandomBot", grid="32x32")
     # the explicit-grid generator (dungeon bank): C3's shape on 16 random
     # 64x64 layouts, tiles staged in LDS by the rollout

@@ -445,6 +445,34 @@ int orx_rollout(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p1,
                 int64_t n_games, uint64_t seed, int64_t game_offset,
                 void* stream);
 
+/* Trajectory row formats (orx_rollout_ex obs_format).
+ * ORX_OBS_INT32: obs int32 [n_ticks][ORX_OBS_FIELDS][n_games], as orx_rollout.
+ * ORX_OBS_COMPACT: obs uint32 [n_ticks][ORX_OBS_COMPACT_FIELDS][n_games], the
+ * same observation in 24 bytes instead of 56 (GameState fields, state.py:25-34):
+ *   row 0  p1.x | p1.y << 8 | p2.x << 16 | p2.y << 24        (u8 each)
+ *   row 1  p1 staircase x | y << 8 | p2 staircase x << 16 | y << 24
+ *   row 2  (uint16)p1.health | (uint16)p2.health << 16      (int16 each)
+ *   row 3  p1.depth, row 4 p2.depth                        (int32)
+ *   row 5  tick | status << 27                             (tick < 2^27)
+ * It needs width, height <= 256, 1 <= max_ticks < 2^27, and health that
+ * stays within int16: player_health, player_damage, npc_damage, mana_max
+ * (ORX_EXT_MANA), item_bonus * item_slots (ORX_EXT_ITEMS) and max_ticks /
+ * sep_period (ORX_EXT_SEPARATION_DAMAGE) each <= ORX_COMPACT_MAX_STAT;
+ * otherwise orx_rollout_ex returns ORX_EINVAL. */
+#define ORX_OBS_INT32 0
+#define ORX_OBS_COMPACT 1
+#define ORX_OBS_COMPACT_FIELDS 6
+#define ORX_COMPACT_MAX_STAT 8000
+
+/* orx_rollout_concurrent with a trajectory row format (obs_format:
+ * ORX_OBS_INT32 or ORX_OBS_COMPACT; act is unchanged).  Results other than
+ * the rows' encoding do not depend on it.  No reference counterpart (the
+ * reference's observation is a GameState view, state.py:53-58). */
+int orx_rollout_ex(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p1,
+                   int32_t policy_p2, int32_t n_ticks, int32_t* obs, int8_t* act,
+                   int32_t obs_format, int64_t n_games, uint64_t seed, int64_t game_offset,
+                   int32_t concurrency, void* stream);
+
 /* orx_rollout as one of `concurrency` (>= 1) launches that run on the device
  * together -- a GPU's batch split over concurrent streams, as
  * StreamShardedEngine does: the launch shape (orx_rollout_shape) is chosen

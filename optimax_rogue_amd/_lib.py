@@ -41,7 +41,8 @@ _lib = None
 EXPORTS = ("orx_abi_version", "orx_last_error", "orx_validate_cfg", "orx_reset", "orx_step",
            "orx_step_events", "orx_policy", "orx_rollout", "orx_dungeon_stairs",
            "orx_dungeon_spawn", "orx_seed_mt", "orx_build_id", "orx_rollout_lanes", "orx_dstore_depths",
-           "orx_rollout_shape", "orx_rollout_concurrent", "orx_env_step")
+           "orx_rollout_shape", "orx_rollout_concurrent", "orx_env_step",
+           "orx_rollout_ex")
 
 
 def load() -> ctypes.CDLL:
@@ -92,6 +93,10 @@ def load() -> ctypes.CDLL:
         L.orx_rollout_concurrent.restype = ctypes.c_int
         L.orx_rollout_concurrent.argtypes = [P(OrxCfg), P(OrxState), i32, i32, i32, vp, vp, i64,
                                              u64, i64, i32, vp]
+    if hasattr(L, "orx_rollout_ex"):
+        L.orx_rollout_ex.restype = ctypes.c_int
+        L.orx_rollout_ex.argtypes = [P(OrxCfg), P(OrxState), i32, i32, i32, vp, vp, i32, i64, u64,
+                                     i64, i32, vp]
     if hasattr(L, "orx_env_step"):
         L.orx_env_step.restype = ctypes.c_int
         L.orx_env_step.argtypes = [P(OrxCfg), P(OrxState), vp, i32, i32, i32, vp, vp, vp, vp, vp,

@@ -2644,19 +2644,35 @@ constexpr int32_t kPartialAux = 0;
 // the launch tables pick an instance by (AUX == kStreamAux) == nt: equal
 // policies would leave one store form with no instance
 static_assert(kStreamAux != kPartialAux, "ORX_STREAM_AUX must differ from the partial-line policy");
-template <bool FAST, int AUX = kStreamAux>
+// ORX_OBS_COMPACT rows (include/orx.h): a cell as x | y << 8 (x, y < 256),
+// two int16 healths in a word, tick | status << 27
+__device__ __forceinline__ uint32_t cell8(int32_t x, int32_t y) {
+  return (uint32_t)x | ((uint32_t)y << 8);
+}
+__device__ __forceinline__ uint32_t compact_hp(int32_t hp1, int32_t hp2) {
+  return ((uint32_t)hp1 & 0xFFFFu) | ((uint32_t)hp2 << 16);
+}
+__device__ __forceinline__ uint32_t compact_ts(int32_t tick, int32_t status) {
+  return (uint32_t)tick | ((uint32_t)status << 27);
+}
+
+// CF: the compact row format (FAST writers; the generic writer reads `fmt`)
+template <bool FAST, int AUX = kStreamAux, bool CF = false>
 struct TrajWriter {
+  static constexpr int kRows = CF ? ORX_OBS_COMPACT_FIELDS : ORX_OBS_FIELDS;
   int32_t* obs;
   int8_t* act;
   uint32_t B, i;
-  uint32_t vo[ORX_OBS_FIELDS], va;
-  __device__ __forceinline__ TrajWriter(int32_t* o, int8_t* a, uint32_t B_, uint32_t i_)
-      : obs(o), act(a), B(B_), i(i_) {
+  int32_t fmt;  // the generic writer's row format
+  uint32_t vo[kRows], va;
+  __device__ __forceinline__ TrajWriter(int32_t* o, int8_t* a, uint32_t B_, uint32_t i_,
+                                        int32_t fmt_ = ORX_OBS_INT32)
+      : obs(o), act(a), B(B_), i(i_), fmt(fmt_) {
     if constexpr (FAST) {
 #pragma unroll
-      for (int f = 0; f < ORX_OBS_FIELDS; ++f) {
+      for (int f = 0; f < kRows; ++f) {
 #ifdef ORX_OBS_TILED  // diagnostic: [T][B/64][14][64] tiles (B a multiple of 64)
-        vo[f] = ((i >> 6) * (uint32_t)ORX_OBS_FIELDS * 64u + (uint32_t)f * 64u + (i & 63u)) * 4u;
+        vo[f] = ((i >> 6) * (uint32_t)kRows * 64u + (uint32_t)f * 64u + (i & 63u)) * 4u;
 #else
         vo[f] = i * 4u + (uint32_t)f * B * 4u;
 #endif
@@ -2669,24 +2685,47 @@ struct TrajWriter {
   // row t, the next row of a FAST writer
   __device__ __forceinline__ void write(int32_t t, const Player& p1, const Player& p2,
                                         int32_t tick, int32_t status, int32_t a1, int32_t a2) {
-    const int32_t vals[ORX_OBS_FIELDS] = {p1.x, p1.y, p1.d, p1.hp, p2.x, p2.y, p2.d, p2.hp,
-                                          tick, status, p1.sx, p1.sy, p2.sx, p2.sy};
     if constexpr (FAST) {
-      const auto ro = __builtin_amdgcn_make_buffer_rsrc(obs, 0, (int32_t)(ORX_OBS_FIELDS * B * 4u),
+      const auto ro = __builtin_amdgcn_make_buffer_rsrc(obs, 0, (int32_t)(kRows * B * 4u),
                                                         kBufferDword3);
+      if constexpr (CF) {
+        const uint32_t vals[kRows] = {cell8(p1.x, p1.y) | (cell8(p2.x, p2.y) << 16),
+                                      cell8(p1.sx, p1.sy) | (cell8(p2.sx, p2.sy) << 16),
+                                      compact_hp(p1.hp, p2.hp), (uint32_t)p1.d, (uint32_t)p2.d,
+                                      compact_ts(tick, status)};
 #pragma unroll
-      for (int f = 0; f < ORX_OBS_FIELDS; ++f)
-        __builtin_amdgcn_raw_buffer_store_b32(vals[f], ro, (int32_t)vo[f], 0, AUX);
+        for (int f = 0; f < kRows; ++f)
+          __builtin_amdgcn_raw_buffer_store_b32(vals[f], ro, (int32_t)vo[f], 0, AUX);
+      } else {
+        const int32_t vals[kRows] = {p1.x, p1.y, p1.d, p1.hp, p2.x, p2.y, p2.d, p2.hp,
+                                     tick, status, p1.sx, p1.sy, p2.sx, p2.sy};
+#pragma unroll
+        for (int f = 0; f < kRows; ++f)
+          __builtin_amdgcn_raw_buffer_store_b32(vals[f], ro, (int32_t)vo[f], 0, AUX);
+      }
       const auto ra = __builtin_amdgcn_make_buffer_rsrc(act, 0, (int32_t)(B * 2u), kBufferDword3);
       __builtin_amdgcn_raw_buffer_store_b16(pack_actions(a1, a2), ra, (int32_t)va, 0, AUX);
-      obs += (size_t)ORX_OBS_FIELDS * B;
+      obs += (size_t)kRows * B;
       act += (size_t)2 * B;
     } else {
       if (obs) {
-        int32_t* o = obs + (size_t)t * ORX_OBS_FIELDS * B;  // uniform row base + lane index
+        if (fmt == ORX_OBS_COMPACT) {
+          const uint32_t vals[ORX_OBS_COMPACT_FIELDS] = {
+              cell8(p1.x, p1.y) | (cell8(p2.x, p2.y) << 16),
+              cell8(p1.sx, p1.sy) | (cell8(p2.sx, p2.sy) << 16), compact_hp(p1.hp, p2.hp),
+              (uint32_t)p1.d, (uint32_t)p2.d, compact_ts(tick, status)};
+          uint32_t* o = reinterpret_cast<uint32_t*>(obs) + (size_t)t * ORX_OBS_COMPACT_FIELDS * B;
 #pragma unroll
-        for (int f = 0; f < ORX_OBS_FIELDS; ++f)
-          __builtin_nontemporal_store(vals[f], (o + (size_t)f * B) + i);
+          for (int f = 0; f < ORX_OBS_COMPACT_FIELDS; ++f)
+            __builtin_nontemporal_store(vals[f], (o + (size_t)f * B) + i);
+        } else {
+          const int32_t vals[ORX_OBS_FIELDS] = {p1.x, p1.y, p1.d, p1.hp, p2.x, p2.y, p2.d, p2.hp,
+                                                tick, status, p1.sx, p1.sy, p2.sx, p2.sy};
+          int32_t* o = obs + (size_t)t * ORX_OBS_FIELDS * B;  // uniform row base + lane index
+#pragma unroll
+          for (int f = 0; f < ORX_OBS_FIELDS; ++f)
+            __builtin_nontemporal_store(vals[f], (o + (size_t)f * B) + i);
+        }
       }
       if (act)
         __builtin_nontemporal_store(pack_actions(a1, a2),
@@ -2702,14 +2741,15 @@ struct TrajWriter {
 // "enemies + items": mana, experience and items, heal optional).  The
 // specialized forms carry no per-tick uniform branches on policy codes or
 // pointers and write the trajectory with buffer stores.
-template <int NCAP, int PM, bool GRID, int AUX = kStreamAux>
+template <int NCAP, int PM, bool GRID, int AUX = kStreamAux, bool CF = false>
 __global__ void __launch_bounds__(kRolloutBlock) rollout_kernel(orx_cfg_t hc, orx_state_t st,
                                                                 int32_t pol1_,
                                                       int32_t pol2_, int32_t n_ticks,
                                                       int32_t* __restrict__ obs,
                                                       int8_t* __restrict__ act, uint32_t B,
                                                       Key key, uint32_t off, uint32_t lanes,
-                                                      uint32_t lds_n, uint32_t lds_bits) {
+                                                      uint32_t lds_n, uint32_t lds_bits,
+                                                      int32_t fmt) {
   constexpr bool kTraj = PM != 0;
   const int32_t pol1 = (PM == 1 || PM == 3) ? (int32_t)ORX_POLICY_RANDOM
                        : PM == 2 ? (int32_t)ORX_POLICY_STAIRCASE : pol1_;
@@ -2774,7 +2814,7 @@ __global__ void __launch_bounds__(kRolloutBlock) rollout_kernel(orx_cfg_t hc, or
   Deltas dl = {0, 0, 0, 0, 0, 0};
   int32_t sep = (c.ext & ORX_EXT_SEPARATION_DAMAGE) ? st.sep_start[i] : -1;
   bool restarted = false;
-  TrajWriter<kTraj, AUX> traj(obs, act, B, i);
+  TrajWriter<kTraj, AUX, CF> traj(obs, act, B, i, fmt);
 #ifdef ORX_STAMPS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
@@ -2878,36 +2918,70 @@ __device__ __forceinline__ uint32_t pack_cell(int32_t x, int32_t y) {
 // 12/13), lane 2j the tick and lane 2j+1 the status (rows 8 and 9), and its
 // own action byte: 7 dword stores and one byte store per tick, each covering
 // two rows, instead of 14 and a 16-bit store.
-template <int AUX>
+// CF (ORX_OBS_COMPACT): three dword rows per lane -- lane 2j the cells (row 0),
+// player 1's depth (3) and tick | status << 27 (5), lane 2j+1 the staircases
+// (1), player 2's depth (4) and the healths (2) -- each cell pair and health
+// pair assembled from the lane's own value and its partner's (DPP).
+template <int AUX, bool CF = false>
 struct PairWriter {
+  static constexpr int kStores = CF ? 3 : 7;
+  static constexpr int kRows = CF ? ORX_OBS_COMPACT_FIELDS : ORX_OBS_FIELDS;
   int32_t* obs;
   int8_t* act;
   uint32_t B;
-  uint32_t vo[7], va;
+  uint32_t vo[kStores], va;
   __device__ __forceinline__ PairWriter(int32_t* o, int8_t* a, uint32_t B_, uint32_t i,
                                         uint32_t who)
       : obs(o), act(a), B(B_) {
-    const uint32_t rows[7] = {0u + 4u * who, 1u + 4u * who, 2u + 4u * who, 3u + 4u * who,
-                              (uint32_t)ORX_OBS_TICK + who, (uint32_t)ORX_OBS_P1_STAIR_X + 2u * who,
-                              (uint32_t)ORX_OBS_P1_STAIR_Y + 2u * who};
+    if constexpr (CF) {
+      const uint32_t rows[3] = {who, 3u + who, who ? 2u : 5u};
 #pragma unroll
-    for (int k = 0; k < 7; ++k) {
-      vo[k] = (rows[k] * B + i) * 4u;
-      asm volatile("" : "+v"(vo[k]));
+      for (int k = 0; k < 3; ++k) {
+        vo[k] = (rows[k] * B + i) * 4u;
+        asm volatile("" : "+v"(vo[k]));
+      }
+    } else {
+      const uint32_t rows[7] = {0u + 4u * who, 1u + 4u * who, 2u + 4u * who, 3u + 4u * who,
+                                (uint32_t)ORX_OBS_TICK + who,
+                                (uint32_t)ORX_OBS_P1_STAIR_X + 2u * who,
+                                (uint32_t)ORX_OBS_P1_STAIR_Y + 2u * who};
+#pragma unroll
+      for (int k = 0; k < 7; ++k) {
+        vo[k] = (rows[k] * B + i) * 4u;
+        asm volatile("" : "+v"(vo[k]));
+      }
     }
     va = 2u * i + who;
     asm volatile("" : "+v"(va));
   }
-  __device__ __forceinline__ void write(const Player& me, int32_t ts, int32_t move) {
-    const int32_t vals[7] = {me.x, me.y, me.d, me.hp, ts, me.sx, me.sy};
-    const auto ro = __builtin_amdgcn_make_buffer_rsrc(obs, 0, (int32_t)(ORX_OBS_FIELDS * B * 4u),
+  // me: this lane's player; kp / ks: its cell and staircase as x | y << 8
+  // (compact only); tick and status: the game's (identical in both lanes)
+  __device__ __forceinline__ void write(const Player& me, uint32_t kp, uint32_t ks, bool isB,
+                                        int32_t tick, int32_t status, int32_t move) {
+    const auto ro = __builtin_amdgcn_make_buffer_rsrc(obs, 0, (int32_t)(kRows * B * 4u),
                                                       kBufferDword3);
+    if constexpr (CF) {
+      // lane 2j assembles the cells, so it takes its partner's cell; lane
+      // 2j+1 the staircases, so it takes its partner's staircase: each lane
+      // offers its partner what the partner assembles
+      const uint32_t a = isB ? ks : kp, give = isB ? kp : ks;
+      const uint32_t sw = (uint32_t)pair_swap((int32_t)give);
+      const uint32_t lo = isB ? sw : a, hi = isB ? a : sw;
+      const int32_t ohp = pair_swap(me.hp);
+      const uint32_t vals[3] = {lo | (hi << 16), (uint32_t)me.d,
+                                isB ? compact_hp(ohp, me.hp) : compact_ts(tick, status)};
 #pragma unroll
-    for (int k = 0; k < 7; ++k)
-      __builtin_amdgcn_raw_buffer_store_b32(vals[k], ro, (int32_t)vo[k], 0, AUX);
+      for (int k = 0; k < 3; ++k)
+        __builtin_amdgcn_raw_buffer_store_b32(vals[k], ro, (int32_t)vo[k], 0, AUX);
+    } else {
+      const int32_t vals[7] = {me.x, me.y, me.d, me.hp, isB ? status : tick, me.sx, me.sy};
+#pragma unroll
+      for (int k = 0; k < 7; ++k)
+        __builtin_amdgcn_raw_buffer_store_b32(vals[k], ro, (int32_t)vo[k], 0, AUX);
+    }
     const auto ra = __builtin_amdgcn_make_buffer_rsrc(act, 0, (int32_t)(B * 2u), kBufferDword3);
     __builtin_amdgcn_raw_buffer_store_b8((uint8_t)move, ra, (int32_t)va, 0, AUX);
-    obs += (size_t)ORX_OBS_FIELDS * B;
+    obs += (size_t)kRows * B;
     act += (size_t)2 * B;
   }
 };
@@ -2920,7 +2994,7 @@ struct PairWriter {
 #ifndef ORX_PAIR_ATTR
 #define ORX_PAIR_ATTR
 #endif
-template <int NCAP, int PM, int AUX, bool SEP>
+template <int NCAP, int PM, int AUX, bool SEP, bool CF = false>
 __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kernel(orx_cfg_t hc, orx_state_t st,
                                                                      int32_t n_ticks,
                                                                      int32_t* __restrict__ obs,
@@ -2966,7 +3040,7 @@ __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kern
   Deltas dl = {0, 0, 0, 0, 0, 0};
   bool restarted = false;
   constexpr int need = PM == 1 ? 2 : 0;
-  PairWriter<AUX> traj(obs, act, B, i, who);
+  PairWriter<AUX, CF> traj(obs, act, B, i, who);
 #ifdef ORX_STAMPS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
@@ -2978,7 +3052,7 @@ __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kern
 #endif
     if constexpr ((ORX_DIAG & 32) != 0) {  // diagnostic: the trajectory stores alone
       tick += 1;
-      traj.write(me, isB ? status : tick, ORX_MOVE_STAY);
+      traj.write(me, kp, ks, isB, tick, status, ORX_MOVE_STAY);
       continue;
     }
     // the bot's move (randombot.py:20-21 / staircasebot.py:9-21)
@@ -3303,7 +3377,7 @@ __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kern
         }
       }
     }
-    if (!(ORX_DIAG & 16)) traj.write(me, isB ? status : tick, move);
+    if (!(ORX_DIAG & 16)) traj.write(me, kp, ks, isB, tick, status, move);
     } while (++t < n_ticks);
   ORX_STAMP(3);
   st.p_x[who * B + i] = me.x;
@@ -3550,7 +3624,7 @@ __global__ void __launch_bounds__(256) mt_rollout_kernel(orx_cfg_t hc, orx_state
                                                          int32_t n_ticks,
                                                          int32_t* __restrict__ obs,
                                                          int8_t* __restrict__ act, uint32_t B,
-                                                         Key key, uint32_t off) {
+                                                         Key key, uint32_t off, int32_t fmt) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= B) return;
   const Cfg c = make_cfg(hc, st);
@@ -3571,7 +3645,7 @@ __global__ void __launch_bounds__(256) mt_rollout_kernel(orx_cfg_t hc, orx_state
   bool stairs_dirty = false, npc_dirty = false;
   MtSrc src;
   src.open(st, c, B, i);
-  TrajWriter<false> traj(obs, act, B, i);
+  TrajWriter<false> traj(obs, act, B, i, fmt);
   for (int32_t t = 0; t < n_ticks; ++t) {
     int32_t a1 = ORX_MOVE_STAY, a2 = ORX_MOVE_STAY;
     bool err = false;
@@ -3723,6 +3797,27 @@ int check_policy(int32_t p) {
   return ORX_OK;
 }
 
+// ORX_OBS_COMPACT's field widths (include/orx.h): u8 cells, int16 healths,
+// a 27-bit tick
+int check_compact(const orx_cfg_t* c) {
+  if (c->width > 256 || c->height > 256)
+    return fail(ORX_EINVAL, "compact rows: width and height must be <= 256");
+  if (c->max_ticks < 1 || c->max_ticks >= (1 << 27))
+    return fail(ORX_EINVAL, "compact rows: max_ticks must be in [1, 2^27)");
+  const int32_t m = ORX_COMPACT_MAX_STAT;
+  bool ok = c->player_health <= m && c->player_damage <= m && c->player_armor >= -m &&
+            (c->n_npcs == 0 || c->npc_damage <= m);
+  if (c->flags & ORX_EXT_MANA) ok = ok && c->mana_max <= m;
+  if (c->flags & ORX_EXT_ITEMS)
+    ok = ok && (int64_t)c->item_bonus * (int64_t)c->item_slots <= m;
+  if (c->flags & ORX_EXT_SEPARATION_DAMAGE)
+    ok = ok && c->max_ticks / (c->sep_period > 0 ? c->sep_period : 1) <= m;
+  if (!ok)
+    return fail(ORX_EINVAL, "compact rows: a health, damage or separation-damage bound above "
+                            "ORX_COMPACT_MAX_STAT (health must fit int16)");
+  return ORX_OK;
+}
+
 int launch_status(const char* what) {
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
@@ -3865,8 +3960,9 @@ struct RolloutPlan {
 RolloutPlan plan_rollout(const orx_cfg_t* cfg, int pm, uint32_t B, uint32_t concurrency) {
   RolloutPlan p;
   p.lanes = rollout_lanes(B);
+  // (its packed cells x | y << 8 need x, y < 256)
   p.paired = ncap_for(cfg->n_npcs) != kDense && cfg->n_layouts == 0 && (pm == 1 || pm == 2) &&
-             p.lanes <= 32u && paired_enabled();
+             cfg->width <= 256 && cfg->height <= 256 && p.lanes <= 32u && paired_enabled();
   if (p.paired) {
     if (const int o = lanes_override()) {
       p.lanes = o < 32 ? (uint32_t)o : 32u;
@@ -4111,11 +4207,23 @@ int orx_rollout_concurrent(const orx_cfg_t* cfg, const orx_state_t* st, int32_t 
                            int32_t policy_p2, int32_t n_ticks, int32_t* obs, int8_t* act,
                            int64_t n_games, uint64_t seed, int64_t game_offset,
                            int32_t concurrency, void* stream) {
+  return orx_rollout_ex(cfg, st, policy_p1, policy_p2, n_ticks, obs, act, ORX_OBS_INT32, n_games,
+                        seed, game_offset, concurrency, stream);
+}
+
+int orx_rollout_ex(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p1,
+                   int32_t policy_p2, int32_t n_ticks, int32_t* obs, int8_t* act,
+                   int32_t obs_format, int64_t n_games, uint64_t seed, int64_t game_offset,
+                   int32_t concurrency, void* stream) {
   int r;
   if (concurrency < 1) return fail(ORX_EINVAL, "concurrency must be >= 1");
   if ((r = check_cfg(cfg)) || (r = check_sizes(n_games, game_offset)) ||
       (r = check_policy(policy_p1)) || (r = check_policy(policy_p2)))
     return r;
+  if (obs_format != ORX_OBS_INT32 && obs_format != ORX_OBS_COMPACT)
+    return fail(ORX_EINVAL, "unknown obs_format");
+  const bool cf = obs_format == ORX_OBS_COMPACT;
+  if (cf && (r = check_compact(cfg))) return r;
   if (policy_p1 == ORX_POLICY_NONE || policy_p2 == ORX_POLICY_NONE)
     return fail(ORX_EINVAL, "orx_rollout needs an action producer for both players");
   if (n_ticks < 0) return fail(ORX_EINVAL, "n_ticks < 0");
@@ -4131,13 +4239,17 @@ int orx_rollout_concurrent(const orx_cfg_t* cfg, const orx_state_t* st, int32_t 
 #define ORX_ROLLOUT(N, G)                                                                       \
   if (nc == N && grid == G)                                                                     \
     hipLaunchKernelGGL((mt_rollout_kernel<N, G>), grid_for(B), dim3(kBlock), 0, s, *cfg, *st,   \
-                       policy_p1, policy_p2, n_ticks, obs, act, B, k, off);
+                       policy_p1, policy_p2, n_ticks, obs, act, B, k, off, obs_format);
     ORX_ROLLOUT(0, false) ORX_ROLLOUT(8, false) ORX_ROLLOUT(16, false) ORX_ROLLOUT(kDense, false)
     ORX_ROLLOUT(0, true) ORX_ROLLOUT(8, true) ORX_ROLLOUT(16, true) ORX_ROLLOUT(kDense, true)
 #undef ORX_ROLLOUT
     return launch_status("orx_rollout");
   }
-  const int pm = rollout_pm(cfg, policy_p1, policy_p2, B, obs && act);
+  int pm = rollout_pm(cfg, policy_p1, policy_p2, B, obs && act);
+  // compact rows: the buffer-store forms of PM 1 / 2 without a bank or dense
+  // NPCs have compact instances; every other launch takes the generic form,
+  // whose writer reads the format at run time
+  if (cf && (pm == 3 || grid || nc == kDense)) pm = 0;
   const RolloutPlan plan = plan_rollout(cfg, pm, B, (uint32_t)concurrency);
   const uint32_t lanes = plan.lanes;
   const uint32_t threads = rollout_threads(B, lanes);
@@ -4169,40 +4281,48 @@ int orx_rollout_concurrent(const orx_cfg_t* cfg, const orx_state_t* st, int32_t 
   if (plan.paired) {
     const dim3 blocks((B + per_block - 1) / per_block);
     const bool sepd = pm == 2 && (cfg->flags & ORX_EXT_SEPARATION_DAMAGE) != 0;
-#define ORX_PAIR(N, P, A, S)                                                                    \
-    if (nc == N && pm == P && (A == kStreamAux) == nt && S == sepd) {                           \
-      hipLaunchKernelGGL((pair_rollout_kernel<N, P, A, S>), blocks, dim3(threads), 0, s, *cfg,  \
-                         *st, n_ticks, obs, act, B, k, off, lanes);                             \
+#define ORX_PAIR(N, P, A, S, C)                                                                 \
+    if (nc == N && pm == P && (A == kStreamAux) == nt && S == sepd && C == cf) {                \
+      hipLaunchKernelGGL((pair_rollout_kernel<N, P, A, S, C>), blocks, dim3(threads), 0, s,     \
+                         *cfg, *st, n_ticks, obs, act, B, k, off, lanes);                       \
       return launch_status("orx_rollout");                                                      \
     }
-#define ORX_PAIRS(N)                                                                            \
-    ORX_PAIR(N, 1, kStreamAux, false) ORX_PAIR(N, 1, kPartialAux, false)                        \
-    ORX_PAIR(N, 2, kStreamAux, false) ORX_PAIR(N, 2, kPartialAux, false)                        \
-    ORX_PAIR(N, 2, kStreamAux, true) ORX_PAIR(N, 2, kPartialAux, true)
+#define ORX_PAIRS_C(N, C)                                                                       \
+    ORX_PAIR(N, 1, kStreamAux, false, C) ORX_PAIR(N, 1, kPartialAux, false, C)                  \
+    ORX_PAIR(N, 2, kStreamAux, false, C) ORX_PAIR(N, 2, kPartialAux, false, C)                  \
+    ORX_PAIR(N, 2, kStreamAux, true, C) ORX_PAIR(N, 2, kPartialAux, true, C)
+#define ORX_PAIRS(N) ORX_PAIRS_C(N, false) ORX_PAIRS_C(N, true)
     ORX_PAIRS(0) ORX_PAIRS(8) ORX_PAIRS(16)
+#undef ORX_PAIRS_C
 #undef ORX_PAIRS
 #undef ORX_PAIR
     return fail(ORX_EIO, "orx_rollout: no paired kernel instance for this plan");
   }
-#define ORX_ROLLOUT_A(N, P, G, A)                                                               \
-  if (nc == N && pm == P && grid == G && (P == 0 || (A == kStreamAux) == nt)) {                \
+#define ORX_ROLLOUT_AC(N, P, G, A, C)                                                           \
+  if (nc == N && pm == P && grid == G && (P == 0 || (A == kStreamAux) == nt) &&                 \
+      (P == 0 || C == cf)) {                                                                    \
     if (lds > 65536u &&                                                                         \
-        hipFuncSetAttribute(reinterpret_cast<const void*>(&rollout_kernel<N, P, G, A>),         \
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&rollout_kernel<N, P, G, A, C>),      \
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) { \
       (void)hipGetLastError();                                                                  \
       if (lds_bits) { lds -= per_block * lds_bits; lds_bits = 0; }                              \
       if (lds > 65536u) return fail(ORX_EIO, "orx_rollout: cannot raise the LDS limit");        \
     }                                                                                           \
-    hipLaunchKernelGGL((rollout_kernel<N, P, G, A>), dim3((B + per_block - 1) / per_block),     \
+    hipLaunchKernelGGL((rollout_kernel<N, P, G, A, C>), dim3((B + per_block - 1) / per_block),  \
                        dim3(threads), lds, s, *cfg, *st,                                        \
                        policy_p1, policy_p2, n_ticks, obs, act, B, k, off, lanes, lds_n,        \
-                       lds_bits);                                                               \
+                       lds_bits, obs_format);                                                   \
     return launch_status("orx_rollout");                                                        \
   }
-// the buffer-store forms in both store policies; the generic form (PM 0) in one
+#define ORX_ROLLOUT_A(N, P, G, A) ORX_ROLLOUT_AC(N, P, G, A, false)
+// the buffer-store forms in both store policies (PM 1 / 2 without a bank also
+// in the compact format); the generic form (PM 0) in one, any format
 #define ORX_ROLLOUT(N, P, G)                                                                    \
   ORX_ROLLOUT_A(N, P, G, kStreamAux)                                                            \
-  if (P != 0) { ORX_ROLLOUT_A(N, P, G, kPartialAux) }
+  if (P != 0) { ORX_ROLLOUT_A(N, P, G, kPartialAux) }                                           \
+  if ((P == 1 || P == 2) && !G && N != kDense) {                                                \
+    ORX_ROLLOUT_AC(N, P, false, kStreamAux, true) ORX_ROLLOUT_AC(N, P, false, kPartialAux, true) \
+  }
   ORX_ROLLOUT(0, 0, false) ORX_ROLLOUT(0, 1, false) ORX_ROLLOUT(0, 2, false)
   ORX_ROLLOUT(8, 0, false) ORX_ROLLOUT(8, 1, false) ORX_ROLLOUT(8, 2, false)
   ORX_ROLLOUT(16, 0, false) ORX_ROLLOUT(16, 1, false) ORX_ROLLOUT(16, 2, false)
@@ -4214,6 +4334,8 @@ int orx_rollout_concurrent(const orx_cfg_t* cfg, const orx_state_t* st, int32_t 
   ORX_ROLLOUT(kDense, 0, false) ORX_ROLLOUT(kDense, 1, false) ORX_ROLLOUT(kDense, 2, false)
   ORX_ROLLOUT(kDense, 0, true) ORX_ROLLOUT(kDense, 1, true) ORX_ROLLOUT(kDense, 2, true)
 #undef ORX_ROLLOUT
+#undef ORX_ROLLOUT_A
+#undef ORX_ROLLOUT_AC
   return fail(ORX_EIO, "orx_rollout: no rollout kernel instance for this plan");
 }
 

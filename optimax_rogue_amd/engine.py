@@ -18,7 +18,30 @@ import torch
 from . import _lib
 from .config import EnvConfig
 from .enums import (EXT_CHARACTER, EXT_ITEMS, EXT_SEPARATION_DAMAGE, MAX_EVENTS,
-                    MAX_REG_NPCS, N_COUNTERS, OBS_FIELDS, RNG_MT19937, RPG_FIELDS, Policy)
+                    MAX_REG_NPCS, N_COUNTERS, OBS_COMPACT, OBS_COMPACT_FIELDS, OBS_FIELDS,
+                    OBS_INT32, RNG_MT19937, RPG_FIELDS, Policy)
+
+
+def obs_rows(obs_format: int = OBS_INT32) -> int:
+    """Rows per tick of a trajectory in ``obs_format`` (14 int32 or 6 compact)."""
+    if obs_format not in (OBS_INT32, OBS_COMPACT):
+        raise ValueError(f"unknown obs_format {obs_format}")
+    return len(OBS_FIELDS) if obs_format == OBS_INT32 else len(OBS_COMPACT_FIELDS)
+
+
+def decode_compact(obs: torch.Tensor) -> torch.Tensor:
+    """ORX_OBS_COMPACT rows [T, 6, B] (int32 storage of the uint32 words) ->
+    the int32 rows [T, 14, B] of OBS_FIELDS, on the rows' device."""
+    w = obs.to(torch.int64) & 0xFFFFFFFF
+    cells, stairs, hp, d1, d2, ts = (w[:, k] for k in range(6))
+    byte = lambda v, k: (v >> (8 * k)) & 0xFF
+    h16 = lambda v: ((v & 0xFFFF) ^ 0x8000) - 0x8000
+    out = torch.stack([byte(cells, 0), byte(cells, 1), obs[:, 3].to(torch.int64), h16(hp),
+                       byte(cells, 2), byte(cells, 3), obs[:, 4].to(torch.int64), h16(hp >> 16),
+                       ts & ((1 << 27) - 1), ts >> 27, byte(stairs, 0), byte(stairs, 1),
+                       byte(stairs, 2), byte(stairs, 3)], dim=1)
+    return out.to(torch.int32)
+
 
 STATE_FIELDS = ("p_x", "p_y", "p_depth", "p_health", "st_x", "st_y", "tick", "status", "episode",
                 "ret_sum", "ep_count", "counters", "npc_pos", "npc_health", "npc_alive")
@@ -159,19 +182,22 @@ class BatchedEngine:
         _lib.check(name, code)
 
     def rollout_launcher(self, n_ticks: int, p1: int = Policy.Random, p2: int = Policy.Random,
-                         obs: Optional[torch.Tensor] = None, act: Optional[torch.Tensor] = None):
+                         obs: Optional[torch.Tensor] = None, act: Optional[torch.Tensor] = None,
+                         obs_format: int = OBS_INT32):
         """A zero-argument callable that launches ``rollout(n_ticks, p1, p2, obs,
-        act)`` on the current stream of this moment, its C arguments bound once
-        (a timed loop then pays one ctypes call per launch, nothing else)."""
-        self._check_traj(n_ticks, obs, act)
-        fn, check = self.lib.orx_rollout_concurrent, _lib.check
+        act, obs_format)`` on the current stream of this moment, its C
+        arguments bound once (a timed loop then pays one ctypes call per
+        launch, nothing else)."""
+        self._check_traj(n_ticks, obs, act, obs_format)
+        fn, check = self.lib.orx_rollout_ex, _lib.check
         args = (self._pcfg, self._pst, int(p1), int(p2), int(n_ticks), _ptr(obs), _ptr(act),
-                self.B, self.seed, self.game_offset, int(self.concurrency), self._stream())
+                int(obs_format), self.B, self.seed, self.game_offset, int(self.concurrency),
+                self._stream())
 
         def launch():
             code = fn(*args)
             if code:
-                check("orx_rollout_concurrent", code)
+                check("orx_rollout_ex", code)
         return launch
 
     def rollout_lanes(self) -> int:
@@ -275,13 +301,16 @@ class BatchedEngine:
         return a
 
     def rollout(self, n_ticks: int, p1: int = Policy.Random, p2: int = Policy.Random,
-                obs: Optional[torch.Tensor] = None, act: Optional[torch.Tensor] = None) -> None:
+                obs: Optional[torch.Tensor] = None, act: Optional[torch.Tensor] = None,
+                obs_format: int = OBS_INT32) -> None:
         """n_ticks x (policy, step) fused in one launch.  ``obs`` (int32
-        [n_ticks, len(OBS_FIELDS), n_games]) and ``act`` (int8 [n_ticks,
-        n_games, 2]) receive every tick's observation and actions."""
-        self._check_traj(n_ticks, obs, act)
-        self._call("orx_rollout_concurrent", int(p1), int(p2), int(n_ticks), _ptr(obs), _ptr(act),
-                   self.B, self.seed, self.game_offset, int(self.concurrency), self._stream())
+        [n_ticks, obs_rows(obs_format), n_games]: the 14 OBS_FIELDS rows, or
+        with OBS_COMPACT the 6 compact rows, decode_compact) and ``act`` (int8
+        [n_ticks, n_games, 2]) receive every tick's observation and actions."""
+        self._check_traj(n_ticks, obs, act, obs_format)
+        self._call("orx_rollout_ex", int(p1), int(p2), int(n_ticks), _ptr(obs), _ptr(act),
+                   int(obs_format), self.B, self.seed, self.game_offset, int(self.concurrency),
+                   self._stream())
 
     def _check_actions(self, a: torch.Tensor, what: str) -> None:
         # the kernels index [n_games, 2] blindly: a wrong buffer would be an
@@ -291,9 +320,10 @@ class BatchedEngine:
             raise ValueError(f"{what} must be a contiguous int8 [n_games, 2] tensor on "
                              f"{self.device}")
 
-    def _check_traj(self, n_ticks, obs, act):
-        for t, dt, n, what in ((obs, torch.int32, n_ticks * len(OBS_FIELDS) * self.B,
-                                "obs must be a contiguous int32 [n_ticks, 14, n_games] tensor"),
+    def _check_traj(self, n_ticks, obs, act, obs_format=OBS_INT32):
+        rows = obs_rows(obs_format)
+        for t, dt, n, what in ((obs, torch.int32, n_ticks * rows * self.B,
+                                f"obs must be a contiguous int32 [n_ticks, {rows}, n_games] tensor"),
                                (act, torch.int8, n_ticks * self.B * 2,
                                 "act must be a contiguous int8 [n_ticks, n_games, 2] tensor")):
             if t is not None and (t.dtype != dt or t.numel() < n or not t.is_contiguous()
@@ -541,15 +571,16 @@ class StreamShardedEngine:
         for s in self.streams:
             cur.wait_stream(s)
 
-    def trajectory_buffers(self, n_ticks: int):
-        """Per-shard obs int32 [n_ticks, 14, count] and act int8 [n_ticks, count, 2]."""
-        return ([torch.empty((n_ticks, len(OBS_FIELDS), e.B), dtype=torch.int32,
+    def trajectory_buffers(self, n_ticks: int, obs_format: int = OBS_INT32):
+        """Per-shard obs int32 [n_ticks, obs_rows(obs_format), count] and act
+        int8 [n_ticks, count, 2]."""
+        return ([torch.empty((n_ticks, obs_rows(obs_format), e.B), dtype=torch.int32,
                              device=self.device) for e in self.parts],
                 [torch.empty((n_ticks, e.B, 2), dtype=torch.int8, device=self.device)
                  for e in self.parts])
 
     def rollout_launcher(self, n_ticks: int, p1: int = Policy.Random, p2: int = Policy.Random,
-                         obs=None, act=None):
+                         obs=None, act=None, obs_format: int = OBS_INT32):
         """A zero-argument callable launching every shard's rollout on its own
         stream (``obs``/``act``: per-shard lists, or None).  Ordering against
         the caller's stream is explicit: ``fork()`` before (the shards wait for
@@ -561,7 +592,8 @@ class StreamShardedEngine:
         go = []
         for e, s, o, a in zip(self.parts, self.streams, obs, act):
             with torch.cuda.stream(s):
-                go.append(e.rollout_launcher(n_ticks, p1, p2, obs=o, act=a))
+                go.append(e.rollout_launcher(n_ticks, p1, p2, obs=o, act=a,
+                                             obs_format=obs_format))
 
         def launch():
             for g in go:

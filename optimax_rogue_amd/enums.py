@@ -103,6 +103,13 @@ OBS_FIELDS = ("p1_x", "p1_y", "p1_depth", "p1_health", "p2_x", "p2_y", "p2_depth
               "p2_health", "tick", "status", "p1_stair_x", "p1_stair_y", "p2_stair_x",
               "p2_stair_y")
 
+# trajectory row formats of orx_rollout_ex (include/orx.h ORX_OBS_*): the
+# int32 rows above, or the compact uint32 rows (cells as u8 pairs, int16
+# healths, tick | status << 27): 24 bytes per env-step instead of 56
+OBS_INT32, OBS_COMPACT = 0, 1
+OBS_COMPACT_FIELDS = ("cells", "stairs", "health", "p1_depth", "p2_depth", "tick_status")
+COMPACT_MAX_STAT = 8000
+
 # update-event records of orx_step_events (include/orx.h ORX_EV_*)
 EV_COMBAT, EV_DEATH, EV_POSITION, EV_DUNGEON, EV_HEALTH = 1, 2, 3, 4, 5
 MAX_EVENTS = 8

@@ -736,6 +736,32 @@ def test_paired_rollout_vs_oracle(name, oracle_lib):
     torch.cuda.synchronize()
 
 
+@pytest.mark.parametrize("wh", [(300, 260), (256, 256)])
+def test_wide_grid_rollout_form_vs_oracle(wh, oracle_lib):
+    """The paired form packs cells as x | y << 8, so it runs only on grids up
+    to 256 x 256; a wider NPC-free grid takes the one-lane form (round 3's
+    plan paired it and would have rebuilt x from 8 bits).  StaircaseBots
+    (they reach the far cells) against the oracle."""
+    import torch
+    from optimax_rogue_amd.enums import OBS_FIELDS
+    W, H = wh
+    cfg = dict(width=W, height=H, max_ticks=400)
+    B, T, seed = 512, 150, 31
+    ora = oracle_lib.Oracle(cfg, B, seed, 0)
+    ora.reset(episode=np.zeros(B, np.int32))
+    eng = _engine(cfg, B, seed)
+    assert eng.rollout_shape(2, 2)["lanes_per_game"] == (2 if W <= 256 else 1)
+    obs = torch.zeros((T, len(OBS_FIELDS), B), dtype=torch.int32, device=eng.device)
+    act = torch.zeros((T, B, 2), dtype=torch.int8, device=eng.device)
+    for launch in range(3):
+        want_act, want_obs = _replay(ora, T, (2, 2))
+        eng.rollout(T, 2, 2, obs=obs, act=act)
+        compare_state(eng.snapshot(), ora.export(), 0, f"{wh} launch {launch}")
+        assert np.array_equal(act.cpu().numpy(), want_act), f"{wh} actions {launch}"
+        assert np.array_equal(obs.cpu().numpy(), want_obs), f"{wh} obs {launch}"
+    assert (eng.snapshot()["p_x"] > 255).any() or W <= 256
+
+
 def test_dense_npc_character_trajectory_vs_oracle(oracle_lib):
     """Dense NPCs (K > 16) with the character mechanics and RandomBots, WITH
     trajectory buffers: the generic rollout form (there is no dense instance
@@ -758,3 +784,62 @@ def test_dense_npc_character_trajectory_vs_oracle(oracle_lib):
         assert np.array_equal(act.cpu().numpy(), want_act), f"actions {launch}"
         assert np.array_equal(obs.cpu().numpy(), want_obs), f"obs {launch}"
     assert int(eng.snapshot()["episode"].sum()) > 0
+
+
+# ORX_OBS_COMPACT trajectory rows: every launch form -- the paired compact
+# instances (the bench's C3 shards, C2, C5 with separation damage), the
+# one-lane compact instances (C5 and C3 at full waves), and the generic form
+# that reads the format at run time (character mechanics, a dungeon bank,
+# dense NPCs, stock seeding) -- decodes to exactly the int32 rows of the same
+# launches, with identical actions and state.
+COMPACT_FORMS = {
+    "c3_bench_shards": (dict(width=64, height=64, n_npcs=8), (1, 1), 65536, 2, 2),
+    "c2_pair": (dict(width=32, height=32), (1, 1), 4096, 1, 2),
+    "c5_pair_sep": (dict(width=128, height=128, flags=1, sep_period=8), (2, 2), 16384, 1, 2),
+    "c5_one_lane": (dict(width=128, height=128), (2, 2), 131072, 1, 1),
+    "c3_one_lane": (dict(width=64, height=64, n_npcs=8, max_ticks=90), (1, 1), 65536, 1, 1),
+    "rpg_generic": (dict(width=16, height=16, n_npcs=8, flags=4 | 16 | 32, max_ticks=80), (1, 1),
+                    4096, 1, 1),
+    "bank_generic": (dict(width=20, height=16, n_npcs=4, max_ticks=70), (2, 1), 3001, 1, 1),
+    "dense_generic": (dict(width=12, height=12, n_npcs=30, max_ticks=60), (1, 2), 2048, 1, 1),
+    "stock_mt": (dict(width=10, height=9, n_npcs=4, max_ticks=60, rng=1), (1, 2), 1024, 1, 1),
+}
+
+
+@pytest.mark.parametrize("name", sorted(COMPACT_FORMS))
+def test_compact_rows_equal_int32_rows(name):
+    import torch
+    from optimax_rogue_amd import DungeonBank, EnvConfig
+    from optimax_rogue_amd.engine import StreamShardedEngine, decode_compact
+    from optimax_rogue_amd.enums import OBS_COMPACT, OBS_INT32
+    cfgd, pol, B, streams, lanes = COMPACT_FORMS[name]
+    layouts = DungeonBank.random(20, 16, 6, seed=3, n_stairs=2).layouts \
+        if name == "bank_generic" else None
+    cfg = EnvConfig.from_dict(cfgd, layouts=layouts)
+    dev = torch.device("cuda", 0)
+    T = 64 if B >= 65536 else 100
+    res = []
+    for fmt in (OBS_INT32, OBS_COMPACT):
+        eng = StreamShardedEngine(cfg, B, seed=21, game_offset=3, device=dev, n_streams=streams)
+        if name != "stock_mt" and fmt == OBS_INT32:
+            assert eng.rollout_shape(*pol)["lanes_per_game"] == lanes, name
+        obs, act = eng.trajectory_buffers(T, fmt)
+        go = eng.rollout_launcher(T, *pol, obs=obs, act=act, obs_format=fmt)
+        rows, acts = [], []
+        for _ in range(2):
+            eng.fork()
+            go()
+            eng.join()
+            o = torch.cat(obs, dim=2)
+            rows.append((decode_compact(o) if fmt == OBS_COMPACT else o).cpu().numpy())
+            acts.append(torch.cat(act, dim=1).cpu().numpy())
+        res.append((rows, acts, eng.snapshot()))
+        del eng, obs, act
+        torch.cuda.empty_cache()
+    (r0, a0, s0), (r1, a1, s1) = res
+    for k in range(2):
+        assert np.array_equal(r0[k], r1[k]), (name, k)
+        assert np.array_equal(a0[k], a1[k]), (name, k)
+    for k in s0:
+        assert np.array_equal(s0[k], s1[k]), (name, k)
+    assert s0["ep_count"].sum() > 0 or name.startswith("c3_bench") or name.startswith("c5")

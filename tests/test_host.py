@@ -138,3 +138,59 @@ def test_vecenv_step_passes_bad_actions_to_the_engine(bad):
     assert shape == (3, 14) and rd == torch.float32 and dd == torch.bool and sd == torch.int32
     with pytest.raises(ValueError, match="integer"):
         env.step(torch.tensor([1.0, 2.0, 3.0]))
+
+
+def _encode_compact(rows):
+    """The compact encoding of int32 rows [T, 14, B], restated in numpy
+    (include/orx.h ORX_OBS_COMPACT)."""
+    r = rows.astype(np.int64)
+    cell = lambda x, y: (x & 0xFF) | ((y & 0xFF) << 8)
+    w = np.stack([cell(r[:, 0], r[:, 1]) | (cell(r[:, 4], r[:, 5]) << 16),
+                  cell(r[:, 10], r[:, 11]) | (cell(r[:, 12], r[:, 13]) << 16),
+                  (r[:, 3] & 0xFFFF) | ((r[:, 7] & 0xFFFF) << 16), r[:, 2] & 0xFFFFFFFF,
+                  r[:, 6] & 0xFFFFFFFF, r[:, 8] | (r[:, 9] << 27)], axis=1)
+    return w.astype(np.uint32).view(np.int32)
+
+
+def test_decode_compact_round_trip():
+    """decode_compact inverts the compact encoding over the fields' full
+    ranges: cells and staircases 0..255, healths -32768..32767, depths to
+    2^31-1, ticks to 2^27-1, every status code."""
+    import torch
+    from optimax_rogue_amd.engine import decode_compact
+    rs = np.random.RandomState(0)
+    T, B = 3, 4000
+    rows = np.zeros((T, 14, B), np.int64)
+    for f in (0, 1, 4, 5, 10, 11, 12, 13):
+        rows[:, f] = rs.randint(0, 256, (T, B))
+    for f in (3, 7):
+        rows[:, f] = rs.randint(-32768, 32768, (T, B))
+    for f in (2, 6):
+        rows[:, f] = rs.randint(0, 2**31 - 1, (T, B))
+    rows[:, 8] = rs.randint(0, 2**27, (T, B))
+    rows[:, 9] = rs.choice([1, 2, 3, 4, 16, 17], (T, B))
+    got = decode_compact(torch.from_numpy(_encode_compact(rows))).numpy()
+    assert got.dtype == np.int32 and np.array_equal(got, rows.astype(np.int32))
+
+
+def test_compact_rows_refuse_what_does_not_fit():
+    """orx_rollout_ex(ORX_OBS_COMPACT) refuses configurations whose values
+    the compact fields cannot hold, before any device work."""
+    import ctypes
+    from optimax_rogue_amd import EnvConfig, _lib
+    from optimax_rogue_amd.enums import OBS_COMPACT
+    lib = _lib.load()
+    st = _lib.OrxState()
+
+    def rc(cfg, fmt=OBS_COMPACT):
+        return lib.orx_rollout_ex(ctypes.byref(cfg.to_c()), ctypes.byref(st), 1, 1, 4, None,
+                                  None, fmt, 8, 1, 0, 1, None)
+    for bad in (EnvConfig(width=300, height=20), EnvConfig(max_ticks=0),
+                EnvConfig(max_ticks=1 << 27), EnvConfig(player_health=9000),
+                EnvConfig(flags=1, sep_period=1, max_ticks=9000),
+                EnvConfig(n_npcs=2, npc_damage=20000)):
+        assert rc(bad) == -22, bad
+        assert "compact" in lib.orx_last_error().decode()
+    assert rc(EnvConfig(), fmt=7) == -22
+    # a fitting configuration passes the format checks (then fails on the NULL state)
+    assert rc(EnvConfig.c3()) == -22 and "compact" not in lib.orx_last_error().decode()
