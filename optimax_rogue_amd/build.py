@@ -36,6 +36,7 @@ VARIANTS = {
     "diag16": ("ORX_DIAG=16",),   # rollout without its trajectory stores
     "diag32": ("ORX_DIAG=32",),   # the trajectory stores alone (no tick runs)
     "stamps": ("ORX_STAMPS",),    # per-wave s_memtime stamps + rare-block counts
+    "diag64": ("ORX_DIAG=64",),   # the paired RandomBot tick block without Philox
 }
 
 
