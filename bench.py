@@ -218,7 +218,7 @@ def extras(torch, cfg, dev, B_cfg, K, large_rollout=False):
     off by default so that a profile of the bench command sees that kernel at
     the headline shape only), C2 and C5."""
     from optimax_rogue_amd import OBS_FIELDS
-    from optimax_rogue_amd.engine import BatchedEngine
+    from optimax_rogue_amd.engine import BatchedEngine, StreamShardedEngine
     out = {}
     # (1) unfused policy+step, 50 ticks captured in one HIP graph, config batch
     eng = BatchedEngine(cfg, B_cfg, seed=3, device=dev)
@@ -312,11 +312,24 @@ def extras(torch, cfg, dev, B_cfg, K, large_rollout=False):
     from optimax_rogue_amd import EnvConfig
     from optimax_rogue_amd.enums import EXT_SEPARATION_DAMAGE
 
-    def rollout_rate(c, games, pol, T=128, reps=6):
-        e = BatchedEngine(c, games, seed=5, device=dev)
-        o = torch.empty((T, len(OBS_FIELDS), games), dtype=torch.int32, device=dev)
-        a = torch.empty((T, games, 2), dtype=torch.int8, device=dev)
-        go = e.rollout_launcher(T, pol, pol, obs=o, act=a)
+    def rollout_rate(c, games, pol, T=128, reps=6, streams=1):
+        """µs per T-tick launch of `games` (median of `reps`); with streams > 1
+        the games run as that many stream shards, as the headline step does
+        (StreamShardedEngine; a step = one launch per shard, fork/join)."""
+        if streams > 1:
+            e = StreamShardedEngine(c, games, seed=5, device=dev, n_streams=streams)
+            o, a = e.trajectory_buffers(T)
+            go1 = e.rollout_launcher(T, pol, pol, obs=o, act=a)
+
+            def go():
+                e.fork()
+                go1()
+                e.join()
+        else:
+            e = BatchedEngine(c, games, seed=5, device=dev)
+            o = torch.empty((T, len(OBS_FIELDS), games), dtype=torch.int32, device=dev)
+            a = torch.empty((T, games, 2), dtype=torch.int8, device=dev)
+            go = e.rollout_launcher(T, pol, pol, obs=o, act=a)
         go()
         d = timed_launches(torch, go, reps)
         us = sorted(d)[len(d) // 2]
@@ -324,12 +337,11 @@ def extras(torch, cfg, dev, B_cfg, K, large_rollout=False):
         del e, o, a, go
         return {"games": games, "ticks_per_launch": T, "games_per_wave": shape["games_per_wave"],
                 "lanes_per_game": shape["lanes_per_game"], "nontemporal": shape["nontemporal"],
-                "us_per_launch": us * 1e6, "env_steps_per_s": games * T / us}
+                "streams": streams, "us_per_launch": us * 1e6, "env_steps_per_s": games * T / us}
 
     # (3a) the headline step with ORX_OBS_COMPACT trajectory rows (24 B per
     # env-step instead of 56: u8 cells and staircases, int16 healths,
     # tick | status << 27; the same launches, shards and stream layout)
-    from optimax_rogue_amd.engine import StreamShardedEngine
     from optimax_rogue_amd.enums import OBS_COMPACT
     sh = StreamShardedEngine(cfg, B_cfg, seed=3, device=dev, n_streams=2)
     T = 128
@@ -366,18 +378,21 @@ def extras(torch, cfg, dev, B_cfg, K, large_rollout=False):
     from optimax_rogue_amd import DungeonBank
     bank = DungeonBank.random(64, 64, 16, seed=7)
     out["bank"] = dict(rollout_rate(EnvConfig(width=64, height=64, n_npcs=8, layouts=bank.layouts),
-                                    65536, 1),
+                                    65536, 1, streams=2),
                        policy="2x RandomBot", grid="64x64, 16 layouts (15% walls)",
-                       note="tiles staged in LDS (64 KiB)")
+                       note="two stream shards as the headline step (the paired form, tiles "
+                            "staged in LDS: 64 KiB); us_per_launch = one step")
     # configs[2] read literally, "64x64 grid with enemies+items enabled": C3 with
     # the readme's character mechanics on (build extensions, no reference
     # semantics, so not the bit-exact headline)
     from optimax_rogue_amd.enums import EXT_RPG
     out["c3_rpg"] = dict(rollout_rate(EnvConfig(width=64, height=64, n_npcs=8, flags=EXT_RPG),
-                                      65536, 1),
+                                      65536, 1, streams=2),
                          policy="2x RandomBot", grid="64x64, 8 NPCs",
                          note="mana, heal, experience, item drops/pickup on (EXT_RPG; engine "
-                              "vs oracle bit-exact, parity unpinned vs the reference)")
+                              "vs oracle bit-exact, parity unpinned vs the reference); two "
+                              "stream shards as the headline step (the paired form); "
+                              "us_per_launch = one step")
     c5 = {}
     for flag in (0, EXT_SEPARATION_DAMAGE):
         c = EnvConfig.c5()

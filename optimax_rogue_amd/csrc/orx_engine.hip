@@ -3017,9 +3017,11 @@ struct PairStageWriter {
   uint32_t ao;    // action flush: (tick * B + i0 + 4 q) * 2
   uint32_t fk;    // the flush lane's tick
   __device__ __forceinline__ PairStageWriter(int32_t* o, int8_t* a, uint32_t B_, uint32_t i,
-                                             uint32_t who, uint32_t lanes, bool enable)
+                                             uint32_t who, uint32_t lanes, bool enable,
+                                             uint32_t base)
       : direct(o, a, B_, i, who), obs(o), act(a), B(B_), G(lanes) {
-    const uint32_t wave = (threadIdx.x >> 6) * kStageWaveBytes;
+    // (base: the LDS bytes before the stage region -- a dungeon bank's tiles)
+    const uint32_t wave = base + (threadIdx.x >> 6) * kStageWaveBytes;
     const uint32_t j = (threadIdx.x & 63u) >> 1;   // game within the wave
     i0 = (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(i - j));   // (uniform)
     staged = enable && (G & 3u) == 0u && G <= 16u && (B & 3u) == 0u && i0 + G <= B;
@@ -3092,14 +3094,37 @@ struct PairStageWriter {
 #ifndef ORX_PAIR_ATTR
 #define ORX_PAIR_ATTR
 #endif
-template <int NCAP, int PM, int AUX, bool SEP, bool CF = false>
+// GRID (round 4): a dungeon bank -- each lane reads its target's tile (its
+// player's layout; LDS-staged when the bank fits, lds_n bytes), a Wall or the
+// grid's edge blocks, ANY staircase tile makes the tick rare; descends and
+// resets take rare_tick's bank forms (the closed-form fast paths are for
+// empty dungeons).
+template <int NCAP, int PM, int AUX, bool SEP, bool CF = false, bool GRID = false>
 __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kernel(orx_cfg_t hc, orx_state_t st,
                                                                      int32_t n_ticks,
                                                                      int32_t* __restrict__ obs,
                                                                      int8_t* __restrict__ act,
                                                                      uint32_t B, Key key,
                                                                      uint32_t off, uint32_t lanes,
-                                                                     uint32_t stage) {
+                                                                     uint32_t stage,
+                                                                     uint32_t lds_n) {
+  bool lds_tiles = false;
+  if constexpr (GRID) {  // stage the bank's tiles in LDS (the whole block, before any exit)
+    if (lds_n > 0u) {
+      const uint8_t* src = st.bank_tiles;
+      for (uint32_t k = threadIdx.x * 4u; k < lds_n; k += blockDim.x * 4u) {
+        if (k + 4u <= lds_n) {
+          uint32_t v;
+          __builtin_memcpy(&v, src + k, 4);
+          __builtin_memcpy(orx_lds_tiles + k, &v, 4);
+        } else {
+          for (uint32_t j = k; j < lds_n; ++j) orx_lds_tiles[j] = src[j];
+        }
+      }
+      __syncthreads();
+      lds_tiles = true;
+    }
+  }
   const uint32_t lane = threadIdx.x & 63u;
   if (lane >= 2u * lanes) return;  // uniform per wave
   const uint32_t i = ((blockIdx.x * blockDim.x + threadIdx.x) >> 6) * lanes + (lane >> 1);
@@ -3107,7 +3132,11 @@ __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kern
   const uint32_t who = lane & 1u;  // 0: player 1, 1: player 2
   const bool isB = who != 0u;
   Cfg c = make_cfg(hc, st);
-  c.ext = SEP ? ORX_EXT_SEPARATION_DAMAGE : 0;  // PM 1: none; PM 2: at most this one
+  // PM 1: no extension; PM 2: at most separation damage; PM 3: mana,
+  // experience and items (HEAL is inert: the bots never heal)
+  c.ext = PM == 3 ? (ORX_EXT_MANA | ORX_EXT_LEVELING | ORX_EXT_ITEMS)
+                  : SEP ? ORX_EXT_SEPARATION_DAMAGE : 0;
+  c.lds_tiles = lds_tiles;
   const uint32_t game = off + i;
   ORX_STAMP(0);
   Player me;
@@ -3117,10 +3146,19 @@ __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kern
   me.hp = st.p_health[who * B + i];
   me.sx = st.st_x[who * B + i];
   me.sy = st.st_y[who * B + i];
-  me.lay = -1;
+  me.lay = GRID ? st.p_layout[who * B + i] : -1;
   me.move = ORX_MOVE_STAY;
   me.tx = me.ty = 0;
   me.mana = me.xp = me.dmg = me.mhp = me.nitems = me.cool = me.heal = me.hd = 0;
+  if constexpr (PM == 3) {  // this lane's player's attributes (p_rpg [field][2][B])
+    const int32_t* r = st.p_rpg + who * B + i;
+    const size_t f = 2 * (size_t)B;
+    me.mana = r[ORX_RPG_MANA * f];
+    me.xp = r[ORX_RPG_XP * f];
+    me.dmg = r[ORX_RPG_DAMAGE * f];
+    me.mhp = r[ORX_RPG_MAX_HEALTH * f];
+    me.nitems = r[ORX_RPG_ITEMS * f];
+  }
   uint32_t kp = pack_cell(me.x, me.y), ks = pack_cell(me.sx, me.sy);  // packed cells
   uint32_t dk = me.d == c.d1 ? 0u : 0x80008000u;  // off the NPCs' depth (npc_any1_dk)
   int32_t tick = st.tick[i];
@@ -3136,13 +3174,20 @@ __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kern
   if constexpr (NCAP > 0) hp.load(st.npc_health, c.K, B, i);
   Items<NCAP> items;
   items.clear();
+  if constexpr (PM == 3 && NCAP > 0) {  // the game's items, in their NPCs' slots (both lanes)
+    items.on = st.item_mask[i];
+    items.kind = st.item_mask[B + i];
+    for (int k = 0; k < c.K; ++k)
+      if ((items.on >> k) & 1u) npc.set(k, st.item_pos[(size_t)k * B + i]);
+  }
   Deltas dl = {0, 0, 0, 0, 0, 0};
   bool restarted = false;
-  constexpr int need = PM == 1 ? 2 : 0;
+  constexpr int need = (PM == 1 || PM == 3) ? 2 : 0;
   // partial-line int32 rows: staged through LDS (PairStageWriter)
   constexpr bool kStage = AUX == kPartialAux && !CF;
   std::conditional_t<kStage, PairStageWriter, PairWriter<AUX, CF>> traj = [&] {
-    if constexpr (kStage) return PairStageWriter(obs, act, B, i, who, lanes, stage != 0u);
+    if constexpr (kStage)
+      return PairStageWriter(obs, act, B, i, who, lanes, stage != 0u, (lds_n + 15u) & ~15u);
     else return PairWriter<AUX, CF>(obs, act, B, i, who);
   }();
 #ifdef ORX_STAMPS
@@ -3163,7 +3208,7 @@ __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kern
     W4 tb = {0u, 0u, 0u, 0u};
     uint32_t h0 = 0u, h3 = 0u;  // PM 1: the tick block's deferred words c, d
     int32_t move;
-    if constexpr (PM == 1) {
+    if constexpr (PM == 1 || PM == 3) {
       // the tick block in both lanes; player 1 takes the first accepted 3-bit
       // field of word b, player 2 the second (as rollout_tick)
       if constexpr ((ORX_DIAG & 64) != 0) {  // diagnostic: a cheap hash for the tick block
@@ -3195,8 +3240,20 @@ __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kern
     // effective target (own cell when blocked: the border, clamped)
     int32_t tx, ty;
     calc_pos(me.x, me.y, move, tx, ty);
-    tx = med3_1(tx, c.W - 2);
-    ty = med3_1(ty, c.H - 2);
+    bool st_tile = false;  // GRID: the target tile is a staircase
+    if constexpr (GRID) {
+      // one tile read: a Wall or the grid's edge blocks (a blocked player's
+      // own cell is never a staircase)
+      const bool in = (uint32_t)tx < (uint32_t)c.W && (uint32_t)ty < (uint32_t)c.H;
+      const uint32_t tile = bank_tile(c, me.lay, in ? tx : me.x, in ? ty : me.y);
+      const bool blk = !in || tile == ORX_TILE_WALL;
+      st_tile = !blk && tile == ORX_TILE_STAIRCASE_DOWN;
+      tx = blk ? me.x : tx;
+      ty = blk ? me.y : ty;
+    } else {
+      tx = med3_1(tx, c.W - 2);
+      ty = med3_1(ty, c.H - 2);
+    }
     const uint32_t kt = pack_cell(tx, ty);
     // The rare test on packed cells (x | y << 8): a meet is both players on
     // one depth with my target on the other's cell, the other's target on
@@ -3209,7 +3266,8 @@ __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kern
     const uint32_t mt = min(e_mo, min(e_om, e_tt)) | e_d;  // 0: a meet
     bool hit_me = false;
     if constexpr (NCAP > 0) hit_me = npc_any1_dk(npc, kt, dk);
-    const uint32_t z = hit_me ? 0u : (kt ^ ks);  // 0: my staircase or an NPC on my target
+    // 0: my staircase (GRID: any staircase tile) or an NPC on my target
+    const uint32_t z = (hit_me | st_tile) ? 0u : GRID ? 1u : (kt ^ ks);
     const bool rare = !in_progress | (min(mt, min_swapped(z)) == 0u);
     const int32_t ft = tick + 1;
     const bool end = c.max_ticks && ft >= c.max_ticks;
@@ -3219,7 +3277,7 @@ __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kern
       ORX_COUNT(dl.n_rare);
       ORX_CYC_BEGIN(cy0);
 #endif
-      if constexpr (PM == 1) {  // the tick block's words c and d (rare_tick's fallbacks)
+      if constexpr (PM == 1 || PM == 3) {  // the tick block's words c, d (rare_tick's fallbacks)
         asm volatile("" : "+v"(h0), "+v"(h3));
         finish_cd(tb, h0, h3, key);
       }
@@ -3242,7 +3300,12 @@ __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kern
       const int32_t ox = pair_swap(lx), oy = pair_swap(ly), od = pair_swap(ld);
       const int32_t otx = pair_swap(ltx), oty = pair_swap(lty);
       const bool meet = mt == 0u;
-      const bool st_me = (ltx == lsx) & (lty == lsy);
+      bool st_me = (ltx == lsx) & (lty == lsy);
+      if constexpr (GRID) {
+        int32_t sl = st_tile ? 1 : 0;
+        asm volatile("" : "+v"(sl));
+        st_me = sl != 0;
+      }
       const int32_t st_o = pair_swap(st_me ? 1 : 0);
       const int32_t hit_o = pair_swap(hit_me ? 1 : 0);
       // One player descends (C5's common rare tick; StaircaseBots only),
@@ -3251,7 +3314,7 @@ __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kern
       // instruction stream for both -- and the lanes swap them.
       bool fast = false;
       const int32_t osx = pair_swap(me.sx), osy = pair_swap(me.sy);
-      if constexpr (PM == 2 && NCAP == 0) {
+      if constexpr (PM == 2 && NCAP == 0 && !GRID) {
         if (!in_progress & (c.autoreset != 0)) {  // uniform over the pair
           // The next episode (setup_game's keyed first-block form), its two
           // starting dungeons split over the pair: each lane draws its own
@@ -3373,7 +3436,8 @@ __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kern
 #endif
         }
       }
-      if (PM == 2 && (in_progress & !meet & (st_me != (st_o != 0)) & !hit_me & (hit_o == 0))) {
+      if (PM == 2 && !GRID &&
+          (in_progress & !meet & (st_me != (st_o != 0)) & !hit_me & (hit_o == 0))) {
 #ifdef ORX_STAMPS
         ORX_CYC_BEGIN(cyf);
 #endif
@@ -3440,8 +3504,16 @@ __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kern
         o.sx = osx;
         o.sy = osy;
         o.move = pair_swap(move);
+        if constexpr (GRID) o.lay = pair_swap(me.lay);
+        if constexpr (PM == 3) {  // the other player's attributes
+          o.mana = pair_swap(me.mana);
+          o.xp = pair_swap(me.xp);
+          o.dmg = pair_swap(me.dmg);
+          o.mhp = pair_swap(me.mhp);
+          o.nitems = pair_swap(me.nitems);
+        }
         Player p1 = pick(isB, o, me), p2 = pick(isB, me, o);
-        took_ordered = rare_tick<NCAP, false>(c, st, B, i, key, game, ep, p1, p2, npc, items, hp,
+        took_ordered = rare_tick<NCAP, GRID>(c, st, B, i, key, game, ep, p1, p2, npc, items, hp,
                                           tick, status, dl, sep, restarted, tb, need,
                                           isB ? otx : tx, isB ? oty : ty, isB ? tx : otx,
                                           isB ? ty : oty, false);
@@ -3463,6 +3535,10 @@ __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kern
     dl.eps += (!rare & end) ? 1 : 0;
     status = rare ? status : (end ? ORX_TIE : ORX_IN_PROGRESS);
     tick = rare ? tick : ft;
+    if constexpr (PM == 3) {  // the end of the tick: mana regeneration, as rollout_tick
+      const bool base = in_progress & !took_ordered;
+      me.mana = base ? min(me.mana + c.mana_regen, c.mana_max) : me.mana;
+    }
     if constexpr (SEP) {  // as rollout_tick (readme.md:46-47)
       const bool base = in_progress & !took_ordered;
       const int32_t od2 = pair_swap(me.d);
@@ -3496,6 +3572,25 @@ __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kern
   if (restarted || dl.descend != 0) {
     st.st_x[who * B + i] = me.sx;
     st.st_y[who * B + i] = me.sy;
+    if constexpr (GRID) st.p_layout[who * B + i] = (int16_t)me.lay;
+  }
+  if constexpr (PM == 3) {
+    int32_t* r = st.p_rpg + who * B + i;
+    const size_t f = 2 * (size_t)B;
+    r[ORX_RPG_MANA * f] = me.mana;
+    r[ORX_RPG_XP * f] = me.xp;
+    r[ORX_RPG_DAMAGE * f] = me.dmg;
+    r[ORX_RPG_MAX_HEALTH * f] = me.mhp;
+    r[ORX_RPG_ITEMS * f] = me.nitems;
+    r[ORX_RPG_COOLDOWN * f] = 0;
+    if constexpr (NCAP > 0) {
+      if (!isB) {  // the game's items (identical in both lanes)
+        st.item_mask[i] = items.on;
+        st.item_mask[B + i] = items.kind;
+        for (int k = 0; k < c.K; ++k)
+          if ((items.on >> k) & 1u) st.item_pos[(size_t)k * B + i] = (uint16_t)npc.get(k);
+      }
+    }
   }
   if (!isB) {
     st.tick[i] = tick;
@@ -4063,7 +4158,10 @@ struct RolloutPlan {
 };
 
 // The paired form: no dense NPCs (K <= 16), no bank, the RandomBot or StaircaseBot trajectory
-// forms (PM 1 / 2), for batches the one-lane rule leaves below 64 games per
+// forms (PM 1 / 2) and the RandomBot form with the character mechanics (PM 3,
+// round 4: each lane its own player's mana, experience, damage, max health
+// and items held; the game's items beside its NPCs in both lanes; every rare
+// tick through rare_tick), for batches the one-lane rule leaves below 64 games per
 // wave; its games per wave: two waves per SIMD -- counting the `concurrency`
 // launches that share the device (StreamShardedEngine's shards) -- until the
 // wave holds 32 games, at least 8 (C5's 8-GPU share, 16,384 games: 8 per
@@ -4075,7 +4173,10 @@ RolloutPlan plan_rollout(const orx_cfg_t* cfg, int pm, uint32_t B, uint32_t conc
   RolloutPlan p;
   p.lanes = rollout_lanes(B);
   // (its packed cells x | y << 8 need x, y < 256)
-  p.paired = ncap_for(cfg->n_npcs) != kDense && cfg->n_layouts == 0 && (pm == 1 || pm == 2) &&
+  // a dungeon bank: PM 1 / 3, and PM 2 without separation damage
+  const bool bank_ok = cfg->n_layouts == 0 ||
+                       !(pm == 2 && (cfg->flags & ORX_EXT_SEPARATION_DAMAGE) != 0);
+  p.paired = ncap_for(cfg->n_npcs) != kDense && bank_ok && pm >= 1 && pm <= 3 &&
              cfg->width <= 256 && cfg->height <= 256 && p.lanes <= 32u && paired_enabled();
   if (p.paired) {
     if (const int o = lanes_override()) {
@@ -4395,20 +4496,40 @@ int orx_rollout_ex(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p
   if (plan.paired) {
     const dim3 blocks((B + per_block - 1) / per_block);
     const bool sepd = pm == 2 && (cfg->flags & ORX_EXT_SEPARATION_DAMAGE) != 0;
-#define ORX_PAIR(N, P, A, S, C)                                                                 \
-    if (nc == N && pm == P && (A == kStreamAux) == nt && S == sepd && C == cf) {                \
-      const uint32_t plds = (A == kPartialAux && !C) ? threads / 64u * kStageWaveBytes : 0u;     \
-      hipLaunchKernelGGL((pair_rollout_kernel<N, P, A, S, C>), blocks, dim3(threads), plds, s,  \
-                         *cfg, *st, n_ticks, obs, act, B, k, off, lanes, stage_enabled()); \
+    // dynamic LDS: a bank's tiles when they fit (lds_n), then the staged
+    // writer's 8 KiB per wave (partial-line int32 forms); above the default
+    // 64 KiB the limit is raised, or the tiles stay in global memory
+    const uint32_t stage_bytes = threads / 64u * kStageWaveBytes;
+#define ORX_PAIR(N, P, A, S, C, G)                                                              \
+    if (nc == N && pm == P && (A == kStreamAux) == nt && S == sepd && C == cf && G == grid) {   \
+      auto* kfn = &pair_rollout_kernel<N, P, A, S, C, G>;                                       \
+      uint32_t pn = lds_n;                                                                      \
+      const uint32_t st_b = (A == kPartialAux && !C) ? stage_bytes : 0u;                         \
+      uint32_t plds = ((pn + 15u) & ~15u) + st_b;                                               \
+      if (plds > 65536u &&                                                                      \
+          hipFuncSetAttribute(reinterpret_cast<const void*>(kfn),                               \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)plds) != hipSuccess) { \
+        (void)hipGetLastError();                                                                \
+        pn = 0u;                                                                                \
+        plds = st_b;                                                                            \
+      }                                                                                         \
+      hipLaunchKernelGGL(kfn, blocks, dim3(threads), plds, s, *cfg, *st, n_ticks, obs, act, B,  \
+                         k, off, lanes, stage_enabled(), pn);                                   \
       return launch_status("orx_rollout");                                                      \
     }
 #define ORX_PAIRS_C(N, C)                                                                       \
-    ORX_PAIR(N, 1, kStreamAux, false, C) ORX_PAIR(N, 1, kPartialAux, false, C)                  \
-    ORX_PAIR(N, 2, kStreamAux, false, C) ORX_PAIR(N, 2, kPartialAux, false, C)                  \
-    ORX_PAIR(N, 2, kStreamAux, true, C) ORX_PAIR(N, 2, kPartialAux, true, C)
-#define ORX_PAIRS(N) ORX_PAIRS_C(N, false) ORX_PAIRS_C(N, true)
+    ORX_PAIR(N, 1, kStreamAux, false, C, false) ORX_PAIR(N, 1, kPartialAux, false, C, false)    \
+    ORX_PAIR(N, 2, kStreamAux, false, C, false) ORX_PAIR(N, 2, kPartialAux, false, C, false)    \
+    ORX_PAIR(N, 2, kStreamAux, true, C, false) ORX_PAIR(N, 2, kPartialAux, true, C, false)
+#define ORX_PAIRS_G(N, G)                                                                       \
+    ORX_PAIR(N, 3, kStreamAux, false, false, G) ORX_PAIR(N, 3, kPartialAux, false, false, G)
+#define ORX_PAIRS(N)                                                                            \
+    ORX_PAIRS_C(N, false) ORX_PAIRS_C(N, true) ORX_PAIRS_G(N, false) ORX_PAIRS_G(N, true)        \
+    ORX_PAIR(N, 1, kStreamAux, false, false, true) ORX_PAIR(N, 1, kPartialAux, false, false, true) \
+    ORX_PAIR(N, 2, kStreamAux, false, false, true) ORX_PAIR(N, 2, kPartialAux, false, false, true)
     ORX_PAIRS(0) ORX_PAIRS(8) ORX_PAIRS(16)
 #undef ORX_PAIRS_C
+#undef ORX_PAIRS_G
 #undef ORX_PAIRS
 #undef ORX_PAIR
     return fail(ORX_EIO, "orx_rollout: no paired kernel instance for this plan");

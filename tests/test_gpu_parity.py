@@ -709,14 +709,35 @@ PAIRED_CASES = {
 }
 
 
+# round 4: the paired form with the character mechanics (PM 3: mana,
+# experience, items; parity unpinned vs the reference, engine vs oracle) and
+# with a dungeon bank (walls, several staircases per layout; PM 1 with NPCs,
+# PM 2 under both despawn rules, PM 3)
+PAIRED_CASES.update({
+    "rpg_npcs": (dict(width=10, height=9, n_npcs=8, npc_health=2, max_ticks=45,
+                      flags=4 | 16 | 32, xp_per_level=2, item_drop_pct=70), (1, 1), 1000, 72),
+    "rpg_heal_flag_k14": (dict(width=9, height=9, n_npcs=14, max_ticks=40, flags=4 | 8 | 16 | 32,
+                               mana_max=12, item_bonus=2), (1, 1), 1024, 73),
+    "bank_random_npcs": (dict(width=20, height=16, n_npcs=8, max_ticks=50), (1, 1), 1000, 74),
+    "bank_stairs_unused": (dict(width=12, height=10, max_ticks=60, despawn=2, start_mode=2,
+                                p1_depth=2, p2_depth=0), (2, 2), 1000, 75),
+    "bank_stairs_npcs": (dict(width=14, height=12, n_npcs=5, max_ticks=60), (2, 2), 1001, 76),
+    "bank_rpg": (dict(width=16, height=12, n_npcs=8, npc_health=2, max_ticks=50,
+                      flags=4 | 16 | 32, item_drop_pct=60), (1, 1), 1000, 77),
+})
+PAIRED_BANKS = {"bank_random_npcs": (20, 16, 6, 81, (1, 2)), "bank_stairs_unused": (12, 10, 5, 82, (1, 2)),
+                "bank_stairs_npcs": (14, 12, 4, 83, (2,)), "bank_rpg": (16, 12, 5, 84, (1, 3))}
+
+
 @pytest.mark.parametrize("name", sorted(PAIRED_CASES))
 def test_paired_rollout_vs_oracle(name, oracle_lib):
     import torch
     from optimax_rogue_amd.enums import OBS_FIELDS
     cfg, pol, B, seed = PAIRED_CASES[name]
-    ora = oracle_lib.Oracle(cfg, B, seed, 5)
+    lay = _bank(*PAIRED_BANKS[name]) if name in PAIRED_BANKS else None
+    ora = oracle_lib.Oracle(cfg, B, seed, 5, layouts=lay)
     ora.reset(episode=np.zeros(B, np.int32))
-    eng = _engine(cfg, B, seed, 5)
+    eng = _engine(cfg, B, seed, 5, layouts=lay)
     assert eng.rollout_shape(*pol)["lanes_per_game"] == 2, name
     T = 40
     obs = torch.zeros((T, len(OBS_FIELDS), B), dtype=torch.int32, device=eng.device)
