@@ -263,15 +263,31 @@ def extras(torch, cfg, dev, B_cfg, K, large_rollout=False):
         env.step(pool[k % 16])
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
-    ks = timed_launches(torch, lambda: env.step(pool[0]), 30)
+    # the same 50 calls captured in one HIP graph (no host sync inside
+    # VecEnv.step makes it capturable): the device's time per tick
+    gv = torch.cuda.CUDAGraph()
+    sv = torch.cuda.Stream(device=dev)
+    sv.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(sv):
+        with torch.cuda.graph(gv, stream=sv):
+            for k in range(50):
+                env.step(pool[k % 16])
+    torch.cuda.current_stream().wait_stream(sv)
+    gv.replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(10):
+        gv.replay()
+    torch.cuda.synchronize()
+    gel = (time.perf_counter() - t0) / 500
     out["vecenv_step"] = {"value": B_cfg * n_ve / el, "unit": "env-steps/s",
                           "us_per_tick": el / n_ve * 1e6,
-                          "device_us_per_tick": sorted(ks)[len(ks) // 2] * 1e6,
-                          "note": "VecEnv.step eager from Python (int64 learner actions + "
-                                  "RandomBot opponent -> obs, reward, done, status): one "
+                          "graph_us_per_tick": gel * 1e6,
+                          "note": "VecEnv.step called eagerly from Python (int64 learner actions "
+                                  "+ RandomBot opponent -> obs, reward, done, status): one "
                                   "orx_env_step launch per tick, no host sync; "
-                                  "device_us_per_tick = HIP events around one call"}
-    del env, pool
+                                  "graph_us_per_tick: 50 calls captured in one HIP graph"}
+    del env, pool, gv
     torch.cuda.empty_cache()
     # (2) large batch: the chip full (2^21 games)
     BL = 1 << 21

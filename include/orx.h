@@ -425,7 +425,8 @@ int orx_policy(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p1,
  * observation row obs[b * ORX_OBS_FIELDS + f] (the orx_rollout fields), the
  * status, reward[b] (player 1's view: +1 Player1Win, -1 Player2Win, 0
  * otherwise, on the tick the episode ends) and done[b] (1 on that tick; an
- * engine stop code >= 16 ends it as a truncation).  No host sync.  Philox
+ * engine stop code >= 16 ends it as a truncation); status may be NULL (it is
+ * also the observation row's field ORX_OBS_STATUS).  No host sync.  Philox
  * mode only (stock-seed mode: orx_policy + orx_step).  Replaces the bot
  * loop's per-tick exchange, optimax_rogue_bots/main.py:118-155, and
  * server/main.py:110-113 for a learner. */

@@ -2105,7 +2105,7 @@ __global__ void __launch_bounds__(256) env_step_kernel(
   done[i] = ended ? 1 : 0;
   reward[i] = !ended ? 0.0f : after == ORX_PLAYER1_WIN ? 1.0f : after == ORX_PLAYER2_WIN ? -1.0f
                                                                                          : 0.0f;
-  status_out[i] = after;
+  if (status_out) status_out[i] = after;
 }
 
 // One player descends -- the common case of handle_descend (updater.py:259-296)
@@ -2958,8 +2958,7 @@ struct PairWriter {
   // me: this lane's player; kp / ks: its cell and staircase as x | y << 8
   // (compact only); tick and status: the game's (identical in both lanes)
   __device__ __forceinline__ void write(const Player& me, uint32_t kp, uint32_t ks, bool isB,
-                                        int32_t tick, int32_t status, int32_t move,
-                                        int32_t = 0, int32_t = 0) {
+                                        int32_t tick, int32_t status, int32_t move) {
     const auto ro = __builtin_amdgcn_make_buffer_rsrc(obs, 0, (int32_t)(kRows * B * 4u),
                                                       kBufferDword3);
     if constexpr (CF) {
@@ -2988,104 +2987,6 @@ struct PairWriter {
   }
 };
 
-// The partial-line paired forms (fewer than 32 games per wave, default store
-// policy): a wave's row segments are G * 4 bytes, and the CU's vector-memory
-// path pays per store INSTRUCTION, not per byte -- C5's 8-game waves spent
-// most of a common tick on their 7 dword + 1 byte stores.  Here each lane
-// puts its 7 values and its move into LDS (8 ds_write_b32 at immediate
-// offsets from one running address), and every 8 ticks the wave writes them
-// out as 16-byte chunks: one pass per observation row (lane l: tick l / (G/4),
-// games 4 (l % (G/4)) .. +3; 2G lanes cover 8 ticks exactly) plus one pass of
-// action bytes -- 15 vector stores per 8 ticks instead of 64.  LDS per wave:
-// 8 ticks x [2 players][8 slots][16 games] dwords = 8 KiB (dynamic LDS).  A
-// wave whose G is not a multiple of 4 (or above 16), whose games run past
-// the batch's end, or a batch not a multiple of 4 games (16-byte chunks
-// must not straddle a row) stores directly, as PairWriter.
-constexpr uint32_t kStageTicks = 8;
-constexpr uint32_t kStageTickBytes = 1024;
-constexpr uint32_t kStageWaveBytes = kStageTicks * kStageTickBytes;
-struct PairStageWriter {
-  PairWriter<kPartialAux, false> direct;
-  int32_t* obs;   // row 0 of the next flush's first tick
-  int8_t* act;
-  uint32_t B, i0, G;
-  bool staged;    // uniform per wave
-  uint32_t lb;    // this lane's LDS base: wave + who * 512 + j * 4
-  uint32_t lp;    // ... plus the current tick slot
-  uint32_t fl;    // flush lanes: wave + tick * 1024 + q * 16
-  uint32_t fo;    // ... their global byte offset: (tick * 14 * B + i0 + 4 q) * 4
-  uint32_t ao;    // action flush: (tick * B + i0 + 4 q) * 2
-  uint32_t fk;    // the flush lane's tick
-  __device__ __forceinline__ PairStageWriter(int32_t* o, int8_t* a, uint32_t B_, uint32_t i,
-                                             uint32_t who, uint32_t lanes, bool enable,
-                                             uint32_t base)
-      : direct(o, a, B_, i, who), obs(o), act(a), B(B_), G(lanes) {
-    // (base: the LDS bytes before the stage region -- a dungeon bank's tiles)
-    const uint32_t wave = base + (threadIdx.x >> 6) * kStageWaveBytes;
-    const uint32_t j = (threadIdx.x & 63u) >> 1;   // game within the wave
-    i0 = (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(i - j));   // (uniform)
-    staged = enable && (G & 3u) == 0u && G <= 16u && (B & 3u) == 0u && i0 + G <= B;
-    lb = wave + who * 512u + j * 4u;
-    lp = lb;
-    const uint32_t l = threadIdx.x & 63u, qn = G >> 2;
-    const uint32_t q = qn ? l % qn : 0u;
-    fk = qn ? l / qn : 0u;
-    fl = wave + fk * kStageTickBytes + q * 16u;
-    fo = (fk * (uint32_t)ORX_OBS_FIELDS * B + i0 + 4u * q) * 4u;
-    ao = (fk * B + i0 + 4u * q) * 2u;
-    asm volatile("" : "+v"(lb), "+v"(lp), "+v"(fl), "+v"(fo), "+v"(ao));
-  }
-  __device__ __forceinline__ void flush(uint32_t nk) {
-    // the rows: global row r holds slot (who_r, k_r)
-    constexpr uint32_t src[ORX_OBS_FIELDS] = {0, 1, 2, 3, 8, 9, 10, 11, 4, 12, 5, 6, 13, 14};
-    const auto ro = __builtin_amdgcn_make_buffer_rsrc(obs, 0, (int32_t)(ORX_OBS_FIELDS * B * 4u *
-                                                                         kStageTicks),
-                                                      kBufferDword3);
-    const bool live = fk < nk;
-    if (live) {
-#pragma unroll
-      for (uint32_t r = 0; r < (uint32_t)ORX_OBS_FIELDS; ++r) {
-        const uint32_t sw = src[r] < 8u ? src[r] * 64u : 512u + (src[r] - 8u) * 64u;
-        const auto v = *reinterpret_cast<const __attribute__((ext_vector_type(4))) uint32_t*>(
-            orx_lds_tiles + fl + sw);
-        __builtin_amdgcn_raw_buffer_store_b128(v, ro, (int32_t)fo, (int32_t)(r * B * 4u),
-                                               kPartialAux);
-      }
-      // the moves (slot 7 of each player's block) as bytes p1, p2 per game
-      using U4 = __attribute__((ext_vector_type(4))) uint32_t;
-      const U4 m1 = *reinterpret_cast<const U4*>(orx_lds_tiles + fl + 7u * 64u);
-      const U4 m2 = *reinterpret_cast<const U4*>(orx_lds_tiles + fl + 512u + 7u * 64u);
-      const uint32_t w0 = (m1.x & 0xFFu) | ((m2.x & 0xFFu) << 8) | ((m1.y & 0xFFu) << 16) |
-                          (m2.y << 24);
-      const uint32_t w1 = (m1.z & 0xFFu) | ((m2.z & 0xFFu) << 8) | ((m1.w & 0xFFu) << 16) |
-                          (m2.w << 24);
-      const auto ra = __builtin_amdgcn_make_buffer_rsrc(act, 0, (int32_t)(B * 2u * kStageTicks),
-                                                        kBufferDword3);
-      using U2 = __attribute__((ext_vector_type(2))) uint32_t;
-      __builtin_amdgcn_raw_buffer_store_b64(U2{w0, w1}, ra, (int32_t)ao, 0, kPartialAux);
-    }
-    obs += (size_t)ORX_OBS_FIELDS * B * kStageTicks;
-    act += (size_t)2 * B * kStageTicks;
-    lp = lb;
-  }
-  __device__ __forceinline__ void write(const Player& me, uint32_t kp, uint32_t ks, bool isB,
-                                        int32_t tick, int32_t status, int32_t move, int32_t t,
-                                        int32_t n_ticks) {
-    if (!staged) {
-      direct.write(me, kp, ks, isB, tick, status, move);
-      return;
-    }
-    const int32_t vals[8] = {me.x, me.y, me.d, me.hp, isB ? status : tick, me.sx, me.sy, move};
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-      *reinterpret_cast<int32_t*>(orx_lds_tiles + lp + (uint32_t)k * 64u) = vals[k];
-    lp += kStageTickBytes;
-    const int32_t done = __builtin_amdgcn_readfirstlane(t) + 1;   // (uniform)
-    if ((done & (int32_t)(kStageTicks - 1)) == 0 || done == n_ticks)
-      flush((uint32_t)(done - ((done - 1) & ~(int32_t)(kStageTicks - 1))));
-  }
-};
-
 // PM 1: both players RandomBot (no extension flags); PM 2: both StaircaseBot
 // (at most separation damage).  NCAP 0 / 8 / 16 (register NPCs, no dense
 // grid), empty dungeons, obs and act given.  The bench's C3 shards run
@@ -3106,7 +3007,6 @@ __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kern
                                                                      int8_t* __restrict__ act,
                                                                      uint32_t B, Key key,
                                                                      uint32_t off, uint32_t lanes,
-                                                                     uint32_t stage,
                                                                      uint32_t lds_n) {
   bool lds_tiles = false;
   if constexpr (GRID) {  // stage the bank's tiles in LDS (the whole block, before any exit)
@@ -3183,13 +3083,7 @@ __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kern
   Deltas dl = {0, 0, 0, 0, 0, 0};
   bool restarted = false;
   constexpr int need = (PM == 1 || PM == 3) ? 2 : 0;
-  // partial-line int32 rows: staged through LDS (PairStageWriter)
-  constexpr bool kStage = AUX == kPartialAux && !CF;
-  std::conditional_t<kStage, PairStageWriter, PairWriter<AUX, CF>> traj = [&] {
-    if constexpr (kStage)
-      return PairStageWriter(obs, act, B, i, who, lanes, stage != 0u, (lds_n + 15u) & ~15u);
-    else return PairWriter<AUX, CF>(obs, act, B, i, who);
-  }();
+  PairWriter<AUX, CF> traj(obs, act, B, i, who);
 #ifdef ORX_STAMPS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
@@ -3201,7 +3095,7 @@ __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kern
 #endif
     if constexpr ((ORX_DIAG & 32) != 0) {  // diagnostic: the trajectory stores alone
       tick += 1;
-      traj.write(me, kp, ks, isB, tick, status, ORX_MOVE_STAY, t, n_ticks);
+      traj.write(me, kp, ks, isB, tick, status, ORX_MOVE_STAY);
       continue;
     }
     // the bot's move (randombot.py:20-21 / staircasebot.py:9-21)
@@ -3562,7 +3456,7 @@ __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kern
         }
       }
     }
-    if (!(ORX_DIAG & 16)) traj.write(me, kp, ks, isB, tick, status, move, t, n_ticks);
+    if (!(ORX_DIAG & 16)) traj.write(me, kp, ks, isB, tick, status, move);
     } while (++t < n_ticks);
   ORX_STAMP(3);
   st.p_x[who * B + i] = me.x;
@@ -4100,11 +3994,6 @@ uint32_t device_lds_per_block() {
   return (uint32_t)n;
 }
 
-uint32_t stage_enabled() {  // read per launch (ORX_PAIR_STAGE=0: direct partial-line stores)
-  const char* e = getenv("ORX_PAIR_STAGE");
-  return (e && e[0] == '0') ? 0u : 1u;
-}
-
 bool paired_enabled() {  // read per launch (ORX_ROLLOUT_PAIRED=0: the one-lane form)
   const char* e = getenv("ORX_ROLLOUT_PAIRED");
   return !(e && e[0] == '0');
@@ -4389,8 +4278,8 @@ int orx_env_step(const orx_cfg_t* cfg, const orx_state_t* st, const void* action
                             "games' own streams; use orx_policy + orx_step");
   if (n_games == 0) return ORX_OK;
   if ((r = check_state(cfg, st, true))) return r;
-  if (!actions || !act || !obs || !reward || !done || !status)
-    return fail(ORX_EINVAL, "a pointer is NULL");
+  if (!actions || !act || !obs || !reward || !done)
+    return fail(ORX_EINVAL, "a pointer is NULL (only status may be)");
   const uint32_t B = (uint32_t)n_games, off = (uint32_t)game_offset;
   const hipStream_t s = (hipStream_t)stream;
   const Key k = make_key(seed);
@@ -4496,25 +4385,20 @@ int orx_rollout_ex(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p
   if (plan.paired) {
     const dim3 blocks((B + per_block - 1) / per_block);
     const bool sepd = pm == 2 && (cfg->flags & ORX_EXT_SEPARATION_DAMAGE) != 0;
-    // dynamic LDS: a bank's tiles when they fit (lds_n), then the staged
-    // writer's 8 KiB per wave (partial-line int32 forms); above the default
+    // dynamic LDS: a bank's tiles when they fit (lds_n); above the default
     // 64 KiB the limit is raised, or the tiles stay in global memory
-    const uint32_t stage_bytes = threads / 64u * kStageWaveBytes;
 #define ORX_PAIR(N, P, A, S, C, G)                                                              \
     if (nc == N && pm == P && (A == kStreamAux) == nt && S == sepd && C == cf && G == grid) {   \
       auto* kfn = &pair_rollout_kernel<N, P, A, S, C, G>;                                       \
       uint32_t pn = lds_n;                                                                      \
-      const uint32_t st_b = (A == kPartialAux && !C) ? stage_bytes : 0u;                         \
-      uint32_t plds = ((pn + 15u) & ~15u) + st_b;                                               \
-      if (plds > 65536u &&                                                                      \
+      if (pn > 65536u &&                                                                        \
           hipFuncSetAttribute(reinterpret_cast<const void*>(kfn),                               \
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)plds) != hipSuccess) { \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)pn) != hipSuccess) { \
         (void)hipGetLastError();                                                                \
         pn = 0u;                                                                                \
-        plds = st_b;                                                                            \
       }                                                                                         \
-      hipLaunchKernelGGL(kfn, blocks, dim3(threads), plds, s, *cfg, *st, n_ticks, obs, act, B,  \
-                         k, off, lanes, stage_enabled(), pn);                                   \
+      hipLaunchKernelGGL(kfn, blocks, dim3(threads), pn, s, *cfg, *st, n_ticks, obs, act, B,    \
+                         k, off, lanes, pn);                                                    \
       return launch_status("orx_rollout");                                                      \
     }
 #define ORX_PAIRS_C(N, C)                                                                       \

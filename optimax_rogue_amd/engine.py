@@ -287,9 +287,18 @@ class BatchedEngine:
             if t.dtype != dt or tuple(t.shape) != shape or not t.is_contiguous() \
                     or t.device != self.device:
                 raise ValueError(f"env_step output must be a contiguous {dt} {shape} tensor")
-        self._call("orx_env_step", _ptr(actions), nb, actions.dim(), int(p2), _ptr(self.actions),
-                   _ptr(obs), _ptr(reward), _ptr(done), _ptr(status), self.B, self.seed,
-                   self.game_offset, self._stream())
+        self._env_step_raw(actions, nb, int(p2), obs, reward, done, status)
+
+    def _env_step_raw(self, actions, nb, p2, obs, reward, done, status=None) -> None:
+        """orx_env_step on tensors already checked (VecEnv.step's own buffers):
+        one ctypes call; status may be None (it is obs[:, 9])."""
+        code = self.lib.orx_env_step(
+            self._pcfg, self._pst, actions.data_ptr(), nb, actions.dim(), p2,
+            self.actions.data_ptr(), obs.data_ptr(), reward.data_ptr(), done.data_ptr(),
+            None if status is None else status.data_ptr(), self.B, self.seed, self.game_offset,
+            torch.cuda.current_stream(self.device).cuda_stream)
+        if code:
+            _lib.check("orx_env_step", code)
 
     def policy(self, p1: int = Policy.Random, p2: int = Policy.Random,
                out: Optional[torch.Tensor] = None) -> torch.Tensor:

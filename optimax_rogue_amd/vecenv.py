@@ -45,6 +45,14 @@ class VecEnv:
         # every step synchronizes); False (default): the engine stops that game
         # with STATUS_BAD_ACTION, which step() reports as done (a truncation)
         self.check_actions = bool(check_actions)
+        self._init_step_consts()
+
+    def _init_step_consts(self) -> None:
+        """Per-call constants of step() (its Python cost is the eager path's)."""
+        self._shape1 = torch.Size([self.B])
+        self._shape2 = torch.Size([self.B, 2])
+        self._obs_shape = (self.B, len(OBS_FIELDS))
+        self._p2 = int(Policy.NONE if self.opponent is None else self.opponent)
 
     # -- observation -----------------------------------------------------------
     def observe(self) -> torch.Tensor:
@@ -96,14 +104,15 @@ class VecEnv:
         with ``check_actions=True`` it raises ValueError instead (a host check:
         that step synchronizes).  One launch (orx_env_step) and no host sync
         otherwise.  Returns (observation, reward, done, status), all fresh
-        tensors."""
+        tensors (status is the observation's status column, a view)."""
         e = self.engine
-        if tuple(actions.shape) not in ((self.B,), (self.B, 2)):   # no silent broadcasting
-            raise ValueError(f"actions must be [n_games] or [n_games, 2], got "
-                             f"{tuple(actions.shape)}")
-        if actions.dtype not in BatchedEngine._ACTION_BYTES:
+        shape = actions.shape
+        if shape != self._shape1 and shape != self._shape2:   # no silent broadcasting
+            raise ValueError(f"actions must be [n_games] or [n_games, 2], got {tuple(shape)}")
+        nb = BatchedEngine._ACTION_BYTES.get(actions.dtype)
+        if nb is None:
             raise ValueError(f"actions must be an integer tensor, got {actions.dtype}")
-        if actions.dim() == 1 and self.opponent is None:
+        if self.opponent is None and len(shape) == 1:
             raise ValueError("self-play (opponent=None) takes [n_games, 2] actions")
         a = actions if actions.device == self.device else actions.to(self.device)
         if not a.is_contiguous():
@@ -115,14 +124,11 @@ class VecEnv:
                                  "0-based: add 1)")
         if e.mt_py is not None:
             return self._step_stock(a)
-        B = self.B
-        obs = torch.empty((B, len(OBS_FIELDS)), dtype=torch.int32, device=self.device)
-        reward = torch.empty(B, dtype=torch.float32, device=self.device)
-        done = torch.empty(B, dtype=torch.bool, device=self.device)
-        status = torch.empty(B, dtype=torch.int32, device=self.device)
-        e.env_step(a, Policy.NONE if self.opponent is None else self.opponent, obs, reward, done,
-                   status)
-        return obs, reward, done, status
+        obs = torch.empty(self._obs_shape, dtype=torch.int32, device=self.device)
+        reward = torch.empty(self.B, dtype=torch.float32, device=self.device)
+        done = torch.empty(self.B, dtype=torch.bool, device=self.device)
+        e._env_step_raw(a, nb, self._p2, obs, reward, done)
+        return obs, reward, done, obs[:, _STATUS]
 
     def _step_stock(self, a: torch.Tensor):
         """Stock-seed mode (the bots draw from each game's own MT19937 stream):

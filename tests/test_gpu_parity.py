@@ -815,12 +815,13 @@ def test_dense_npc_character_trajectory_vs_oracle(oracle_lib):
 # launches, with identical actions and state.
 COMPACT_FORMS = {
     "c3_bench_shards": (dict(width=64, height=64, n_npcs=8), (1, 1), 65536, 2, 2),
-    "c2_pair": (dict(width=32, height=32), (1, 1), 4096, 1, 2),
+    "c2_pair": (dict(width=32, height=32, max_ticks=90), (1, 1), 4096, 1, 2),
     "c5_pair_sep": (dict(width=128, height=128, flags=1, sep_period=8), (2, 2), 16384, 1, 2),
     "c5_one_lane": (dict(width=128, height=128), (2, 2), 131072, 1, 1),
     "c3_one_lane": (dict(width=64, height=64, n_npcs=8, max_ticks=90), (1, 1), 65536, 1, 1),
-    "rpg_generic": (dict(width=16, height=16, n_npcs=8, flags=4 | 16 | 32, max_ticks=80), (1, 1),
-                    4096, 1, 1),
+    # int32 rows: the paired character form; compact rows: the generic form
+    "rpg_pair_vs_generic": (dict(width=16, height=16, n_npcs=8, flags=4 | 16 | 32, max_ticks=80),
+                            (1, 1), 4096, 1, 2),
     "bank_generic": (dict(width=20, height=16, n_npcs=4, max_ticks=70), (2, 1), 3001, 1, 1),
     "dense_generic": (dict(width=12, height=12, n_npcs=30, max_ticks=60), (1, 2), 2048, 1, 1),
     "stock_mt": (dict(width=10, height=9, n_npcs=4, max_ticks=60, rng=1), (1, 2), 1024, 1, 1),
@@ -864,40 +865,3 @@ def test_compact_rows_equal_int32_rows(name):
     for k in s0:
         assert np.array_equal(s0[k], s1[k]), (name, k)
     assert s0["ep_count"].sum() > 0 or name.startswith("c3_bench") or name.startswith("c5")
-
-
-@pytest.mark.parametrize("pol,cfgd", [((1, 1), dict(width=32, height=32, max_ticks=60)),
-                                      ((2, 2), dict(width=24, height=20, max_ticks=70, flags=1,
-                                                    sep_period=3)),
-                                      ((1, 1), dict(width=12, height=12, n_npcs=6,
-                                                    max_ticks=50))])
-def test_pair_staged_rows_equal_direct_rows(pol, cfgd, monkeypatch):
-    """The partial-line paired forms stage their rows in LDS and write them
-    every 8 ticks (PairStageWriter): identical rows, actions and state to the
-    direct stores (ORX_PAIR_STAGE=0), at 4, 8 and 16 games per wave, for a
-    batch that is a multiple of 4 games (staged) and one that is not (direct
-    fallback), over launches of 37 ticks (a partial last flush) handed over
-    from launch to launch."""
-    import torch
-    from optimax_rogue_amd.enums import OBS_FIELDS
-    T = 37
-    for lanes in ("4", "8", "16"):
-        monkeypatch.setenv("ORX_ROLLOUT_LANES", lanes)
-        for B in (4096, 4093):
-            res = []
-            for stage in ("1", "0"):
-                monkeypatch.setenv("ORX_PAIR_STAGE", stage)
-                e = _engine(cfgd, B, 41, 9)
-                sh = e.rollout_shape(*pol)
-                assert sh["lanes_per_game"] == 2 and sh["games_per_wave"] == int(lanes)
-                obs = torch.zeros((3 * T, len(OBS_FIELDS), B), dtype=torch.int32, device=e.device)
-                act = torch.zeros((3 * T, B, 2), dtype=torch.int8, device=e.device)
-                for k in range(3):
-                    e.rollout(T, *pol, obs=obs[k * T:(k + 1) * T], act=act[k * T:(k + 1) * T])
-                res.append((obs.cpu().numpy(), act.cpu().numpy(), e.snapshot()))
-            (o1, a1, s1), (o0, a0, s0) = res
-            assert np.array_equal(o1, o0), (lanes, B)
-            assert np.array_equal(a1, a0), (lanes, B)
-            for k in STATE_KEYS:
-                assert np.array_equal(s1[k], s0[k]), (lanes, B, k)
-    monkeypatch.delenv("ORX_PAIR_STAGE")

@@ -29,6 +29,7 @@ def test_vecenv_step_rejects_non_moves(bad):
     env = VecEnv.__new__(VecEnv)
     env.engine = _bare_engine(EnvConfig(), 3)
     env.B, env.device, env.opponent, env.check_actions = 3, torch.device("cpu"), 1, True
+    env._init_step_consts()
     with pytest.raises(ValueError, match="Move values"):
         env.step(torch.tensor(bad, dtype=torch.int32))
     with pytest.raises(ValueError, match="Move values"):
@@ -126,16 +127,18 @@ def test_vecenv_step_passes_bad_actions_to_the_engine(bad):
     class Eng:
         cfg, mt_py = EnvConfig(), None
 
-        def env_step(self, a, p2, obs, reward, done, status):
-            calls.append((a.clone(), p2, obs.shape, reward.dtype, done.dtype, status.dtype))
+        def _env_step_raw(self, a, nb, p2, obs, reward, done, status=None):
+            calls.append((a.clone(), nb, p2, obs.shape, obs.dtype, reward.dtype, done.dtype))
 
     env = VecEnv.__new__(VecEnv)
     env.engine, env.check_actions = Eng(), False
     env.B, env.device, env.opponent = 3, torch.device("cpu"), 2
-    env.step(torch.tensor(bad, dtype=torch.int64))
-    a, p2, shape, rd, dd, sd = calls[0]
-    assert a.dtype == torch.int64 and a.tolist() == bad and p2 == 2
-    assert shape == (3, 14) and rd == torch.float32 and dd == torch.bool and sd == torch.int32
+    env._init_step_consts()
+    obs, reward, done, status = env.step(torch.tensor(bad, dtype=torch.int64))
+    a, nb, p2, shape, od, rd, dd = calls[0]
+    assert a.dtype == torch.int64 and a.tolist() == bad and nb == 8 and p2 == 2
+    assert shape == (3, 14) and od == torch.int32 and rd == torch.float32 and dd == torch.bool
+    assert status.data_ptr() == obs[:, 9].data_ptr()   # the observation's status column
     with pytest.raises(ValueError, match="integer"):
         env.step(torch.tensor([1.0, 2.0, 3.0]))
 
