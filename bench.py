@@ -84,14 +84,15 @@ def bytes_per_game(kernel: str, K: int, ticks: int = 1) -> int:
 def rollout_kernel_name(K: int, shape: dict) -> str:
     """The kernel orx_rollout launches for this workload, as rocprofv3 names
     it: the RandomBot + trajectory specialization (PM=1), NPC capacity
-    0/8/16, in the form orx_rollout_shape reports -- pair_rollout_kernel (two
-    lanes per game, separation damage off) or rollout_kernel -- with its
-    store policy (AUX 2 = nontemporal, 0 = default)."""
+    0/8/16, in the form orx_rollout_shape reports -- pair_rollout_kernel<NCAP,
+    PM, AUX, SEP, CF, GRID> (two lanes per game; separation damage off, int32
+    rows, empty dungeons) or rollout_kernel<NCAP, PM, GRID, AUX, CF> -- with
+    its store policy (AUX 2 = nontemporal, 0 = default)."""
     ncap = 0 if K == 0 else 8 if K <= 8 else 16
     aux = 2 if shape["nontemporal"] else 0
     if shape["lanes_per_game"] == 2:
-        return f"pair_rollout_kernel<{ncap}, 1, {aux}, false>"
-    return f"rollout_kernel<{ncap}, 1, false, {aux}>"
+        return f"pair_rollout_kernel<{ncap}, 1, {aux}, false, false, false>"
+    return f"rollout_kernel<{ncap}, 1, false, {aux}, false>"
 
 
 def _cpu_model() -> str:
@@ -333,22 +334,32 @@ def extras(torch, cfg, dev, B_cfg, K, large_rollout=False):
         the games run as that many stream shards, as the headline step does
         (StreamShardedEngine; a step = one launch per shard, fork/join)."""
         if streams > 1:
+            # as the headline step: the shards' launches back to back on their
+            # streams between one fork and one join, HIP events around them all
             e = StreamShardedEngine(c, games, seed=5, device=dev, n_streams=streams)
             o, a = e.trajectory_buffers(T)
-            go1 = e.rollout_launcher(T, pol, pol, obs=o, act=a)
-
-            def go():
-                e.fork()
-                go1()
-                e.join()
+            go = e.rollout_launcher(T, pol, pol, obs=o, act=a)
+            e.fork()
+            go()
+            e.join()
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            ev0.record()
+            e.fork()
+            for _ in range(reps):
+                go()
+            e.join()
+            ev1.record()
+            torch.cuda.synchronize()
+            us = ev0.elapsed_time(ev1) * 1e-3 / reps
         else:
             e = BatchedEngine(c, games, seed=5, device=dev)
             o = torch.empty((T, len(OBS_FIELDS), games), dtype=torch.int32, device=dev)
             a = torch.empty((T, games, 2), dtype=torch.int8, device=dev)
             go = e.rollout_launcher(T, pol, pol, obs=o, act=a)
-        go()
-        d = timed_launches(torch, go, reps)
-        us = sorted(d)[len(d) // 2]
+            go()
+            d = timed_launches(torch, go, reps)
+            us = sorted(d)[len(d) // 2]
         shape = e.rollout_shape(pol, pol)
         del e, o, a, go
         return {"games": games, "ticks_per_launch": T, "games_per_wave": shape["games_per_wave"],
@@ -396,8 +407,8 @@ def extras(torch, cfg, dev, B_cfg, K, large_rollout=False):
     out["bank"] = dict(rollout_rate(EnvConfig(width=64, height=64, n_npcs=8, layouts=bank.layouts),
                                     65536, 1, streams=2),
                        policy="2x RandomBot", grid="64x64, 16 layouts (15% walls)",
-                       note="two stream shards as the headline step (the paired form, tiles "
-                            "staged in LDS: 64 KiB); us_per_launch = one step")
+                       note="two stream shards timed as the headline step (the paired form, "
+                            "tiles staged in LDS: 64 KiB); us_per_launch = one step")
     # configs[2] read literally, "64x64 grid with enemies+items enabled": C3 with
     # the readme's character mechanics on (build extensions, no reference
     # semantics, so not the bit-exact headline)
@@ -407,8 +418,8 @@ def extras(torch, cfg, dev, B_cfg, K, large_rollout=False):
                          policy="2x RandomBot", grid="64x64, 8 NPCs",
                          note="mana, heal, experience, item drops/pickup on (EXT_RPG; engine "
                               "vs oracle bit-exact, parity unpinned vs the reference); two "
-                              "stream shards as the headline step (the paired form); "
-                              "us_per_launch = one step")
+                              "stream shards timed as the headline step (one lane per game at "
+                              "32 games per wave); us_per_launch = one step")
     c5 = {}
     for flag in (0, EXT_SEPARATION_DAMAGE):
         c = EnvConfig.c5()

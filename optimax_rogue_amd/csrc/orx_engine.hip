@@ -4075,6 +4075,15 @@ RolloutPlan plan_rollout(const orx_cfg_t* cfg, int pm, uint32_t B, uint32_t conc
       uint32_t L = 32;
       while (L > 8 && (uint64_t)B * concurrency < 2 * simds * L) L >>= 1;
       p.lanes = L;
+      // the character mechanics' rare ticks all run rare_tick, over twice the
+      // active lanes when paired: the pair loses at 32 games per wave (the
+      // 65,536-game two-shard step 196 us paired, 117 one lane) and wins at
+      // 8 (16,384 games 91 against 94, 4,096 games 75 against 88;
+      // profiles/r04_v6/forms_ab.jsonl)
+      if (pm == 3 && L > 16u) {
+        p.paired = false;
+        p.lanes = rollout_lanes(B);
+      }
     }
   }
   p.nt = p.lanes * 4u >= 128u;  // a wave's row segment is a whole line

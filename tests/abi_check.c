@@ -26,6 +26,15 @@ int main(void) {
   if (orx_step(&c, NULL, NULL, 0, 1, 0, NULL) != ORX_OK) { printf("empty step failed\n"); return 5; }
   if (orx_rollout(&c, NULL, ORX_POLICY_RANDOM, ORX_POLICY_RANDOM, 5, NULL, NULL, 0, 1, 0, NULL) != ORX_OK) return 6;
   if (orx_step(&c, NULL, NULL, 16, 1, 0, NULL) != ORX_EINVAL) { printf("NULL state accepted\n"); return 7; }
+  /* ABI 5: the learner's tick and the row formats -- argument checks only */
+  if (orx_env_step(&c, NULL, NULL, 8, 1, ORX_POLICY_RANDOM, NULL, NULL, NULL, NULL, NULL, 0, 1, 0,
+                   NULL) != ORX_OK) { printf("empty env step failed\n"); return 9; }
+  if (orx_env_step(&c, NULL, NULL, 3, 1, ORX_POLICY_RANDOM, NULL, NULL, NULL, NULL, NULL, 16, 1, 0,
+                   NULL) != ORX_EINVAL) { printf("3-byte actions accepted\n"); return 10; }
+  if (orx_rollout_ex(&c, NULL, ORX_POLICY_RANDOM, ORX_POLICY_RANDOM, 5, NULL, NULL, ORX_OBS_COMPACT,
+                     0, 1, 0, 1, NULL) != ORX_OK) { printf("empty compact rollout failed\n"); return 11; }
+  if (orx_rollout_ex(&c, NULL, ORX_POLICY_RANDOM, ORX_POLICY_RANDOM, 5, NULL, NULL, 7, 16, 1, 0, 1,
+                     NULL) != ORX_EINVAL) { printf("unknown row format accepted\n"); return 12; }
   printf("sizeof(orx_cfg_t)=%zu sizeof(orx_state_t)=%zu off_flags=%zu off_npc_alive=%zu\n",
          sizeof(orx_cfg_t), sizeof(orx_state_t), offsetof(orx_cfg_t, flags),
          offsetof(orx_state_t, npc_alive));

@@ -188,9 +188,11 @@ def test_rollout_shape_rules(lib):
     from optimax_rogue_amd import EnvConfig
     from optimax_rogue_amd._lib import OrxRolloutShape
 
-    def shape(cfg, B, p1=1, p2=1, traj=1, conc=1):
+    def shape(cfg, B, p1=1, p2=1, traj=1, conc=1, n_layouts=0):
         out = OrxRolloutShape()
-        assert lib.orx_rollout_shape(ctypes.byref(cfg.to_c()), p1, p2, B, traj, conc,
+        c = cfg.to_c()
+        c.n_layouts = n_layouts
+        assert lib.orx_rollout_shape(ctypes.byref(c), p1, p2, B, traj, conc,
                                      ctypes.byref(out)) == 0
         return out.games_per_wave, out.lanes_per_game, out.nontemporal
 
@@ -204,6 +206,16 @@ def test_rollout_shape_rules(lib):
     assert shape(EnvConfig(n_npcs=40), 4096) == (16, 1, 0)        # LDS NPC table: one lane per game
     assert shape(EnvConfig.c5(), 16384, 2, 1) == (16, 1, 1)       # mixed bots: the generic form
     assert shape(EnvConfig.c2(), 4096, traj=0) == (16, 1, 1)      # no trajectory buffers
+    # round 4: the character mechanics pair at 8-16 games per wave only; a
+    # dungeon bank pairs (not with separation damage for StaircaseBots)
+    rpg = EnvConfig(width=64, height=64, n_npcs=8, flags=4 | 8 | 16 | 32)
+    assert shape(rpg, 32768, conc=2) == (32, 1, 1)                # one lane at 32 per wave
+    assert shape(rpg, 4096) == (8, 2, 0)
+    assert shape(EnvConfig.c3(), 32768, conc=2, n_layouts=16) == (32, 2, 1)
+    assert shape(EnvConfig(width=12, height=10), 4096, 2, 2, n_layouts=4) == (8, 2, 0)
+    assert shape(EnvConfig(width=12, height=10, flags=1, sep_period=2), 4096, 2, 2,
+                 n_layouts=4)[1] == 1
+    assert shape(EnvConfig(width=300, height=200), 4096, 2, 2)[1] == 1  # packed cells: <= 256
     bad = OrxRolloutShape()
     assert lib.orx_rollout_shape(ctypes.byref(EnvConfig.c2().to_c()), 9, 1, 64, 1, 1,
                                  ctypes.byref(bad)) == -22
