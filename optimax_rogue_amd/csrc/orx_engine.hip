@@ -630,9 +630,11 @@ __device__ __forceinline__ void calc_pos(int32_t x, int32_t y, int32_t m, int32_
 }
 
 // Dungeon.tiles[x, y] of bank layout `lay` (x, y inside the grid).
-__device__ __forceinline__ uint32_t bank_tile(const Cfg& c, int32_t lay, int32_t x, int32_t y) {
-  const uint32_t idx = (uint32_t)lay * (uint32_t)(c.W * c.H) + (uint32_t)(x * c.H + y);
+__device__ __forceinline__ uint32_t bank_tile_at(const Cfg& c, uint32_t idx) {
   return c.lds_tiles ? orx_lds_tiles[idx] : c.tiles[idx];
+}
+__device__ __forceinline__ uint32_t bank_tile(const Cfg& c, int32_t lay, int32_t x, int32_t y) {
+  return bank_tile_at(c, (uint32_t)lay * (uint32_t)(c.W * c.H) + (uint32_t)(x * c.H + y));
 }
 
 // Dungeon.is_blocked (world.py:41-46).  GRID = dungeon bank: outside the grid
@@ -3098,6 +3100,18 @@ __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kern
       traj.write(me, kp, ks, isB, tick, status, ORX_MOVE_STAY);
       continue;
     }
+    // GRID: the four neighbours' tiles (up, right, down, left: a byte each),
+    // read before the move is known, so the read is off the tick's chain
+    uint32_t nb_tiles = 0u;
+    if constexpr (GRID) {
+      const uint32_t own = (uint32_t)me.lay * (uint32_t)(c.W * c.H) + (uint32_t)(me.x * c.H + me.y);
+      const uint32_t last = (uint32_t)(c.L * c.W * c.H) - 1u;
+      auto rd = [&](int32_t d) -> uint32_t {
+        const uint32_t k = own + (uint32_t)d;
+        return bank_tile_at(c, k > last ? own : k);  // (off the grid: blocked below)
+      };
+      nb_tiles = rd(-1) | (rd(c.H) << 8) | (rd(1) << 16) | (rd(-c.H) << 24);
+    }
     // the bot's move (randombot.py:20-21 / staircasebot.py:9-21)
     W4 tb = {0u, 0u, 0u, 0u};
     uint32_t h0 = 0u, h3 = 0u;  // PM 1: the tick block's deferred words c, d
@@ -3136,10 +3150,13 @@ __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kern
     calc_pos(me.x, me.y, move, tx, ty);
     bool st_tile = false;  // GRID: the target tile is a staircase
     if constexpr (GRID) {
-      // one tile read: a Wall or the grid's edge blocks (a blocked player's
+      // the target's tile from the prefetched neighbours (a Stay: the own
+      // cell, Ground); a Wall or the grid's edge blocks (a blocked player's
       // own cell is never a staircase)
       const bool in = (uint32_t)tx < (uint32_t)c.W && (uint32_t)ty < (uint32_t)c.H;
-      const uint32_t tile = bank_tile(c, me.lay, in ? tx : me.x, in ? ty : me.y);
+      const uint32_t tile = move == ORX_MOVE_STAY
+                                ? (uint32_t)ORX_TILE_GROUND
+                                : __builtin_amdgcn_ubfe(nb_tiles, 8u * (uint32_t)(move - 1), 8u);
       const bool blk = !in || tile == ORX_TILE_WALL;
       st_tile = !blk && tile == ORX_TILE_STAIRCASE_DOWN;
       tx = blk ? me.x : tx;
@@ -3284,6 +3301,64 @@ __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kern
                    isB ? kme : k_o);
           me.x = hit_me ? me.x : tx;
           me.y = hit_me ? me.y : ty;
+          dl.eps += end ? 1 : 0;
+          tick = ft;
+          status = end ? ORX_TIE : ORX_IN_PROGRESS;
+          fast = true;
+#ifdef ORX_STAMPS
+          ORX_COUNT(dl.n_hits);
+#endif
+        }
+      }
+      if constexpr (PM == 3 && NCAP > 0) {
+        // The character mechanics' common rare tick: NPC hits and steps onto
+        // items without a meet or a staircase (rare_tick's rules, in its
+        // order: moves, hits, the kills' drops, experience, pickups).  Each
+        // lane spends its own player's mana on its own hit and takes its own
+        // item; both lanes apply both hits, drops and pickups to their
+        // identical NPC and item registers (no meet: the two targets differ,
+        // so the hits are order-free).
+        if (in_progress & !meet & !st_me & (st_o == 0) & (hit_me | (hit_o != 0))) {
+          const uint32_t kme = pack_cell(tx, ty);
+          const int s_me = hit_me ? npc.find(kme) : -1;
+          const bool item_me = s_me >= 0 && ((items.on >> s_me) & 1u) != 0u;
+          const int h_me = item_me ? -1 : s_me;                    // the NPC I attack
+          const int32_t d_me = h_me >= 0 ? rpg_attack(c, me) : 0;  // my damage and mana
+          const int h_o = pair_swap(h_me);
+          const int32_t d_o = pair_swap(d_me);
+          const uint32_t k_o = (uint32_t)pair_swap((int32_t)kme);
+          const int h1 = isB ? h_o : h_me, h2 = isB ? h_me : h_o;
+          const uint32_t key1 = isB ? k_o : kme, key2 = isB ? kme : k_o;
+          Events<false> ev{nullptr, 0};
+          bool k1 = false, k2 = false;
+          dl.combat += (h1 >= 0 ? 1 : 0) + (h2 >= 0 ? 1 : 0);
+          npc_hits(c, npc, hp, h1, h2, isB ? d_o : d_me, isB ? d_me : d_o, dl, ev, k1, k2, key1,
+                   key2);
+          if (k1) drop_item(c, key, game, ep, tick, h1, key1, npc, items);
+          if (k2) drop_item(c, key, game, ep, tick, h2, key2, npc, items);
+          if (isB ? k2 : k1) gain_xp(c, me);
+          me.x = h_me >= 0 ? me.x : tx;  // attackers stay
+          me.y = h_me >= 0 ? me.y : ty;
+          // pickups, player 1's then player 2's (a free item spot takes it)
+          const int p_me = (item_me && me.nitems < c.item_slots) ? s_me : -1;
+          const int p_o = pair_swap(p_me);
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const bool mine = (j == 1) == isB;
+            const int k = mine ? p_me : p_o;
+            if (k >= 0) {
+              const bool health_item = ((items.kind >> k) & 1u) != 0u;
+              items.on &= ~(1u << k);
+              items.kind &= ~(1u << k);
+              npc.kill(k);
+              if (mine) {
+                me.nitems += 1;
+                me.mhp += health_item ? c.item_bonus : 0;
+                me.hp += health_item ? c.item_bonus : 0;
+                me.dmg += health_item ? 0 : c.item_bonus;
+              }
+            }
+          }
           dl.eps += end ? 1 : 0;
           tick = ft;
           status = end ? ORX_TIE : ORX_IN_PROGRESS;

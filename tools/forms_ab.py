@@ -1,7 +1,9 @@
 """Paired vs one-lane rollout forms for the character mechanics (PM 3) and a
 dungeon bank (diagnostics): µs per 128-tick step at several batches, as one
 engine or as two stream shards (the headline's layout), with the paired form
-allowed (default) or not (ORX_ROLLOUT_PAIRED=0, read per launch).
+allowed (default) or not (ORX_ROLLOUT_PAIRED=0, read per launch), and for
+two shards also the paired form forced to 32 games per wave
+(ORX_ROLLOUT_LANES=32: the plan's own rule may decline it).
 
     python tools/forms_ab.py > forms.jsonl
 """
@@ -26,8 +28,13 @@ def main():
     T, reps = 128, 8
     for name, cfg in cfgs.items():
         for games, streams in ((65536, 1), (65536, 2), (16384, 1), (4096, 1)):
-            for paired in ("1", "0"):
+            variants = [("1", ""), ("0", "")] + ([("1", "32")] if streams == 2 else [])
+            for paired, lanes in variants:
                 os.environ["ORX_ROLLOUT_PAIRED"] = paired
+                if lanes:
+                    os.environ["ORX_ROLLOUT_LANES"] = lanes
+                else:
+                    os.environ.pop("ORX_ROLLOUT_LANES", None)
                 e = StreamShardedEngine(cfg, games, seed=5, device=dev, n_streams=streams)
                 o, a = e.trajectory_buffers(T)
                 go = e.rollout_launcher(T, 1, 1, obs=o, act=a)
@@ -47,7 +54,8 @@ def main():
                 us = s.elapsed_time(f) * 1e3 / reps
                 sh = e.rollout_shape(1, 1)
                 print(json.dumps({"cfg": name, "games": games, "streams": streams,
-                                  "paired_allowed": paired == "1", "shape": sh,
+                                  "paired_allowed": paired == "1", "lanes_forced": lanes or None,
+                                  "shape": sh,
                                   "us_per_step": round(us, 2),
                                   "env_steps_per_s": games * T / us * 1e6}), flush=True)
                 del e, o, a, go
