@@ -418,8 +418,8 @@ def extras(torch, cfg, dev, B_cfg, K, large_rollout=False):
                          policy="2x RandomBot", grid="64x64, 8 NPCs",
                          note="mana, heal, experience, item drops/pickup on (EXT_RPG; engine "
                               "vs oracle bit-exact, parity unpinned vs the reference); two "
-                              "stream shards timed as the headline step (one lane per game at "
-                              "32 games per wave); us_per_launch = one step")
+                              "stream shards timed as the headline step (the paired form); "
+                              "us_per_launch = one step")
     c5 = {}
     for flag in (0, EXT_SEPARATION_DAMAGE):
         c = EnvConfig.c5()

@@ -630,8 +630,15 @@ __device__ __forceinline__ void calc_pos(int32_t x, int32_t y, int32_t m, int32_
 }
 
 // Dungeon.tiles[x, y] of bank layout `lay` (x, y inside the grid).
+// (The two reads must stay two: merged, they become one flat load of a
+// selected pointer, whose completion waits for every vector memory operation
+// in flight -- the trajectory stores of the ticks before -- measured +10% on
+// a bank's rollout.  The asm on the global read keeps them apart.)
 __device__ __forceinline__ uint32_t bank_tile_at(const Cfg& c, uint32_t idx) {
-  return c.lds_tiles ? orx_lds_tiles[idx] : c.tiles[idx];
+  if (c.lds_tiles) return orx_lds_tiles[idx];
+  uint32_t r = c.tiles[idx];
+  asm volatile("" : "+v"(r));
+  return r;
 }
 __device__ __forceinline__ uint32_t bank_tile(const Cfg& c, int32_t lay, int32_t x, int32_t y) {
   return bank_tile_at(c, (uint32_t)lay * (uint32_t)(c.W * c.H) + (uint32_t)(x * c.H + y));
@@ -2818,6 +2825,14 @@ __global__ void __launch_bounds__(kRolloutBlock) rollout_kernel(orx_cfg_t hc, or
   int32_t sep = (c.ext & ORX_EXT_SEPARATION_DAMAGE) ? st.sep_start[i] : -1;
   bool restarted = false;
   TrajWriter<kTraj, AUX, CF> traj(obs, act, B, i, fmt);
+  // every state load resolved before the tick loop (pair_rollout_kernel)
+  if constexpr (GRID) {
+    launder(p1.x, p1.y, p1.d, p1.hp);
+    launder(p2.x, p2.y, p2.d, p2.hp);
+    launder(p1.sx, p1.sy, p2.sx, p2.sy);
+    launder(p1.lay, p2.lay, tick, status);
+    asm volatile("" : "+v"(sep), "+v"(ep));
+  }
 #ifdef ORX_STAMPS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
@@ -3086,6 +3101,13 @@ __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kern
   bool restarted = false;
   constexpr int need = (PM == 1 || PM == 3) ? 2 : 0;
   PairWriter<AUX, CF> traj(obs, act, B, i, who);
+  // every state load resolved before the tick loop: a value first read in the
+  // loop leaves its load pending at the loop head, and that wait then also
+  // covers the previous ticks' row stores (vmcnt counts both) -- each tick
+  launder(me.x, me.y, me.d, me.hp);
+  launder(me.sx, me.sy, me.lay, tick);
+  launder(status, sep, me.mana, me.xp);
+  launder(me.dmg, me.mhp, me.nitems, reinterpret_cast<int32_t&>(ep));
 #ifdef ORX_STAMPS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
@@ -3099,18 +3121,6 @@ __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kern
       tick += 1;
       traj.write(me, kp, ks, isB, tick, status, ORX_MOVE_STAY);
       continue;
-    }
-    // GRID: the four neighbours' tiles (up, right, down, left: a byte each),
-    // read before the move is known, so the read is off the tick's chain
-    uint32_t nb_tiles = 0u;
-    if constexpr (GRID) {
-      const uint32_t own = (uint32_t)me.lay * (uint32_t)(c.W * c.H) + (uint32_t)(me.x * c.H + me.y);
-      const uint32_t last = (uint32_t)(c.L * c.W * c.H) - 1u;
-      auto rd = [&](int32_t d) -> uint32_t {
-        const uint32_t k = own + (uint32_t)d;
-        return bank_tile_at(c, k > last ? own : k);  // (off the grid: blocked below)
-      };
-      nb_tiles = rd(-1) | (rd(c.H) << 8) | (rd(1) << 16) | (rd(-c.H) << 24);
     }
     // the bot's move (randombot.py:20-21 / staircasebot.py:9-21)
     W4 tb = {0u, 0u, 0u, 0u};
@@ -3150,13 +3160,10 @@ __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kern
     calc_pos(me.x, me.y, move, tx, ty);
     bool st_tile = false;  // GRID: the target tile is a staircase
     if constexpr (GRID) {
-      // the target's tile from the prefetched neighbours (a Stay: the own
-      // cell, Ground); a Wall or the grid's edge blocks (a blocked player's
+      // one tile read: a Wall or the grid's edge blocks (a blocked player's
       // own cell is never a staircase)
       const bool in = (uint32_t)tx < (uint32_t)c.W && (uint32_t)ty < (uint32_t)c.H;
-      const uint32_t tile = move == ORX_MOVE_STAY
-                                ? (uint32_t)ORX_TILE_GROUND
-                                : __builtin_amdgcn_ubfe(nb_tiles, 8u * (uint32_t)(move - 1), 8u);
+      const uint32_t tile = bank_tile(c, me.lay, in ? tx : me.x, in ? ty : me.y);
       const bool blk = !in || tile == ORX_TILE_WALL;
       st_tile = !blk && tile == ORX_TILE_STAIRCASE_DOWN;
       tx = blk ? me.x : tx;
@@ -4150,15 +4157,6 @@ RolloutPlan plan_rollout(const orx_cfg_t* cfg, int pm, uint32_t B, uint32_t conc
       uint32_t L = 32;
       while (L > 8 && (uint64_t)B * concurrency < 2 * simds * L) L >>= 1;
       p.lanes = L;
-      // the character mechanics' rare ticks all run rare_tick, over twice the
-      // active lanes when paired: the pair loses at 32 games per wave (the
-      // 65,536-game two-shard step 196 us paired, 117 one lane) and wins at
-      // 8 (16,384 games 91 against 94, 4,096 games 75 against 88;
-      // profiles/r04_v6/forms_ab.jsonl)
-      if (pm == 3 && L > 16u) {
-        p.paired = false;
-        p.lanes = rollout_lanes(B);
-      }
     }
   }
   p.nt = p.lanes * 4u >= 128u;  // a wave's row segment is a whole line

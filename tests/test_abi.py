@@ -206,10 +206,10 @@ def test_rollout_shape_rules(lib):
     assert shape(EnvConfig(n_npcs=40), 4096) == (16, 1, 0)        # LDS NPC table: one lane per game
     assert shape(EnvConfig.c5(), 16384, 2, 1) == (16, 1, 1)       # mixed bots: the generic form
     assert shape(EnvConfig.c2(), 4096, traj=0) == (16, 1, 1)      # no trajectory buffers
-    # round 4: the character mechanics pair at 8-16 games per wave only; a
-    # dungeon bank pairs (not with separation damage for StaircaseBots)
+    # round 4: the character mechanics and dungeon banks pair too (a bank not
+    # with separation damage for StaircaseBots)
     rpg = EnvConfig(width=64, height=64, n_npcs=8, flags=4 | 8 | 16 | 32)
-    assert shape(rpg, 32768, conc=2) == (32, 1, 1)                # one lane at 32 per wave
+    assert shape(rpg, 32768, conc=2) == (32, 2, 1)
     assert shape(rpg, 4096) == (8, 2, 0)
     assert shape(EnvConfig.c3(), 32768, conc=2, n_layouts=16) == (32, 2, 1)
     assert shape(EnvConfig(width=12, height=10), 4096, 2, 2, n_layouts=4) == (8, 2, 0)
