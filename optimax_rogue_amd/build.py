@@ -37,6 +37,7 @@ VARIANTS = {
     "diag32": ("ORX_DIAG=32",),   # the trajectory stores alone (no tick runs)
     "stamps": ("ORX_STAMPS",),    # per-wave s_memtime stamps + rare-block counts
     "diag64": ("ORX_DIAG=64",),   # the paired RandomBot tick block without Philox
+    "noremap": ("ORX_XCD_REMAP=0",),  # workgroups in dispatch order (no XCD-aware remap)
 }
 
 

@@ -111,6 +111,23 @@ constexpr int kRolloutBlock = ORX_ROLLOUT_BLOCK;  // rollout_kernel workgroup si
 // puts a wave on every SIMD (orx_rollout picks it from the batch and the CU
 // count, rollout_lanes()).
 
+#ifndef ORX_XCD_REMAP
+#define ORX_XCD_REMAP 1
+#endif
+// The rollout kernels' workgroup order, XCD-aware: the dispatcher deals
+// workgroups round-robin over the chip's 8 XCDs (workgroup b to XCD b % 8),
+// so XCD x takes the x-th contiguous run of the grid.  Neighbouring
+// workgroups' games -- which share a 128-B trajectory row segment when a
+// workgroup holds fewer than 32 games -- then write it through one XCD's L2,
+// where the line is merged, instead of two L2s each writing back a partial
+// line.
+__device__ __forceinline__ uint32_t xcd_block() {
+  const uint32_t b = blockIdx.x;
+  if (!ORX_XCD_REMAP) return b;
+  const uint32_t g = gridDim.x, q = g >> 3, r = g & 7u, x = b & 7u;
+  return x * q + (x < r ? x : r) + (b >> 3);
+}
+
 struct Key {
   uint32_t k0, k1;
 };
@@ -2783,7 +2800,7 @@ __global__ void __launch_bounds__(kRolloutBlock) rollout_kernel(orx_cfg_t hc, or
       lds_tiles = true;
     }
   }
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t i = xcd_block() * blockDim.x + threadIdx.x;
   if (lanes < 64u) {  // uniform: lanes >= `lanes` of every wave idle
     if ((threadIdx.x & 63u) >= lanes) return;
     i = (i >> 6) * lanes + (threadIdx.x & 63u);
@@ -3044,7 +3061,7 @@ __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kern
   }
   const uint32_t lane = threadIdx.x & 63u;
   if (lane >= 2u * lanes) return;  // uniform per wave
-  const uint32_t i = ((blockIdx.x * blockDim.x + threadIdx.x) >> 6) * lanes + (lane >> 1);
+  const uint32_t i = ((xcd_block() * blockDim.x + threadIdx.x) >> 6) * lanes + (lane >> 1);
   if (i >= B) return;              // both lanes of a game together
   const uint32_t who = lane & 1u;  // 0: player 1, 1: player 2
   const bool isB = who != 0u;
@@ -3159,12 +3176,18 @@ __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kern
     int32_t tx, ty;
     calc_pos(me.x, me.y, move, tx, ty);
     bool st_tile = false;  // GRID: the target tile is a staircase
+    bool hit_me = false;   // an NPC on my target
     if constexpr (GRID) {
       // one tile read: a Wall or the grid's edge blocks (a blocked player's
       // own cell is never a staircase)
       const bool in = (uint32_t)tx < (uint32_t)c.W && (uint32_t)ty < (uint32_t)c.H;
-      const uint32_t tile = bank_tile(c, me.lay, in ? tx : me.x, in ? ty : me.y);
+      const int32_t cx = in ? tx : me.x, cy = in ? ty : me.y;
+      const uint32_t tile = bank_tile(c, me.lay, cx, cy);
+      // the NPC test on the in-grid cell while the tile read is in flight (a
+      // blocked move's target is the player's own cell, which holds no NPC)
+      if constexpr (NCAP > 0) hit_me = npc_any1_dk(npc, pack_cell(cx, cy), dk);
       const bool blk = !in || tile == ORX_TILE_WALL;
+      hit_me = hit_me & !blk;
       st_tile = !blk && tile == ORX_TILE_STAIRCASE_DOWN;
       tx = blk ? me.x : tx;
       ty = blk ? me.y : ty;
@@ -3182,11 +3205,12 @@ __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kern
     uint32_t e_mo, e_om, e_tt, e_d;
     meet_terms(kp, kt, (uint32_t)me.d, e_mo, e_om, e_tt, e_d);
     const uint32_t mt = min(e_mo, min(e_om, e_tt)) | e_d;  // 0: a meet
-    bool hit_me = false;
-    if constexpr (NCAP > 0) hit_me = npc_any1_dk(npc, kt, dk);
+    if constexpr (NCAP > 0 && !GRID) hit_me = npc_any1_dk(npc, kt, dk);
     // 0: my staircase (GRID: any staircase tile) or an NPC on my target
     const uint32_t z = (hit_me | st_tile) ? 0u : GRID ? 1u : (kt ^ ks);
-    const bool rare = !in_progress | (min(mt, min_swapped(z)) == 0u);
+    // (ORX_DIAG & 128: no rare block -- an ISA census of the common tick only,
+    // never run)
+    const bool rare = (ORX_DIAG & 128) ? false : (!in_progress | (min(mt, min_swapped(z)) == 0u));
     const int32_t ft = tick + 1;
     const bool end = c.max_ticks && ft >= c.max_ticks;
     bool took_ordered = false;

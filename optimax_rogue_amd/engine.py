@@ -545,6 +545,26 @@ class BatchedEngine:
         return torch.stack([self.ret_sum, self.ep_count])
 
 
+# The shard streams, created once per device and shared by every
+# StreamShardedEngine of the process: a HIP stream is bound to one of the
+# process's few hardware queues when it is created, and a fresh pair per engine
+# sometimes landed two shards (or a shard and the caller's stream) on one
+# queue, where they run one after the other -- a two-shard step measured
+# 132 us instead of 84-90 on one engine out of sixteen
+# (profiles/r04_v11/stream_pairs.jsonl).  Reusing the first streams keeps every
+# engine on the queues the first one got; their work is ordered by fork() and
+# join() as before.
+_SHARD_STREAMS: dict = {}
+
+
+def shard_streams(device: torch.device, n: int) -> list:
+    """The process's first ``n`` shard streams on ``device`` (created on first use)."""
+    have = _SHARD_STREAMS.setdefault(torch.device(device), [])
+    while len(have) < n:
+        have.append(torch.cuda.Stream(device=device))
+    return have[:n]
+
+
 class StreamShardedEngine:
     """One GPU's batch as ``n_streams`` shards, each a BatchedEngine on its
     own HIP stream (contiguous global game ids, ``parallel.shard``).
@@ -567,7 +587,7 @@ class StreamShardedEngine:
         self.device = torch.device(device)
         self.B = int(n_games)
         n_streams = max(1, min(int(n_streams), self.B))
-        self.streams = [torch.cuda.Stream(device=self.device) for _ in range(n_streams)]
+        self.streams = shard_streams(self.device, n_streams)
         self.parts = []
         cur = torch.cuda.current_stream(self.device)
         for k, s in enumerate(self.streams):

@@ -3,7 +3,8 @@ dungeon bank (diagnostics): µs per 128-tick step at several batches, as one
 engine or as two stream shards (the headline's layout), with the paired form
 allowed (default) or not (ORX_ROLLOUT_PAIRED=0, read per launch), and for
 two shards also the paired form forced to 32 games per wave
-(ORX_ROLLOUT_LANES=32: the plan's own rule may decline it).
+(ORX_ROLLOUT_LANES=32: the plan's own rule may decline it).  Every variant is
+timed twice, the second pass in reverse order.
 
     python tools/forms_ab.py > forms.jsonl
 """
@@ -29,7 +30,9 @@ def main():
     for name, cfg in cfgs.items():
         for games, streams in ((65536, 1), (65536, 2), (16384, 1), (4096, 1)):
             variants = [("1", ""), ("0", "")] + ([("1", "32")] if streams == 2 else [])
-            for paired, lanes in variants:
+            # two passes, the second in reverse order: an order effect (clock
+            # ramp, first use of a kernel) shows as a pass-to-pass difference
+            for pas, (paired, lanes) in [(0, v) for v in variants] + [(1, v) for v in variants[::-1]]:
                 os.environ["ORX_ROLLOUT_PAIRED"] = paired
                 if lanes:
                     os.environ["ORX_ROLLOUT_LANES"] = lanes
@@ -53,7 +56,7 @@ def main():
                 torch.cuda.synchronize()
                 us = s.elapsed_time(f) * 1e3 / reps
                 sh = e.rollout_shape(1, 1)
-                print(json.dumps({"cfg": name, "games": games, "streams": streams,
+                print(json.dumps({"cfg": name, "games": games, "streams": streams, "pass": pas,
                                   "paired_allowed": paired == "1", "lanes_forced": lanes or None,
                                   "shape": sh,
                                   "us_per_step": round(us, 2),

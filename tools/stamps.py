@@ -27,9 +27,19 @@ def main():
     _lib.LIB_PATH = lib
     from optimax_rogue_amd.engine import BatchedEngine
     dev = torch.device("cuda", 0)
-    cname = os.environ.get("STAMPS_CFG", "c3")   # c5 / c5sep: StaircaseBot on C5's dungeon
+    # c5 / c5sep: StaircaseBot on C5's dungeon; bank: C3 on a 16-layout
+    # dungeon bank; c3_rpg: C3 with the character mechanics
+    cname = os.environ.get("STAMPS_CFG", "c3")
     pol = 2 if cname.startswith("c5") else 1
-    cfg = EnvConfig.c5() if cname == "c5sep" else getattr(EnvConfig, cname)()
+    if cname == "bank":
+        from optimax_rogue_amd import DungeonBank
+        cfg = EnvConfig(width=64, height=64, n_npcs=8,
+                        layouts=DungeonBank.random(64, 64, 16, seed=7).layouts)
+    elif cname == "c3_rpg":
+        from optimax_rogue_amd.enums import EXT_RPG
+        cfg = EnvConfig(width=64, height=64, n_npcs=8, flags=EXT_RPG)
+    else:
+        cfg = EnvConfig.c5() if cname == "c5sep" else getattr(EnvConfig, cname)()
     if cname == "c5sep":
         from optimax_rogue_amd.enums import EXT_SEPARATION_DAMAGE
         cfg.flags, cfg.sep_period = EXT_SEPARATION_DAMAGE, 8
