@@ -114,6 +114,9 @@ constexpr int kRolloutBlock = ORX_ROLLOUT_BLOCK;  // rollout_kernel workgroup si
 #ifndef ORX_XCD_REMAP
 #define ORX_XCD_REMAP 1
 #endif
+#ifndef ORX_LEAN
+#define ORX_LEAN 1  // pair_rollout_kernel's lean StaircaseBot spans (0: A/B builds)
+#endif
 // The rollout kernels' workgroup order, XCD-aware: the dispatcher deals
 // workgroups round-robin over the chip's 8 XCDs (workgroup b to XCD b % 8),
 // so XCD x takes the x-th contiguous run of the grid.  Neighbouring
@@ -306,6 +309,7 @@ struct Deltas {  // counter / return increments, flushed once per launch
 #ifdef ORX_STAMPS
   uint32_t n_rare = 0, n_ordered = 0, n_hits = 0, n_desc = 0, n_meet = 0,  // rare-block entries
            n_reset = 0;
+  uint32_t n_lean = 0;  // lean ticks (pair_rollout_kernel's StaircaseBot spans)
   uint32_t cy_rare = 0, cy_reset = 0, cy_ordered = 0, cy_desc = 0;  // cycles in them
 #endif
 };
@@ -2883,15 +2887,15 @@ __global__ void __launch_bounds__(kRolloutBlock) rollout_kernel(orx_cfg_t hc, or
 #endif
   ORX_STAMP(4);
 #ifdef ORX_STAMPS
-  uint32_t r[10] = {dl.n_rare, dl.n_ordered, dl.n_hits, dl.n_desc, dl.n_meet, dl.n_reset,
-                    dl.cy_rare, dl.cy_reset, dl.cy_ordered, dl.cy_desc};
+  uint32_t r[11] = {dl.n_rare, dl.n_ordered, dl.n_hits, dl.n_desc, dl.n_meet, dl.n_reset,
+                    dl.cy_rare, dl.cy_reset, dl.cy_ordered, dl.cy_desc, dl.n_lean};
 #pragma unroll
-  for (int j = 0; j < 10; ++j)
+  for (int j = 0; j < 11; ++j)
     for (int o = 32; o > 0; o >>= 1) r[j] += __shfl_xor(r[j], o);
   if ((threadIdx.x & 63) == 0) {
     const size_t w = (size_t)((blockIdx.x * blockDim.x + threadIdx.x) >> 6) * 16;
 #pragma unroll
-    for (int j = 0; j < 10; ++j) g_stamps[w + 5 + j] = r[j];
+    for (int j = 0; j < 11; ++j) g_stamps[w + 5 + j] = r[j];
   }
 #endif
 }
@@ -3129,6 +3133,16 @@ __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kern
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
   ORX_STAMP(1);
+  // Lean spans (StaircaseBots on an empty dungeon, C5): both bots walk
+  // greedily to their staircases, so a game's next ticks are plain moves until
+  // a player's target is its staircase (its distance to it, less one), the
+  // two could meet (same depth: the distance between them shrinks by at most
+  // 2 a tick, a meet needs at most 2), the episode ends or, with separation
+  // damage, the depths differ.  `span` counts those ticks from the state a
+  // general tick leaves; while every game of the wave has one left, the wave
+  // runs lean ticks: the move, the step and the row, nothing else.
+  constexpr bool kLean = ORX_LEAN && PM == 2 && NCAP == 0 && !GRID && (ORX_DIAG & (16 | 32 | 64 | 128)) == 0;
+  int32_t span = 0;
   int32_t t = 0;
   do {
 #ifdef ORX_STAMPS
@@ -3138,6 +3152,25 @@ __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kern
       tick += 1;
       traj.write(me, kp, ks, isB, tick, status, ORX_MOVE_STAY);
       continue;
+    }
+    if constexpr (kLean) {
+      if (__builtin_amdgcn_ballot_w64(span <= 0) == 0) {  // uniform: a lean tick
+        const int32_t dx = me.sx - me.x, dy = me.sy - me.y;
+        const int32_t adx = dx < 0 ? -dx : dx, ady = dy < 0 ? -dy : dy;
+        const int32_t mv = adx > ady ? (dx > 0 ? ORX_MOVE_RIGHT : ORX_MOVE_LEFT)
+                                     : (dy > 0 ? ORX_MOVE_DOWN : ORX_MOVE_UP);
+        calc_pos(me.x, me.y, mv, me.x, me.y);
+        me.move = mv;
+        kp = pack_cell(me.x, me.y);
+        tick += 1;
+        if constexpr (SEP) sep = -1;  // one depth: as the common tick's timer reset
+        span -= 1;
+#ifdef ORX_STAMPS
+        ORX_COUNT(dl.n_lean);
+#endif
+        traj.write(me, kp, ks, isB, tick, status, mv);
+        continue;
+      }
     }
     // the bot's move (randombot.py:20-21 / staircasebot.py:9-21)
     W4 tb = {0u, 0u, 0u, 0u};
@@ -3562,6 +3595,18 @@ __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kern
         }
       }
     }
+    if constexpr (kLean) {  // the lean ticks from this state on
+      const int32_t ox = pair_swap(me.x), oy = pair_swap(me.y), od = pair_swap(me.d);
+      const int32_t ex = me.sx - me.x, ey = me.sy - me.y;
+      const int32_t dme = (ex < 0 ? -ex : ex) + (ey < 0 ? -ey : ey);  // to my staircase
+      const int32_t dot = pair_swap(dme);
+      const int32_t mx = me.x - ox, my = me.y - oy;
+      const int32_t m = (mx < 0 ? -mx : mx) + (my < 0 ? -my : my);  // between the players
+      int32_t sp = min(dme, dot) - 1;
+      sp = min(sp, me.d == od ? (m - 1) >> 1 : SEP ? 0 : sp);
+      if (c.max_ticks) sp = min(sp, c.max_ticks - tick - 1);
+      span = status == ORX_IN_PROGRESS ? sp : 0;
+    }
     if (!(ORX_DIAG & 16)) traj.write(me, kp, ks, isB, tick, status, move);
     } while (++t < n_ticks);
   ORX_STAMP(3);
@@ -3608,15 +3653,15 @@ __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kern
 #endif
   ORX_STAMP(4);
 #ifdef ORX_STAMPS
-  uint32_t r[10] = {dl.n_rare, dl.n_ordered, dl.n_hits, dl.n_desc, dl.n_meet, dl.n_reset,
-                    dl.cy_rare, dl.cy_reset, dl.cy_ordered, dl.cy_desc};
+  uint32_t r[11] = {dl.n_rare, dl.n_ordered, dl.n_hits, dl.n_desc, dl.n_meet, dl.n_reset,
+                    dl.cy_rare, dl.cy_reset, dl.cy_ordered, dl.cy_desc, dl.n_lean};
 #pragma unroll
-  for (int j = 0; j < 10; ++j)
+  for (int j = 0; j < 11; ++j)
     for (int o = 32; o > 0; o >>= 1) r[j] += __shfl_xor(r[j], o);
   if ((threadIdx.x & 63) == 0) {
     const size_t w = (size_t)((blockIdx.x * blockDim.x + threadIdx.x) >> 6) * 16;
 #pragma unroll
-    for (int j = 0; j < 10; ++j) g_stamps[w + 5 + j] = r[j];
+    for (int j = 0; j < 11; ++j) g_stamps[w + 5 + j] = r[j];
   }
 #endif
 }

@@ -2,8 +2,8 @@
 -DORX_STAMPS): lane 0 of each wave records s_memtime at kernel entry (0),
 after the state loads landed (1), at tick 64 (2), after the tick loop (3) and
 after the epilogue's stores drained (4); per wave, the rare-block entries by
-kind and the cycles spent in the rare block, its reset, ordered-tick and
-descend branches.
+kind, the cycles spent in the rare block, its reset, ordered-tick and
+descend branches, and the paired StaircaseBot form's lean ticks.
 
     python tools/stamps.py tools/ab_libs/stamps.so [B] [ticks]
 """
@@ -86,6 +86,8 @@ def main():
     for j, n in enumerate(["rare_block", "reset", "ordered", "descend"]):
         v = rare[:, 6 + j]
         out["cycles_in_" + n] = {"p50": int(np.median(v)), "mean": float(v.mean())}
+    lean = buf.reshape(W, 16)[:, 15].astype(np.int64)   # lean ticks (StaircaseBot spans)
+    out["lean_ticks"] = {"mean": float(lean.mean()), "min": int(lean.min())}
     slow = np.argsort(tot)[-10:]
     out["slowest10_rare"] = rare[slow].tolist()
     out["slowest10_loop"] = tot[slow].tolist()
