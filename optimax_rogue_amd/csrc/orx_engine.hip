@@ -3154,22 +3154,25 @@ __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kern
       continue;
     }
     if constexpr (kLean) {
-      if (__builtin_amdgcn_ballot_w64(span <= 0) == 0) {  // uniform: a lean tick
-        const int32_t dx = me.sx - me.x, dy = me.sy - me.y;
-        const int32_t adx = dx < 0 ? -dx : dx, ady = dy < 0 ? -dy : dy;
-        const int32_t mv = adx > ady ? (dx > 0 ? ORX_MOVE_RIGHT : ORX_MOVE_LEFT)
-                                     : (dy > 0 ? ORX_MOVE_DOWN : ORX_MOVE_UP);
-        calc_pos(me.x, me.y, mv, me.x, me.y);
-        me.move = mv;
-        kp = pack_cell(me.x, me.y);
-        tick += 1;
-        if constexpr (SEP) sep = -1;  // one depth: as the common tick's timer reset
-        span -= 1;
+      // the lean ticks as a loop of their own (its values stay in the tick
+      // loop's registers: no copies at a join with the general tick)
+      if (__builtin_amdgcn_ballot_w64(span <= 0) == 0) {  // uniform
+        do {
+          const int32_t dx = me.sx - me.x, dy = me.sy - me.y;
+          const int32_t adx = dx < 0 ? -dx : dx, ady = dy < 0 ? -dy : dy;
+          const int32_t mv = adx > ady ? (dx > 0 ? ORX_MOVE_RIGHT : ORX_MOVE_LEFT)
+                                       : (dy > 0 ? ORX_MOVE_DOWN : ORX_MOVE_UP);
+          calc_pos(me.x, me.y, mv, me.x, me.y);
+          tick += 1;
+          span -= 1;
 #ifdef ORX_STAMPS
-        ORX_COUNT(dl.n_lean);
+          ORX_COUNT(dl.n_lean);
 #endif
-        traj.write(me, kp, ks, isB, tick, status, mv);
-        continue;
+          traj.write(me, pack_cell(me.x, me.y), ks, isB, tick, status, mv);
+        } while (++t < n_ticks && __builtin_amdgcn_ballot_w64(span <= 0) == 0);
+        kp = pack_cell(me.x, me.y);
+        if constexpr (SEP) sep = -1;  // one depth: as the common tick's timer reset
+        if (t >= n_ticks) break;
       }
     }
     // the bot's move (randombot.py:20-21 / staircasebot.py:9-21)
