@@ -664,6 +664,10 @@ __device__ __forceinline__ uint32_t bank_tile_at(const Cfg& c, uint32_t idx) {
 __device__ __forceinline__ uint32_t bank_tile(const Cfg& c, int32_t lay, int32_t x, int32_t y) {
   return bank_tile_at(c, (uint32_t)lay * (uint32_t)(c.W * c.H) + (uint32_t)(x * c.H + y));
 }
+// The same from the LDS copy (launches that staged the bank: the paired form)
+__device__ __forceinline__ uint32_t bank_tile_lds(const Cfg& c, int32_t lay, int32_t x, int32_t y) {
+  return orx_lds_tiles[(uint32_t)lay * (uint32_t)(c.W * c.H) + (uint32_t)(x * c.H + y)];
+}
 
 // Dungeon.is_blocked (world.py:41-46).  GRID = dungeon bank: outside the grid
 // or a Wall tile; else EmptyDungeonGenerator's border.
@@ -3218,7 +3222,7 @@ __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kern
       // own cell is never a staircase)
       const bool in = (uint32_t)tx < (uint32_t)c.W && (uint32_t)ty < (uint32_t)c.H;
       const int32_t cx = in ? tx : me.x, cy = in ? ty : me.y;
-      const uint32_t tile = bank_tile(c, me.lay, cx, cy);
+      const uint32_t tile = bank_tile_lds(c, me.lay, cx, cy);  // (staged: plan_rollout)
       // the NPC test on the in-grid cell while the tile read is in flight (a
       // blocked move's target is the player's own cell, which holds no NPC)
       if constexpr (NCAP > 0) hit_me = npc_any1_dk(npc, pack_cell(cx, cy), dk);
@@ -4193,6 +4197,13 @@ int rollout_pm(const orx_cfg_t* cfg, int32_t p1, int32_t p2, uint32_t B, bool tr
          : 0;
 }
 
+// A bank's tiles staged in LDS by the rollout kernels: up to 64 KiB (the
+// default per-workgroup limit; env ORX_NO_LDS_TILES: never, for measurements).
+bool bank_in_lds(const orx_cfg_t* cfg) {
+  const uint64_t tiles = (uint64_t)cfg->n_layouts * (uint64_t)(cfg->width * cfg->height);
+  return tiles && tiles <= kMaxLdsTiles && !getenv("ORX_NO_LDS_TILES");
+}
+
 // The form, games per wave and store policy of an orx_rollout launch.
 struct RolloutPlan {
   bool paired;     // pair_rollout_kernel: two lanes per game
@@ -4216,9 +4227,11 @@ RolloutPlan plan_rollout(const orx_cfg_t* cfg, int pm, uint32_t B, uint32_t conc
   RolloutPlan p;
   p.lanes = rollout_lanes(B);
   // (its packed cells x | y << 8 need x, y < 256)
-  // a dungeon bank: PM 1 / 3, and PM 2 without separation damage
+  // a dungeon bank: PM 1 / 3, and PM 2 without separation damage, with the
+  // tiles staged in LDS (the paired form reads them only there)
   const bool bank_ok = cfg->n_layouts == 0 ||
-                       !(pm == 2 && (cfg->flags & ORX_EXT_SEPARATION_DAMAGE) != 0);
+                       (!(pm == 2 && (cfg->flags & ORX_EXT_SEPARATION_DAMAGE) != 0) &&
+                        bank_in_lds(cfg));
   p.paired = ncap_for(cfg->n_npcs) != kDense && bank_ok && pm >= 1 && pm <= 3 &&
              cfg->width <= 256 && cfg->height <= 256 && p.lanes <= 32u && paired_enabled();
   if (p.paired) {
@@ -4515,7 +4528,7 @@ int orx_rollout_ex(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p
   const bool nt = plan.nt;
   // dynamic LDS: the bank's tiles when they fit (rollout_kernel stages them)
   const uint64_t tiles = grid ? (uint64_t)cfg->n_layouts * (uint64_t)(cfg->width * cfg->height) : 0;
-  const bool use_lds = tiles && tiles <= kMaxLdsTiles && !getenv("ORX_NO_LDS_TILES");
+  const bool use_lds = grid && bank_in_lds(cfg);
   const uint32_t lds_n = use_lds ? (uint32_t)tiles : 0u;
   uint32_t lds = use_lds ? (uint32_t)((tiles + 15u) & ~15ull) : 0u;
   // dense NPCs: one occupancy bitmap per game of the block after the tiles,
@@ -4537,6 +4550,7 @@ int orx_rollout_ex(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p
   // forms, at most 32 games
   // per wave (env ORX_ROLLOUT_PAIRED=0 turns it off, for measurements)
   if (plan.paired) {
+    if (grid && !lds_n) return fail(ORX_EIO, "orx_rollout: a paired bank launch without LDS tiles");
     const dim3 blocks((B + per_block - 1) / per_block);
     const bool sepd = pm == 2 && (cfg->flags & ORX_EXT_SEPARATION_DAMAGE) != 0;
     // dynamic LDS: a bank's tiles when they fit (lds_n); above the default

@@ -725,6 +725,17 @@ PAIRED_CASES.update({
     "bank_rpg": (dict(width=16, height=12, n_npcs=8, npc_health=2, max_ticks=50,
                       flags=4 | 16 | 32, item_drop_pct=60), (1, 1), 1000, 77),
 })
+# round 4: the StaircaseBot form's lean spans (greedy walks with no staircase
+# target, meet or episode end ahead) on grids large enough that whole waves
+# walk lean for many ticks: episodes ending inside a span, separation damage
+# (lean only while the depths agree), players on different depths
+PAIRED_CASES.update({
+    "stairs_lean_spans": (dict(width=96, height=96, max_ticks=150), (2, 2), 256, 85),
+    "stairs_lean_sep": (dict(width=96, height=96, max_ticks=120, flags=1, sep_period=4), (2, 2),
+                        256, 86),
+    "stairs_lean_separated": (dict(width=80, height=80, start_mode=2, p1_depth=0, p2_depth=1,
+                                   max_ticks=130), (2, 2), 256, 87),
+})
 PAIRED_BANKS = {"bank_random_npcs": (20, 16, 6, 81, (1, 2)), "bank_stairs_unused": (12, 10, 5, 82, (1, 2)),
                 "bank_stairs_npcs": (14, 12, 4, 83, (2,)), "bank_rpg": (16, 12, 5, 84, (1, 3))}
 
