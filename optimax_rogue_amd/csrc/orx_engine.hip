@@ -3142,11 +3142,14 @@ __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kern
   // a player's target is its staircase (its distance to it, less one), the
   // two could meet (same depth: the distance between them shrinks by at most
   // 2 a tick, a meet needs at most 2), the episode ends or, with separation
-  // damage, the depths differ.  `span` counts those ticks from the state a
-  // general tick leaves; while every game of the wave has one left, the wave
-  // runs lean ticks: the move, the step and the row, nothing else.
+  // damage across depths, the next tick's damage would kill.  `span` counts
+  // those ticks from the state a general tick leaves; while every game of the
+  // wave has one left, the wave runs lean ticks: the move, the step, the
+  // separation damage (its ceil(k / period) carried as quotient and remainder,
+  // no division) and the row, nothing else.
   constexpr bool kLean = ORX_LEAN && PM == 2 && NCAP == 0 && !GRID && (ORX_DIAG & (16 | 32 | 64 | 128)) == 0;
   int32_t span = 0;
+  int32_t l_od = 0, l_q = 0, l_r = 0;  // SEP: the other's depth; the next tick's damage and phase
   int32_t t = 0;
   do {
 #ifdef ORX_STAMPS
@@ -3167,15 +3170,27 @@ __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kern
           const int32_t mv = adx > ady ? (dx > 0 ? ORX_MOVE_RIGHT : ORX_MOVE_LEFT)
                                        : (dy > 0 ? ORX_MOVE_DOWN : ORX_MOVE_UP);
           calc_pos(me.x, me.y, mv, me.x, me.y);
-          tick += 1;
           span -= 1;
+          if constexpr (SEP) {  // as the common tick's block (readme.md:46-47)
+            if (me.d != l_od) {
+              sep = sep < 0 ? tick : sep;
+              const bool shallow = me.d < l_od;
+              me.hp -= shallow ? l_q : 0;  // ceil(k / period), k = t0 - sep + 1
+              const bool wrap = l_r + 1 == c.sep_period;
+              l_q += wrap ? 1 : 0;
+              l_r = wrap ? 0 : l_r + 1;
+              if (shallow & (me.hp - l_q <= 0)) span = 0;  // the next tick's damage kills
+            } else {
+              sep = -1;
+            }
+          }
+          tick += 1;
 #ifdef ORX_STAMPS
           ORX_COUNT(dl.n_lean);
 #endif
           traj.write(me, pack_cell(me.x, me.y), ks, isB, tick, status, mv);
         } while (++t < n_ticks && __builtin_amdgcn_ballot_w64(span <= 0) == 0);
         kp = pack_cell(me.x, me.y);
-        if constexpr (SEP) sep = -1;  // one depth: as the common tick's timer reset
         if (t >= n_ticks) break;
       }
     }
@@ -3610,7 +3625,17 @@ __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kern
       const int32_t mx = me.x - ox, my = me.y - oy;
       const int32_t m = (mx < 0 ? -mx : mx) + (my < 0 ? -my : my);  // between the players
       int32_t sp = min(dme, dot) - 1;
-      sp = min(sp, me.d == od ? (m - 1) >> 1 : SEP ? 0 : sp);
+      if (me.d == od) sp = min(sp, (m - 1) >> 1);
+      if constexpr (SEP) {
+        l_od = od;
+        if (me.d != od) {  // the next tick's k = t0 - sep + 1 (sep set there if unset)
+          const int32_t P = c.sep_period;
+          const int32_t kn = tick - (sep < 0 ? tick : sep) + 1;
+          l_q = (kn + P - 1) / P;
+          l_r = kn - 1 - (l_q - 1) * P;
+          if ((me.d < od) & (me.hp - l_q <= 0)) sp = 0;
+        }
+      }
       if (c.max_ticks) sp = min(sp, c.max_ticks - tick - 1);
       span = status == ORX_IN_PROGRESS ? sp : 0;
     }
