@@ -38,7 +38,7 @@ VARIANTS = {
     "stamps": ("ORX_STAMPS",),    # per-wave s_memtime stamps + rare-block counts
     "diag64": ("ORX_DIAG=64",),   # the paired RandomBot tick block without Philox
     "noremap": ("ORX_XCD_REMAP=0",),  # workgroups in dispatch order (no XCD-aware remap)
-    "nolean": ("ORX_LEAN=0",),    # the paired StaircaseBot form without its lean spans
+    "lean": ("ORX_LEAN=1",),      # the paired StaircaseBot form with its lean spans (rejected)
 }
 
 

@@ -115,7 +115,10 @@ constexpr int kRolloutBlock = ORX_ROLLOUT_BLOCK;  // rollout_kernel workgroup si
 #define ORX_XCD_REMAP 1
 #endif
 #ifndef ORX_LEAN
-#define ORX_LEAN 1  // pair_rollout_kernel's lean StaircaseBot spans (0: A/B builds)
+// pair_rollout_kernel's lean StaircaseBot spans: off (measured slower, DESIGN
+// s7.2: the launch is set by its slowest waves, which run few lean ticks and
+// pay the span computation on every general tick); -DORX_LEAN=1 builds them
+#define ORX_LEAN 0
 #endif
 // The rollout kernels' workgroup order, XCD-aware: the dispatcher deals
 // workgroups round-robin over the chip's 8 XCDs (workgroup b to XCD b % 8),

@@ -1,5 +1,7 @@
-"""The paired StaircaseBot form's lean spans (pair_rollout_kernel, kLean),
-checked on the CPU against the oracle: the span the kernel computes after a
+"""The paired StaircaseBot form's lean spans (pair_rollout_kernel, kLean;
+built with -DORX_LEAN=1 -- `python -m optimax_rogue_amd.build --variant lean`
+-- and off by default: measured slower), checked on the CPU
+against the oracle: the span the kernel computes after a
 general tick -- min(distance to the staircase - 1 over both players, (the
 players' distance - 1) / 2 on one depth, ticks before the episode limit; 0
 for a finished game or, with separation damage across depths, when the next
