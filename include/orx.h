@@ -336,9 +336,11 @@ int orx_rollout_lanes(int64_t n_games);
 /* The shape of an orx_rollout launch with these arguments (trajectory:
  * obs and act both given): games per wave (1..64), lanes per game (2 for the
  * paired form -- no dense NPCs (n_npcs <= ORX_MAX_REG_NPCS, held in
- * registers), no dungeon bank, two RandomBots or two StaircaseBots, batches
- * below 64 games per wave: one lane per player; the bench's C3 shards run
- * pair_rollout_kernel<8, 1, 2, false>) and
+ * registers), grids up to 256 x 256, two RandomBots (also with the character
+ * mechanics: mana, experience, items) or two StaircaseBots, a dungeon bank
+ * only when its tiles fit the 64 KiB staged in LDS (and for StaircaseBots
+ * without separation damage), batches below 64 games per wave: one lane per
+ * player; the bench's C3 shards run pair_rollout_kernel<8, 1, 2, false>) and
  * whether the trajectory rows are stored nontemporal (whole-line row
  * segments) or with the default policy; concurrency as in
  * orx_rollout_concurrent (1 for orx_rollout).  Results never depend on it.
