@@ -331,6 +331,42 @@ def test_stream_shards_equal_one_engine(n_streams):
     assert a["ep_count"].sum() >= B
 
 
+def test_engines_sharing_shard_streams():
+    """Two StreamShardedEngines alive at once share the process's shard
+    streams (engine.shard_streams); their launches interleave on them and
+    each still computes what its own single engine does."""
+    import torch
+    from optimax_rogue_amd import EnvConfig
+    from optimax_rogue_amd.engine import StreamShardedEngine
+    from optimax_rogue_amd.enums import OBS_FIELDS
+    cfg = dict(EnvConfig.c3().to_dict(), max_ticks=60)
+    B, T = 3000, 70
+    dev = torch.device("cuda", 0)
+    engs = [StreamShardedEngine(EnvConfig.from_dict(cfg), B, seed=s, device=dev, n_streams=2)
+            for s in (4, 9)]
+    assert all(x is y for x, y in zip(engs[0].streams, engs[1].streams))
+    bufs = [e.trajectory_buffers(T) for e in engs]
+    gos = [e.rollout_launcher(T, 1, 1, obs=o, act=a) for e, (o, a) in zip(engs, bufs)]
+    for e in engs:
+        e.fork()
+    for _ in range(2):
+        for go in gos:
+            go()
+    for e in engs:
+        e.join()
+    for s, e, (so, sa) in zip((4, 9), engs, bufs):
+        one = _engine(cfg, B, s)
+        obs = torch.zeros((T, len(OBS_FIELDS), B), dtype=torch.int32, device=dev)
+        act = torch.zeros((T, B, 2), dtype=torch.int8, device=dev)
+        one.rollout(T, 1, 1, obs=obs, act=act)
+        one.rollout(T, 1, 1, obs=obs, act=act)
+        a, b = one.snapshot(), e.snapshot()
+        for k in STATE_KEYS:
+            assert np.array_equal(a[k], b[k]), (s, k)
+        assert np.array_equal(obs.cpu().numpy(), torch.cat(so, dim=2).cpu().numpy()), s
+        assert np.array_equal(act.cpu().numpy(), torch.cat(sa, dim=1).cpu().numpy()), s
+
+
 @pytest.mark.parametrize("pol", [(1, 1), (2, 2)])
 def test_bank_rollout_forms_agree(pol, monkeypatch):
     """A dungeon bank through the trajectory-specialized rollout (obs and act:
