@@ -39,7 +39,6 @@ VARIANTS = {
     "diag64": ("ORX_DIAG=64",),   # the paired RandomBot tick block without Philox
     "noremap": ("ORX_XCD_REMAP=0",),  # workgroups in dispatch order (no XCD-aware remap)
     "lean": ("ORX_LEAN=1",),      # the paired StaircaseBot form with its lean spans (rejected)
-    "keyshoist": ("ORX_PHILOX_KEYS_AT_USE=0",),  # Philox round keys hoisted (round 4's earlier form)
 }
 
 

@@ -114,9 +114,6 @@ constexpr int kRolloutBlock = ORX_ROLLOUT_BLOCK;  // rollout_kernel workgroup si
 #ifndef ORX_XCD_REMAP
 #define ORX_XCD_REMAP 1
 #endif
-#ifndef ORX_PHILOX_KEYS_AT_USE
-#define ORX_PHILOX_KEYS_AT_USE 1
-#endif
 #ifndef ORX_LEAN
 // pair_rollout_kernel's lean StaircaseBot spans: off (measured slower, DESIGN
 // s7.2: the launch is set by its slowest waves, which run few lean ticks and
@@ -147,12 +144,6 @@ struct W4 {
 
 __device__ __forceinline__ W4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, Key key) {
   uint32_t k0 = key.k0, k1 = key.k1;
-#if ORX_PHILOX_KEYS_AT_USE
-  // the round keys from scalar adds where the block is drawn, not twenty
-  // round-key SGPRs hoisted out of a tick loop (spilled to VGPR lanes and
-  // read back with v_readlane in every rare block that draws)
-  asm volatile("" : "+s"(k0), "+s"(k1));
-#endif
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
     const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
