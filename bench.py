@@ -426,10 +426,17 @@ def extras(torch, cfg, dev, B_cfg, K, large_rollout=False):
         if flag:
             c.flags, c.sep_period = flag, 8
         key = "separation_damage_on" if flag else "separation_damage_off"
-        c5[key] = [rollout_rate(c, g, 2) for g in (131072 // 8, 131072)]
+        # the 8-GPU share as two stream shards timed as the headline step (one
+        # shard's next launch runs while the other's slowest waves finish:
+        # 64 vs 70 us, profiles/r04_v18/shard_small.jsonl), then as one launch,
+        # then the whole 131,072 on one GPU
+        c5[key] = [rollout_rate(c, 131072 // 8, 2, streams=2), rollout_rate(c, 131072 // 8, 2),
+                   rollout_rate(c, 131072, 2)]
     out["c5"] = dict(c5, policy="2x StaircaseBot", grid="128x128",
                      note="separation damage = build extension EXT_SEPARATION_DAMAGE, "
-                          "sep_period 8 (parity unpinned: engine vs oracle only)")
+                          "sep_period 8 (parity unpinned: engine vs oracle only); entries: "
+                          "16,384 games (the 8-GPU share) as two stream shards "
+                          "(us_per_launch = one step) and as one launch, 131,072 as one launch")
     torch.cuda.empty_cache()
     return out
 

@@ -571,6 +571,36 @@ def test_bench_timed_path_vs_oracle(oracle_lib):
     assert (snap["ep_count"][gids] >= 1).all() and (snap["episode"][gids] >= 1).all()
 
 
+@pytest.mark.parametrize("sep", [0, 1])
+def test_bench_c5_share_stream_shards_vs_oracle(sep, oracle_lib):
+    """bench.py's C5 line at the 8-GPU share as it is timed since round 4:
+    StreamShardedEngine(C5, 16,384 games, seed 5, two stream shards of 8,192)
+    -- pair_rollout_kernel<0, 2, 0, SEP> at 8 games per wave -- for 9
+    back-to-back 128-tick launches (fork, launches, join), separation damage
+    off (reference semantics) and on; sampled games replayed on the oracle
+    tick by tick (staircasebot.py:9-21, updater.py:76-162)."""
+    import torch
+    from optimax_rogue_amd import EnvConfig
+    from optimax_rogue_amd.engine import StreamShardedEngine
+    from optimax_rogue_amd.enums import EXT_SEPARATION_DAMAGE
+    cfg = EnvConfig.c5()
+    if sep:
+        cfg.flags, cfg.sep_period = EXT_SEPARATION_DAMAGE, 8
+    B, T, L, seed = 16384, 128, 9, 5
+    eng = StreamShardedEngine(cfg, B, seed=seed, game_offset=0, device=torch.device("cuda", 0),
+                              n_streams=2)
+    assert [e.B for e in eng.parts] == [8192, 8192]
+    assert eng.rollout_shape(2, 2) == {"games_per_wave": 8, "lanes_per_game": 2,
+                                       "nontemporal": False}
+    obs, act = eng.trajectory_buffers(T)
+    launch = eng.rollout_launcher(T, 2, 2, obs=obs, act=act)
+    starts = _window_starts(B, 8192, 6, 17)
+    snap, gids = _timed_form_vs_oracle(oracle_lib, eng, eng.parts, obs, act, launch, cfg,
+                                       (2, 2), seed, T, L, starts)
+    assert (snap["ep_count"][gids] >= 1).all()
+    assert snap["counters"][1][gids].sum() > 100   # the StaircaseBots went deep
+
+
 # bench.py's extras at their timed shapes (bench.extras: rollout_rate, seed 5,
 # one BatchedEngine, 128-tick launches with both trajectory buffers): the
 # form each one launches (lanes per game, nontemporal stores), and 9 launches
