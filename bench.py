@@ -336,12 +336,16 @@ def extras(torch, cfg, dev, B_cfg, K, large_rollout=False):
         if streams > 1:
             # as the headline step: the shards' launches back to back on their
             # streams between one fork and one join, HIP events around them all
+            # (3 warmup steps and 20 timed, as the headline: the shards' tails
+            # overlap the next steps' launches, which a short run under-counts)
             e = StreamShardedEngine(c, games, seed=5, device=dev, n_streams=streams)
             o, a = e.trajectory_buffers(T)
             go = e.rollout_launcher(T, pol, pol, obs=o, act=a)
             e.fork()
-            go()
+            for _ in range(3):
+                go()
             e.join()
+            reps = max(reps, 20)
             ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             torch.cuda.synchronize()
             ev0.record()
