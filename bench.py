@@ -75,6 +75,13 @@ def bytes_per_game(kernel: str, K: int, ticks: int = 1) -> int:
         return 2 + 32 + 16 + 12 + npc_read + 20
     if kernel == "policy":
         return 4 + 4 + 2                       # tick, episode -> 2 int8 actions
+    if kernel == "env_step":
+        # orx_env_step_ex with int64 learner actions for player 1 and a RandomBot
+        # opponent: read the actions 8, status/tick/episode 12, players and
+        # staircases 48, the NPCs; write the action pair 2, positions 16, tick
+        # 4, the observation row 56, reward 4, done 1, status 4 (depth, health
+        # and staircases only where a descend or combat changed them)
+        return 8 + 12 + 48 + npc_read + 2 + 16 + 4 + OBS_BYTES + 4 + 1 + 4
     # players, staircases, tick/status/episode, NPC positions + alive mask + health
     state_in = 32 + 16 + 12 + npc_read + K
     state_out = 32 + 12 + (4 + K if K else 0)  # players, tick/status/episode, alive, health
@@ -248,22 +255,27 @@ def extras(torch, cfg, dev, B_cfg, K, large_rollout=False):
                             "note": "orx_policy + orx_step per tick, 50 ticks per HIP graph"}
     del eng, g
     torch.cuda.empty_cache()
-    # (1b) the learner's per-tick path: VecEnv.step (one orx_env_step launch:
+    # (1b) the learner's per-tick path: VecEnv.step (one orx_env_step_ex launch:
     # int64 learner actions for player 1, RandomBot opponent, observation /
-    # reward / done / status out, no host sync), called eagerly from Python
-    # at the config batch, 400 ticks, wall clock
+    # reward / done / status out, the deferred refused-action count, no host
+    # sync), called eagerly from Python at the config batch, 400 ticks, wall
+    # clock -- with fresh output tensors per step (the default) and from a
+    # ring of two preallocated sets (out_buffers=2)
     from optimax_rogue_amd import VecEnv
-    env = VecEnv(cfg, B_cfg, seed=3, device=dev, opponent=1)
     pool = torch.randint(1, 6, (16, B_cfg), dtype=torch.int64, device=dev)
-    for k in range(20):
-        env.step(pool[k % 16])
-    torch.cuda.synchronize()
     n_ve = 400
-    t0 = time.perf_counter()
-    for k in range(n_ve):
-        env.step(pool[k % 16])
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
+    eager = {}
+    for ring in (0, 2):
+        env = VecEnv(cfg, B_cfg, seed=3, device=dev, opponent=1, out_buffers=ring)
+        for k in range(20):
+            env.step(pool[k % 16])
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(n_ve):
+            env.step(pool[k % 16])
+        torch.cuda.synchronize()
+        eager[ring] = time.perf_counter() - t0
+    el = eager[0]
     # the same 50 calls captured in one HIP graph (no host sync inside
     # VecEnv.step makes it capturable): the device's time per tick
     gv = torch.cuda.CUDAGraph()
@@ -283,11 +295,14 @@ def extras(torch, cfg, dev, B_cfg, K, large_rollout=False):
     gel = (time.perf_counter() - t0) / 500
     out["vecenv_step"] = {"value": B_cfg * n_ve / el, "unit": "env-steps/s",
                           "us_per_tick": el / n_ve * 1e6,
+                          "ring_us_per_tick": eager[2] / n_ve * 1e6,
                           "graph_us_per_tick": gel * 1e6,
                           "note": "VecEnv.step called eagerly from Python (int64 learner actions "
                                   "+ RandomBot opponent -> obs, reward, done, status): one "
-                                  "orx_env_step launch per tick, no host sync; "
-                                  "graph_us_per_tick: 50 calls captured in one HIP graph"}
+                                  "orx_env_step_ex launch per tick, no host sync; us_per_tick "
+                                  "with fresh output tensors, ring_us_per_tick with "
+                                  "out_buffers=2; graph_us_per_tick: 50 calls captured in one "
+                                  "HIP graph"}
     del env, pool, gv
     torch.cuda.empty_cache()
     # (2) large batch: the chip full (2^21 games)
@@ -297,8 +312,19 @@ def extras(torch, cfg, dev, B_cfg, K, large_rollout=False):
         eng.step(eng.policy(1, 1))
     step_s = timed_launches(torch, lambda: eng.step(), 30)
     pol_s = timed_launches(torch, lambda: eng.policy(1, 1), 30)
+    # the learner's fused tick (orx_env_step_ex) at the same batch, its
+    # buffers allocated once
+    la = torch.randint(1, 6, (BL,), dtype=torch.int64, device=dev)
+    lo = torch.empty((BL, len(OBS_FIELDS)), dtype=torch.int32, device=dev)
+    lr = torch.empty(BL, dtype=torch.float32, device=dev)
+    ld = torch.empty(BL, dtype=torch.bool, device=dev)
+    ls = torch.empty(BL, dtype=torch.int32, device=dev)
+    lb = torch.zeros(1, dtype=torch.int32, device=dev)
+    env_s = timed_launches(torch, lambda: eng.env_step(la, 1, lo, lr, ld, ls, lb), 30)
+    del la, lo, lr, ld, ls, lb
     med = lambda v: sorted(v)[len(v) // 2]
     sb = contract_bytes_per_env_step(K) * BL
+    eb = bytes_per_game("env_step", K) * BL
     out["large_batch"] = {
         "games": BL,
         "step_kernel": {"avg_us": med(step_s) * 1e6, "achieved_GBps": sb / med(step_s) / 1e9,
@@ -306,6 +332,13 @@ def extras(torch, cfg, dev, B_cfg, K, large_rollout=False):
                         "bytes_per_env_step": contract_bytes_per_env_step(K),
                         "moved_bytes_per_env_step": bytes_per_game("step", K)},
         "policy_kernel": {"avg_us": med(pol_s) * 1e6},
+        "env_step": {"avg_us": med(env_s) * 1e6, "env_steps_per_s": BL / med(env_s),
+                     "achieved_GBps": eb / med(env_s) / 1e9,
+                     "frac": eb / med(env_s) / 1e9 / HBM_PEAK_GBS,
+                     "bytes_per_env_step": bytes_per_game("env_step", K),
+                     "note": "orx_env_step_ex (int64 learner actions, RandomBot opponent, obs / "
+                             "reward / done / status / refused-action count), median of 30 "
+                             "launches between HIP events"},
     }
     if large_rollout:
         T = 20
@@ -435,12 +468,13 @@ def extras(torch, cfg, dev, B_cfg, K, large_rollout=False):
         # 64 vs 70 us, profiles/r04_v18/shard_small.jsonl), then as one launch,
         # then the whole 131,072 on one GPU
         c5[key] = [rollout_rate(c, 131072 // 8, 2, streams=2), rollout_rate(c, 131072 // 8, 2),
-                   rollout_rate(c, 131072, 2)]
+                   rollout_rate(c, 131072, 2, streams=2), rollout_rate(c, 131072, 2)]
     out["c5"] = dict(c5, policy="2x StaircaseBot", grid="128x128",
                      note="separation damage = build extension EXT_SEPARATION_DAMAGE, "
                           "sep_period 8 (parity unpinned: engine vs oracle only); entries: "
                           "16,384 games (the 8-GPU share) as two stream shards "
-                          "(us_per_launch = one step) and as one launch, 131,072 as one launch")
+                          "(us_per_launch = one step) and as one launch, 131,072 (C5 on one "
+                          "GPU) as two stream shards and as one launch")
     torch.cuda.empty_cache()
     return out
 

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define ORX_ABI_VERSION 5
+#define ORX_ABI_VERSION 6
 
 /* ---- error codes -------------------------------------------------------- */
 #define ORX_OK 0
@@ -338,17 +338,24 @@ int orx_rollout_lanes(int64_t n_games);
  * paired form -- no dense NPCs (n_npcs <= ORX_MAX_REG_NPCS, held in
  * registers), grids up to 256 x 256, two RandomBots (also with the character
  * mechanics: mana, experience, items) or two StaircaseBots, a dungeon bank
- * only when its tiles fit the 64 KiB staged in LDS (and for StaircaseBots
- * without separation damage), batches below 64 games per wave: one lane per
- * player; the bench's C3 shards run pair_rollout_kernel<8, 1, 2, false>) and
- * whether the trajectory rows are stored nontemporal (whole-line row
- * segments) or with the default policy; concurrency as in
- * orx_rollout_concurrent (1 for orx_rollout).  Results never depend on it.
- * No reference counterpart. */
+ * only when its tiles fit the device's per-workgroup LDS (160 KiB on gfx950;
+ * above 64 KiB the launch raises the kernel's limit, and a refused raise
+ * takes the one-lane form with the tiles in global memory) and for
+ * StaircaseBots without separation damage, batches below 64 games per wave:
+ * one lane per player; the bench's C3 shards run
+ * pair_rollout_kernel<8, 1, 2, false>), whether the trajectory rows are
+ * stored nontemporal (whole-line row segments) or with the default policy,
+ * the threads per workgroup (256; 512 for a paired bank above half the LDS:
+ * one workgroup per CU then holds two waves per SIMD) and the dynamic LDS
+ * bytes per workgroup (a bank's tiles, dense NPCs' occupancy bitmaps);
+ * concurrency as in orx_rollout_concurrent (1 for orx_rollout).  Results
+ * never depend on it.  No reference counterpart. */
 typedef struct orx_rollout_shape {
   int32_t games_per_wave;
   int32_t lanes_per_game;
   int32_t nontemporal;
+  int32_t threads_per_block;  /* (ABI 6) */
+  int32_t lds_bytes;          /* (ABI 6) */
 } orx_rollout_shape_t;
 int orx_rollout_shape(const orx_cfg_t* cfg, int32_t policy_p1, int32_t policy_p2,
                       int64_t n_games, int32_t trajectory, int32_t concurrency,
@@ -429,13 +436,27 @@ int orx_policy(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p1,
  * otherwise, on the tick the episode ends) and done[b] (1 on that tick; an
  * engine stop code >= 16 ends it as a truncation); status may be NULL (it is
  * also the observation row's field ORX_OBS_STATUS).  No host sync.  Philox
- * mode only (stock-seed mode: orx_policy + orx_step).  Replaces the bot
+ * mode only (stock-seed mode: orx_policy + orx_step).  action_cols 1 needs a
+ * policy for player 2 (ORX_POLICY_NONE is refused).  Replaces the bot
  * loop's per-tick exchange, optimax_rogue_bots/main.py:118-155, and
  * server/main.py:110-113 for a learner. */
 int orx_env_step(const orx_cfg_t* cfg, const orx_state_t* st, const void* actions,
                  int32_t action_bytes, int32_t action_cols, int32_t policy_p2, int8_t* act,
                  int32_t* obs, float* reward, uint8_t* done, int32_t* status, int64_t n_games,
                  uint64_t seed, int64_t game_offset, void* stream);
+
+/* orx_env_step plus a refused-action count (ABI 6): when bad_actions (a
+ * device uint32) is not NULL, the number of games stopped with
+ * ORX_STATUS_BAD_ACTION by this tick is added to it (device atomics, no
+ * host sync), so a host can detect a learner's out-of-range actions -- e.g.
+ * a 0-based argmax -- without synchronizing every tick (VecEnv reads it
+ * asynchronously).  action_cols 1 with policy_p2 ORX_POLICY_NONE is refused
+ * (ORX_EINVAL): player 2 then has no move; pass both players' actions. */
+int orx_env_step_ex(const orx_cfg_t* cfg, const orx_state_t* st, const void* actions,
+                    int32_t action_bytes, int32_t action_cols, int32_t policy_p2, int8_t* act,
+                    int32_t* obs, float* reward, uint8_t* done, int32_t* status,
+                    uint32_t* bad_actions, int64_t n_games, uint64_t seed, int64_t game_offset,
+                    void* stream);
 
 /* Fused rollout: n_ticks x (orx_policy then orx_step) in one launch, state
  * kept in registers between ticks.  If obs != NULL, tick t's post-step

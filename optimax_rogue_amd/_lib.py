@@ -13,7 +13,7 @@ from .config import OrxCfg
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "liborx.so")
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 
 class OrxState(ctypes.Structure):
@@ -27,7 +27,8 @@ class OrxState(ctypes.Structure):
 
 class OrxRolloutShape(ctypes.Structure):
     """ctypes mirror of orx_rollout_shape_t."""
-    _fields_ = [(n, ctypes.c_int32) for n in ("games_per_wave", "lanes_per_game", "nontemporal")]
+    _fields_ = [(n, ctypes.c_int32) for n in ("games_per_wave", "lanes_per_game", "nontemporal",
+                                                "threads_per_block", "lds_bytes")]
 
 
 class OrxError(RuntimeError):
@@ -42,7 +43,7 @@ EXPORTS = ("orx_abi_version", "orx_last_error", "orx_validate_cfg", "orx_reset",
            "orx_step_events", "orx_policy", "orx_rollout", "orx_dungeon_stairs",
            "orx_dungeon_spawn", "orx_seed_mt", "orx_build_id", "orx_rollout_lanes", "orx_dstore_depths",
            "orx_rollout_shape", "orx_rollout_concurrent", "orx_env_step",
-           "orx_rollout_ex")
+           "orx_rollout_ex", "orx_env_step_ex")
 
 
 def load() -> ctypes.CDLL:
@@ -101,6 +102,10 @@ def load() -> ctypes.CDLL:
         L.orx_env_step.restype = ctypes.c_int
         L.orx_env_step.argtypes = [P(OrxCfg), P(OrxState), vp, i32, i32, i32, vp, vp, vp, vp, vp,
                                    i64, u64, i64, vp]
+    if hasattr(L, "orx_env_step_ex"):
+        L.orx_env_step_ex.restype = ctypes.c_int
+        L.orx_env_step_ex.argtypes = [P(OrxCfg), P(OrxState), vp, i32, i32, i32, vp, vp, vp, vp,
+                                      vp, vp, i64, u64, i64, vp]
     if hasattr(L, "orx_dstore_depths"):
         L.orx_dstore_depths.restype = ctypes.c_int
         L.orx_dstore_depths.argtypes = [P(OrxCfg)]

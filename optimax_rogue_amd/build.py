@@ -84,14 +84,54 @@ def build(force: bool = False, verbose: bool = False, defines: Iterable[str] = (
     if not force and os.path.exists(out) and built_id(out) == sid:
         return out
     os.makedirs(os.path.dirname(out), exist_ok=True)
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC",
-           "-Wall", f'-DORX_BUILD_ID="{sid}"'] + [f"-D{d}" for d in defines] + \
-          ["-o", out + ".tmp", SRC]
-    if verbose:
-        print(" ".join(cmd))
-    subprocess.check_call(cmd)
+    base = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
+            f'-DORX_BUILD_ID="{sid}"'] + [f"-D{d}" for d in defines]
+    if any(d.split("=")[0] == "ORX_STAMPS" for d in defines):
+        # one translation unit (the stamps buffer is a device global read back
+        # by the host side, so every kernel must live in the host's unit)
+        cmd = base + ["-shared", "-o", out + ".tmp", SRC]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.check_call(cmd)
+    else:
+        _build_parts(base, out + ".tmp", verbose)
     os.replace(out + ".tmp", out)
     return out
+
+
+# The split build: orx_engine.hip compiled NPARTS times in parallel (part 0:
+# the host side, every kernel instance declared extern; parts 1..NPARTS-1:
+# their share of the explicit instantiations, orx_engine.hip "Kernel
+# instances"), then linked -- about a minute on 8 cores instead of ~6 for one
+# translation unit.
+NPARTS = 13
+
+
+def _build_parts(base, out, verbose=False, jobs=None):
+    import tempfile
+    jobs = jobs or max(1, min(NPARTS, int(os.environ.get("MAX_JOBS", 0)) or os.cpu_count() or 1))
+    with tempfile.TemporaryDirectory(prefix="orx_build_") as tmp:
+        objs = [os.path.join(tmp, f"part{k}.o") for k in range(NPARTS)]
+        cmds = [base + ["-c", f"-DORX_NPARTS={NPARTS}", f"-DORX_PART={k}", "-o", objs[k], SRC]
+                for k in range(NPARTS)]
+        if verbose:
+            print(" ".join(cmds[0]) + f"  (parts 0..{NPARTS - 1}, {jobs} at a time)")
+        # the heaviest parts first (the paired and one-lane rollouts)
+        order = list(range(1, NPARTS)) + [0]
+        running, failed = [], []
+        while order or running:
+            while order and len(running) < jobs:
+                k = order.pop(0)
+                running.append((k, subprocess.Popen(cmds[k])))
+            k, p = running.pop(0)
+            if p.wait() != 0:
+                failed.append(k)
+        if failed:
+            raise subprocess.CalledProcessError(1, f"hipcc part(s) {failed}")
+        link = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out] + objs
+        if verbose:
+            print(" ".join(link))
+        subprocess.check_call(link)
 
 
 def build_variant(name: str, force: bool = False, verbose: bool = False) -> str:

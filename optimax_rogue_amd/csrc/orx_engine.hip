@@ -52,7 +52,18 @@
 
 #include "../../include/orx.h"
 
-namespace {
+// Split build (optimax_rogue_amd/build.py): this file is compiled ORX_NPARTS
+// times in parallel.  Part 0 holds the host side (the C-ABI) and declares
+// every kernel instance `extern template`; part k >= 1 explicitly
+// instantiates its share of the instances (the lists before the host side).
+// Without ORX_NPARTS it is one translation unit (the stamps builds).
+#ifdef ORX_NPARTS
+#define ORX_HOST_TU (ORX_PART == 0)
+#else
+#define ORX_HOST_TU 1
+#endif
+
+namespace orx_dev {
 
 // ---------------------------------------------------------------------------
 // Philox4x32-10 and the reference's bounded-integer transforms
@@ -300,12 +311,13 @@ struct Cfg {  // device copy of orx_cfg_t plus derived constants (all wave-unifo
 };
 
 // The dungeon bank's tiles in LDS (the rollout stages them once per block
-// when they fit, kMaxLdsTiles; every tile test of the tick then reads LDS
-// instead of waiting out an L2 round trip -- at one wave per SIMD nothing
-// hides that latency).
+// when they fit the device's per-workgroup LDS; every tile test of the tick
+// then reads LDS instead of waiting out an L2 round trip -- at one wave per
+// SIMD nothing hides that latency).  Above kMaxLdsTiles (the default
+// per-workgroup limit) the launch raises the kernel's limit first.
 extern __shared__ uint8_t orx_lds_tiles[];
-constexpr uint32_t kMaxLdsTiles = 64 * 1024;
-constexpr uint32_t kMaxLdsBlock = 160 * 1024;  // LDS per CU (one workgroup may take it all)
+inline constexpr uint32_t kMaxLdsTiles = 64 * 1024;
+inline constexpr uint32_t kMaxLdsBlock = 160 * 1024;  // LDS per CU (one workgroup may take it all)
 
 struct Deltas {  // counter / return increments, flushed once per launch
   int32_t combat, descend, dungeon, npc_death, ret, eps;
@@ -1976,13 +1988,23 @@ __global__ void __launch_bounds__(256) reset_kernel(orx_cfg_t hc, orx_state_t st
 // code compiled out -- fewer registers, so more waves per SIMD hide the
 // state loads (the per-tick drop-in's common case)
 // One game's Updater.update (or its autoreset): the per-tick step kernels'
-// body.  get_action() yields the game's packed action pair (player 1 in the
-// low byte); it is called only for a game in progress.
-template <int NCAP, bool EV, bool GRID, bool EXT, class A>
+// body.  get_action(p1, p2, tick, ep) yields the game's packed action pair
+// (player 1 in the low byte).  Without an output callback (NoOut: the step
+// kernels) it is called only for a game in progress, with p1 / p2 / tick /
+// ep not loaded.  With one (env_step_kernel) every state word is loaded up
+// front -- one round trip for the whole launch -- get_action sees the
+// pre-tick players for every game, and out(p1, p2, tick, status) receives the
+// post-step state from registers (no re-read of what was just stored).
+struct NoOut {
+  __device__ __forceinline__ void operator()(const Player&, const Player&, int32_t, int32_t) {}
+};
+
+template <int NCAP, bool EV, bool GRID, bool EXT, class A, class O = NoOut>
 __device__ __forceinline__ void step_game(const orx_cfg_t& hc, const orx_state_t& st, A get_action,
                                           uint32_t B, uint32_t i, Key key, uint32_t off,
                                           int32_t* __restrict__ events,
-                                          int32_t* __restrict__ n_events) {
+                                          int32_t* __restrict__ n_events, O out = O{}) {
+  constexpr bool kOut = !std::is_same<O, NoOut>::value;
   Cfg c = make_cfg(hc, st);
   if constexpr (!EXT) c.ext = 0;
   const uint32_t game = off + i;
@@ -1990,37 +2012,52 @@ __device__ __forceinline__ void step_game(const orx_cfg_t& hc, const orx_state_t
   Npcs<NCAP> npc;
   npc.bind(st, c, B, i);
   Player p1, p2;
+  int32_t tick = 0;
+  uint32_t ep = 0;
+  uint16_t a = 0;
+  if constexpr (kOut) {
+    load_players<GRID>(st, B, i, p1, p2);
+    tick = st.tick[i];
+    ep = (uint32_t)st.episode[i];
+    a = get_action(p1, p2, tick, ep);
+  }
   if (status != ORX_IN_PROGRESS) {
     if (EV) n_events[i] = 0;
-    if (!c.autoreset) return;
-    const uint32_t ep = (uint32_t)st.episode[i] + 1u;
-    int32_t tick;
-    setup_game<NCAP, GRID>(c, key, game, ep, p1, p2, npc, tick, status);
+    if (!c.autoreset) {
+      out(p1, p2, tick, status);
+      return;
+    }
+    const uint32_t ep1 = (kOut ? ep : (uint32_t)st.episode[i]) + 1u;
+    setup_game<NCAP, GRID>(c, key, game, ep1, p1, p2, npc, tick, status);
     store_players<GRID>(st, B, i, p1, p2, true);
     Items<NCAP> items;
     items.clear();
     store_rpg(st, c, B, i, p1, p2, npc, items);
     st.tick[i] = tick;
     st.status[i] = status;
-    st.episode[i] = (int32_t)ep;
+    st.episode[i] = (int32_t)ep1;
     if (c.ext & ORX_EXT_SEPARATION_DAMAGE) st.sep_start[i] = -1;
     if constexpr (NCAP > 0) {
       npc.store_alive(st.npc_alive, B, i);
       store_new_npcs(st, c, B, i, npc);
     }
+    out(p1, p2, tick, status);
     return;
   }
-  const uint16_t a = get_action();
+  if constexpr (!kOut) a = get_action(p1, p2, tick, ep);
   p1.move = (int8_t)(a & 0xFF);
   p2.move = (int8_t)(a >> 8);
   if (!valid_move(c, p1.move) || !valid_move(c, p2.move)) {
     st.status[i] = ORX_STATUS_BAD_ACTION;
     if (EV) n_events[i] = 0;
+    out(p1, p2, tick, (int32_t)ORX_STATUS_BAD_ACTION);
     return;
   }
-  const uint32_t ep = (uint32_t)st.episode[i];
-  int32_t tick = st.tick[i];
-  load_players<GRID>(st, B, i, p1, p2);
+  if constexpr (!kOut) {
+    ep = (uint32_t)st.episode[i];
+    tick = st.tick[i];
+    load_players<GRID>(st, B, i, p1, p2);
+  }
   load_npcs(st, c, B, i, npc);
   Items<NCAP> items;
   load_rpg(st, c, B, i, p1, p2, npc, items);
@@ -2040,6 +2077,7 @@ __device__ __forceinline__ void step_game(const orx_cfg_t& hc, const orx_state_t
   if (NCAP > 0 && dl.npc_death) npc.store_alive(st.npc_alive, B, i);
   flush_deltas(st, B, i, dl);
   if (EV) n_events[i] = ev.n;
+  out(p1, p2, tick, status);
 }
 
 template <int NCAP, bool EV, bool GRID, bool EXT = true>
@@ -2051,10 +2089,14 @@ __global__ void __launch_bounds__(256) step_kernel(orx_cfg_t hc, orx_state_t st,
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= B) return;
   step_game<NCAP, EV, GRID, EXT>(
-      hc, st, [&] { return reinterpret_cast<const uint16_t*>(actions)[i]; }, B, i, key, off,
-      events, n_events);
+      hc, st,
+      [&](const Player&, const Player&, int32_t, uint32_t) {
+        return reinterpret_cast<const uint16_t*>(actions)[i];
+      },
+      B, i, key, off, events, n_events);
 }
 
+#if ORX_HOST_TU
 __global__ void __launch_bounds__(256) policy_kernel(orx_state_t st, int32_t pol1, int32_t pol2,
                                                      int8_t* __restrict__ actions, uint32_t B,
                                                      Key key, uint32_t off) {
@@ -2081,68 +2123,79 @@ __global__ void __launch_bounds__(256) policy_kernel(orx_state_t st, int32_t pol
   policy_pair(key, off + i, ep, tick, pol1, pol2, tb, p1, p2, a1, a2);
   out[i] = pack_actions(a1, a2);
 }
+#endif  // ORX_HOST_TU
 
 // A learner's tick (orx_env_step, VecEnv.step): the learner's actions read at
 // their own width (dsize bytes; anything outside 1..max move becomes 0, which
 // the step turns into ORX_STATUS_BAD_ACTION, so a wrapped int8 never becomes
-// a legal move), player 2's move from policy `pol2` when cols == 1, the
-// pair written to act (the engine's actions buffer), step_game, and the
-// game's observation row [14], status, reward (player 1's view: +1 / -1 on
-// the tick its episode ends in a win / loss) and done (that tick; an engine
-// stop code >= 16 is a truncation) -- VecEnv.outcome on device, no host
-// sync.  The row is read back from the state this thread just wrote.
+// a legal move), player 2's move from policy `pol2` when cols == 1 (the
+// pre-tick players), the pair written to act (the engine's actions buffer),
+// step_game, and the game's observation row [14], status, reward (player 1's
+// view: +1 / -1 on the tick its episode ends in a win / loss) and done (that
+// tick; an engine stop code >= 16 is a truncation) -- VecEnv.outcome on
+// device, no host sync.  Every state word is loaded once up front and the
+// row comes from registers (step_game's output callback): one HBM round trip
+// per launch.  bad_count (may be NULL): += the games whose actions were
+// refused this tick (one atomic per wave that has any).
 template <int NCAP, bool GRID, bool EXT>
 __global__ void __launch_bounds__(256) env_step_kernel(
     orx_cfg_t hc, orx_state_t st, const void* __restrict__ actions, int32_t dsize, int32_t cols,
     int32_t pol2, int8_t* __restrict__ act, int32_t* __restrict__ obs, float* __restrict__ reward,
-    uint8_t* __restrict__ done, int32_t* __restrict__ status_out, uint32_t B, Key key,
-    uint32_t off) {
+    uint8_t* __restrict__ done, int32_t* __restrict__ status_out, uint32_t* __restrict__ bad_count,
+    uint32_t B, Key key, uint32_t off) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= B) return;
-  const int32_t before = st.status[i];
-  const int64_t hi = (EXT && (hc.flags & ORX_EXT_HEAL)) ? ORX_MOVE_HEAL : ORX_MOVE_STAY;
-  auto learner = [&](uint32_t k) -> int32_t {
-    int64_t v;
-    if (dsize == 1) v = reinterpret_cast<const int8_t*>(actions)[k];
-    else if (dsize == 2) v = reinterpret_cast<const int16_t*>(actions)[k];
-    else if (dsize == 4) v = reinterpret_cast<const int32_t*>(actions)[k];
-    else v = reinterpret_cast<const int64_t*>(actions)[k];
-    return (v >= ORX_MOVE_UP && v <= hi) ? (int32_t)v : 0;
-  };
-  int32_t a1 = learner(cols == 1 ? i : 2u * i), a2 = ORX_MOVE_STAY;
-  if (cols == 2) {
-    a2 = learner(2u * i + 1u);
-  } else if (pol2 != ORX_POLICY_STAY && pol2 != ORX_POLICY_NONE) {
-    Player p1, p2;
-    p2.x = st.p_x[B + i];
-    p2.y = st.p_y[B + i];
-    p2.sx = st.st_x[B + i];
-    p2.sy = st.st_y[B + i];
-    const uint32_t ep = (uint32_t)st.episode[i];
-    const int32_t tick = st.tick[i];
-    const W4 tb = pol2 == ORX_POLICY_RANDOM ? tick_block(key, off + i, ep, tick)
-                                            : W4{0, 0, 0, 0};
-    int32_t keep = a1;
-    policy_pair(key, off + i, ep, tick, ORX_POLICY_NONE, pol2, tb, p1, p2, keep, a2);
-  } else if (pol2 == ORX_POLICY_NONE) {
-    a2 = (int8_t)(reinterpret_cast<const uint16_t*>(act)[i] >> 8);  // kept from before
-  }
-  const uint16_t a = pack_actions(a1, a2);
-  reinterpret_cast<uint16_t*>(act)[i] = a;
-  step_game<NCAP, false, GRID, EXT>(hc, st, [&] { return a; }, B, i, key, off, nullptr, nullptr);
-  const int32_t after = st.status[i];
-  const int32_t row[ORX_OBS_FIELDS] = {
-      st.p_x[i],      st.p_y[i],     st.p_depth[i],     st.p_health[i],     st.p_x[B + i],
-      st.p_y[B + i],  st.p_depth[B + i], st.p_health[B + i], st.tick[i],   after,
-      st.st_x[i],     st.st_y[i],    st.st_x[B + i],    st.st_y[B + i]};
+  const bool live = i < B;
+  bool bad = false;
+  if (live) {
+    const int64_t hi = (EXT && (hc.flags & ORX_EXT_HEAL)) ? ORX_MOVE_HEAL : ORX_MOVE_STAY;
+    auto learner = [&](uint32_t k) -> int32_t {
+      int64_t v;
+      if (dsize == 1) v = reinterpret_cast<const int8_t*>(actions)[k];
+      else if (dsize == 2) v = reinterpret_cast<const int16_t*>(actions)[k];
+      else if (dsize == 4) v = reinterpret_cast<const int32_t*>(actions)[k];
+      else v = reinterpret_cast<const int64_t*>(actions)[k];
+      return (v >= ORX_MOVE_UP && v <= hi) ? (int32_t)v : 0;
+    };
+    // player 1's (and with cols == 2 player 2's) learner action, read before
+    // the state so that both loads are in flight together
+    const int32_t l1 = learner(cols == 1 ? i : 2u * i);
+    const int32_t l2 = cols == 2 ? learner(2u * i + 1u) : (int32_t)ORX_MOVE_STAY;
+    uint16_t pair = 0;
+    int32_t before = ORX_IN_PROGRESS;
+    auto get_action = [&](const Player& p1, const Player& p2, int32_t tick, uint32_t ep) {
+      int32_t a1 = l1, a2 = l2;
+      if (cols == 1 && pol2 != ORX_POLICY_STAY) {  // (orx_env_step refuses POLICY_NONE here)
+        const W4 tb = pol2 == ORX_POLICY_RANDOM ? tick_block(key, off + i, ep, tick)
+                                                : W4{0, 0, 0, 0};
+        int32_t keep = a1;
+        policy_pair(key, off + i, ep, tick, ORX_POLICY_NONE, pol2, tb, p1, p2, keep, a2);
+      }
+      pair = pack_actions(a1, a2);
+      return pair;
+    };
+    auto out = [&](const Player& p1, const Player& p2, int32_t tick, int32_t after) {
+      const int32_t row[ORX_OBS_FIELDS] = {p1.x, p1.y, p1.d, p1.hp, p2.x, p2.y, p2.d, p2.hp,
+                                           tick, after, p1.sx, p1.sy, p2.sx, p2.sy};
 #pragma unroll
-  for (int f = 0; f < ORX_OBS_FIELDS; ++f) obs[(size_t)i * ORX_OBS_FIELDS + f] = row[f];
-  const bool ended = before == ORX_IN_PROGRESS && after >= ORX_PLAYER1_WIN &&
-                     (after <= ORX_TIE || after >= ORX_STATUS_BAD_ACTION);
-  done[i] = ended ? 1 : 0;
-  reward[i] = !ended ? 0.0f : after == ORX_PLAYER1_WIN ? 1.0f : after == ORX_PLAYER2_WIN ? -1.0f
-                                                                                         : 0.0f;
-  if (status_out) status_out[i] = after;
+      for (int f = 0; f < ORX_OBS_FIELDS; ++f) obs[(size_t)i * ORX_OBS_FIELDS + f] = row[f];
+      const bool ended = before == ORX_IN_PROGRESS && after >= ORX_PLAYER1_WIN &&
+                         (after <= ORX_TIE || after >= ORX_STATUS_BAD_ACTION);
+      done[i] = ended ? 1 : 0;
+      reward[i] = !ended ? 0.0f : after == ORX_PLAYER1_WIN ? 1.0f
+                                : after == ORX_PLAYER2_WIN ? -1.0f : 0.0f;
+      if (status_out) status_out[i] = after;
+      bad = before == ORX_IN_PROGRESS && after == ORX_STATUS_BAD_ACTION;
+    };
+    before = st.status[i];
+    step_game<NCAP, false, GRID, EXT>(hc, st, get_action, B, i, key, off, nullptr, nullptr, out);
+    reinterpret_cast<uint16_t*>(act)[i] = pair;
+  }
+  if (bad_count) {  // uniform
+    const uint64_t m = __builtin_amdgcn_ballot_w64(bad);
+    if (m != 0ull && __lane_id() == (uint32_t)__builtin_ctzll(m))
+      __hip_atomic_fetch_add(bad_count, (uint32_t)__builtin_popcountll(m), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // One player descends -- the common case of handle_descend (updater.py:259-296)
@@ -3046,7 +3099,7 @@ struct PairWriter {
 // resets take rare_tick's bank forms (the closed-form fast paths are for
 // empty dungeons).
 template <int NCAP, int PM, int AUX, bool SEP, bool CF = false, bool GRID = false>
-__global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kernel(orx_cfg_t hc, orx_state_t st,
+__global__ void __launch_bounds__(GRID ? 512 : kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kernel(orx_cfg_t hc, orx_state_t st,
                                                                      int32_t n_ticks,
                                                                      int32_t* __restrict__ obs,
                                                                      int8_t* __restrict__ act,
@@ -3710,6 +3763,7 @@ __global__ void __launch_bounds__(kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kern
 // random.seed(n) (CPython random_seed -> init_by_array over the 32-bit words
 // of n) and np.random.seed(n) (numpy mt19937_seed = init_genrand) for
 // n = seed + global game id; both indices at 624 (the first draw twists).
+#if ORX_HOST_TU
 __global__ void __launch_bounds__(256) mt_seed_kernel(orx_state_t st, uint32_t B, uint64_t seed,
                                                       uint32_t off, uint32_t dstore_n) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -3750,6 +3804,7 @@ __global__ void __launch_bounds__(256) mt_seed_kernel(orx_state_t st, uint32_t B
   py[624 * (size_t)B] = 624;
   for (uint32_t k = 0; k < 2u * dstore_n; ++k) st.dstore[(size_t)(2 * k) * B + i] = -1;
 }
+#endif  // ORX_HOST_TU
 
 // RandomBot.move = random.choice(list(Move)) = Move(1 + _randbelow(5))
 // (randombot.py:21) from the game's CPython stream; StaircaseBot as usual.
@@ -3804,6 +3859,7 @@ __global__ void __launch_bounds__(256) mt_reset_kernel(orx_cfg_t hc, orx_state_t
   }
 }
 
+#if ORX_HOST_TU
 __global__ void __launch_bounds__(256) mt_policy_kernel(orx_state_t st, int32_t pol1,
                                                         int32_t pol2,
                                                         int8_t* __restrict__ actions,
@@ -3829,6 +3885,7 @@ __global__ void __launch_bounds__(256) mt_policy_kernel(orx_state_t st, int32_t 
   py.close();
   out[i] = pack_actions(a1, a2);
 }
+#endif  // ORX_HOST_TU
 
 template <int NCAP, bool EV, bool GRID>
 __global__ void __launch_bounds__(256) mt_step_kernel(orx_cfg_t hc, orx_state_t st,
@@ -3987,6 +4044,162 @@ __global__ void __launch_bounds__(256) stairs_kernel(orx_cfg_t hc, orx_state_t s
   if (layout) layout[i] = err ? -1 : lay;
 }
 
+// ---------------------------------------------------------------------------
+// Kernel instances: every template instance the host side launches, as
+// X-macro lists shared by the host dispatch (below) and the split build's
+// explicit instantiations, so the two cannot drift apart.
+// ---------------------------------------------------------------------------
+// (NCAP, GRID): reset_kernel, mt_reset_kernel, mt_rollout_kernel
+#define ORX_NG_LIST(X)                                                                          \
+  X(0, false) X(8, false) X(16, false) X(kDense, false)                                         \
+  X(0, true) X(8, true) X(16, true) X(kDense, true)
+// (NCAP, EV, GRID): step_kernel (all rules) and mt_step_kernel
+#define ORX_STEP_LIST(X)                                                                        \
+  X(0, false, false) X(0, true, false) X(8, false, false) X(8, true, false)                     \
+  X(16, false, false) X(16, true, false) X(0, false, true) X(0, true, true)                     \
+  X(8, false, true) X(8, true, true) X(16, false, true) X(16, true, true)                       \
+  X(kDense, false, false) X(kDense, true, false) X(kDense, false, true) X(kDense, true, true)
+// NCAP: step_kernel<NCAP, false, false, false> (the reference's rules only)
+#define ORX_STEP_REF_LIST(X) X(0) X(8) X(16)
+// (NCAP, GRID, EXT): env_step_kernel
+#define ORX_ENV_LIST(X)                                                                         \
+  X(0, false, false) X(8, false, false) X(16, false, false)                                     \
+  X(0, false, true) X(8, false, true) X(16, false, true)                                        \
+  X(kDense, false, true) X(0, true, true) X(8, true, true) X(16, true, true) X(kDense, true, true)
+// (NCAP, PM, AUX, SEP, CF, GRID): pair_rollout_kernel, per NCAP in two halves
+// -- A: PM 1 / 2 on empty dungeons in both row formats; B: PM 3 and the banks
+#define ORX_PAIR_LIST_C(X, N, C)                                                                \
+  X(N, 1, kStreamAux, false, C, false) X(N, 1, kPartialAux, false, C, false)                    \
+  X(N, 2, kStreamAux, false, C, false) X(N, 2, kPartialAux, false, C, false)                    \
+  X(N, 2, kStreamAux, true, C, false) X(N, 2, kPartialAux, true, C, false)
+#define ORX_PAIR_LIST_A(X, N) ORX_PAIR_LIST_C(X, N, false) ORX_PAIR_LIST_C(X, N, true)
+#define ORX_PAIR_LIST_B(X, N)                                                                   \
+  X(N, 3, kStreamAux, false, false, false) X(N, 3, kPartialAux, false, false, false)            \
+  X(N, 3, kStreamAux, false, false, true) X(N, 3, kPartialAux, false, false, true)              \
+  X(N, 1, kStreamAux, false, false, true) X(N, 1, kPartialAux, false, false, true)              \
+  X(N, 2, kStreamAux, false, false, true) X(N, 2, kPartialAux, false, false, true)
+#define ORX_PAIR_LIST(X)                                                                        \
+  ORX_PAIR_LIST_A(X, 0) ORX_PAIR_LIST_B(X, 0) ORX_PAIR_LIST_A(X, 8) ORX_PAIR_LIST_B(X, 8)       \
+  ORX_PAIR_LIST_A(X, 16) ORX_PAIR_LIST_B(X, 16)
+// (NCAP, PM, GRID, AUX, CF): rollout_kernel -- the generic form (PM 0) in one
+// store policy and any row format; the buffer-store forms (PM 1 / 2 / 3) in
+// both policies; PM 1 / 2 without a bank or dense NPCs also in compact rows
+#define ORX_ROLLOUT_LIST_NG(X, N, G)                                                            \
+  X(N, 0, G, kStreamAux, false)                                                                 \
+  X(N, 1, G, kStreamAux, false) X(N, 1, G, kPartialAux, false)                                  \
+  X(N, 2, G, kStreamAux, false) X(N, 2, G, kPartialAux, false)                                  \
+  X(N, 3, G, kStreamAux, false) X(N, 3, G, kPartialAux, false)
+#define ORX_ROLLOUT_LIST_N(X, N)                                                                \
+  ORX_ROLLOUT_LIST_NG(X, N, false) ORX_ROLLOUT_LIST_NG(X, N, true)                              \
+  X(N, 1, false, kStreamAux, true) X(N, 1, false, kPartialAux, true)                            \
+  X(N, 2, false, kStreamAux, true) X(N, 2, false, kPartialAux, true)
+#define ORX_ROLLOUT_LIST_DENSE(X)                                                               \
+  X(kDense, 0, false, kStreamAux, false) X(kDense, 0, true, kStreamAux, false)                  \
+  X(kDense, 1, false, kStreamAux, false) X(kDense, 1, false, kPartialAux, false)                \
+  X(kDense, 2, false, kStreamAux, false) X(kDense, 2, false, kPartialAux, false)                \
+  X(kDense, 1, true, kStreamAux, false) X(kDense, 1, true, kPartialAux, false)                  \
+  X(kDense, 2, true, kStreamAux, false) X(kDense, 2, true, kPartialAux, false)
+#define ORX_ROLLOUT_LIST(X)                                                                     \
+  ORX_ROLLOUT_LIST_N(X, 0) ORX_ROLLOUT_LIST_N(X, 8) ORX_ROLLOUT_LIST_N(X, 16)                   \
+  ORX_ROLLOUT_LIST_DENSE(X)
+
+#ifdef ORX_NPARTS
+// ORX_INST: `extern` in the host part (an explicit instantiation
+// declaration: the part that owns the instance emits it), empty in the
+// instance parts (an explicit instantiation definition)
+#if ORX_PART == 0
+#define ORX_INST extern
+#else
+#define ORX_INST
+#endif
+#define ORX_I_RESET(N, G)                                                                       \
+  ORX_INST template __global__ void reset_kernel<N, G>(orx_cfg_t, orx_state_t, const uint8_t*,  \
+                                                       uint32_t, Key, uint32_t);
+#define ORX_I_MT_RESET(N, G)                                                                    \
+  ORX_INST template __global__ void mt_reset_kernel<N, G>(orx_cfg_t, orx_state_t,               \
+                                                          const uint8_t*, uint32_t);
+#define ORX_I_MT_ROLLOUT(N, G)                                                                  \
+  ORX_INST template __global__ void mt_rollout_kernel<N, G>(orx_cfg_t, orx_state_t, int32_t,    \
+                                                            int32_t, int32_t, int32_t*, int8_t*, \
+                                                            uint32_t, Key, uint32_t, int32_t);
+#define ORX_I_STEP(N, E, G)                                                                     \
+  ORX_INST template __global__ void step_kernel<N, E, G, true>(orx_cfg_t, orx_state_t,          \
+                                                               const int8_t*, uint32_t, Key,    \
+                                                               uint32_t, int32_t*, int32_t*);
+#define ORX_I_STEP_REF(N)                                                                       \
+  ORX_INST template __global__ void step_kernel<N, false, false, false>(                        \
+      orx_cfg_t, orx_state_t, const int8_t*, uint32_t, Key, uint32_t, int32_t*, int32_t*);
+#define ORX_I_MT_STEP(N, E, G)                                                                  \
+  ORX_INST template __global__ void mt_step_kernel<N, E, G>(orx_cfg_t, orx_state_t,             \
+                                                            const int8_t*, uint32_t, Key,       \
+                                                            uint32_t, int32_t*, int32_t*);
+#define ORX_I_ENV(N, G, X)                                                                      \
+  ORX_INST template __global__ void env_step_kernel<N, G, X>(                                   \
+      orx_cfg_t, orx_state_t, const void*, int32_t, int32_t, int32_t, int8_t*, int32_t*, float*, \
+      uint8_t*, int32_t*, uint32_t*, uint32_t, Key, uint32_t);
+#define ORX_I_PAIR(N, P, A, S, C, G)                                                            \
+  ORX_INST template __global__ void pair_rollout_kernel<N, P, A, S, C, G>(                      \
+      orx_cfg_t, orx_state_t, int32_t, int32_t*, int8_t*, uint32_t, Key, uint32_t, uint32_t,     \
+      uint32_t);
+#define ORX_I_ROLLOUT(N, P, G, A, C)                                                            \
+  ORX_INST template __global__ void rollout_kernel<N, P, G, A, C>(                              \
+      orx_cfg_t, orx_state_t, int32_t, int32_t, int32_t, int32_t*, int8_t*, uint32_t, Key,      \
+      uint32_t, uint32_t, uint32_t, uint32_t, int32_t);
+#define ORX_I_STAIRS(G)                                                                         \
+  ORX_INST template __global__ void stairs_kernel<G>(orx_cfg_t, orx_state_t, const uint32_t*,    \
+                                                     const int32_t*, const int32_t*,            \
+                                                     const int32_t*, int32_t*, int32_t*,        \
+                                                     int32_t*, uint32_t, Key);
+// the parts: 1-6 the paired rollouts (NCAP 0 / 8 / 16, halves A and B), 7-9
+// the one-lane rollouts per NCAP, 10 the dense rollouts and env_step, 11 the
+// step kernels, 12 the rest; each costs a few tens of seconds of hipcc
+#define ORX_OWNS(k) (ORX_PART == 0 || ORX_PART == (k))
+#if ORX_OWNS(1)
+ORX_PAIR_LIST_A(ORX_I_PAIR, 0)
+#endif
+#if ORX_OWNS(2)
+ORX_PAIR_LIST_B(ORX_I_PAIR, 0)
+#endif
+#if ORX_OWNS(3)
+ORX_PAIR_LIST_A(ORX_I_PAIR, 8)
+#endif
+#if ORX_OWNS(4)
+ORX_PAIR_LIST_B(ORX_I_PAIR, 8)
+#endif
+#if ORX_OWNS(5)
+ORX_PAIR_LIST_A(ORX_I_PAIR, 16)
+#endif
+#if ORX_OWNS(6)
+ORX_PAIR_LIST_B(ORX_I_PAIR, 16)
+#endif
+#if ORX_OWNS(7)
+ORX_ROLLOUT_LIST_N(ORX_I_ROLLOUT, 0)
+#endif
+#if ORX_OWNS(8)
+ORX_ROLLOUT_LIST_N(ORX_I_ROLLOUT, 8)
+#endif
+#if ORX_OWNS(9)
+ORX_ROLLOUT_LIST_N(ORX_I_ROLLOUT, 16)
+#endif
+#if ORX_OWNS(10)
+ORX_ROLLOUT_LIST_DENSE(ORX_I_ROLLOUT)
+ORX_ENV_LIST(ORX_I_ENV)
+#endif
+#if ORX_OWNS(11)
+ORX_STEP_LIST(ORX_I_STEP)
+ORX_STEP_REF_LIST(ORX_I_STEP_REF)
+ORX_STEP_LIST(ORX_I_MT_STEP)
+#endif
+#if ORX_OWNS(12)
+ORX_NG_LIST(ORX_I_RESET)
+ORX_NG_LIST(ORX_I_MT_RESET)
+ORX_NG_LIST(ORX_I_MT_ROLLOUT)
+ORX_I_STAIRS(false)
+ORX_I_STAIRS(true)
+#endif
+#endif  // ORX_NPARTS
+
+#if ORX_HOST_TU
 // ---------------------------------------------------------------------------
 // Host side of the C-ABI
 // ---------------------------------------------------------------------------
@@ -4225,11 +4438,45 @@ int rollout_pm(const orx_cfg_t* cfg, int32_t p1, int32_t p2, uint32_t B, bool tr
          : 0;
 }
 
-// A bank's tiles staged in LDS by the rollout kernels: up to 64 KiB (the
-// default per-workgroup limit; env ORX_NO_LDS_TILES: never, for measurements).
+// A bank's tiles staged in LDS by the rollout kernels: up to the device's
+// per-workgroup limit (160 KiB on gfx950; above the default 64 KiB the launch
+// raises the kernel's limit, raise_lds).  Env ORX_NO_LDS_TILES: never, for
+// measurements.
 bool bank_in_lds(const orx_cfg_t* cfg) {
   const uint64_t tiles = (uint64_t)cfg->n_layouts * (uint64_t)(cfg->width * cfg->height);
-  return tiles && tiles <= kMaxLdsTiles && !getenv("ORX_NO_LDS_TILES");
+  return tiles && tiles <= device_lds_per_block() && !getenv("ORX_NO_LDS_TILES");
+}
+
+// Raises kernel `fn`'s dynamic-LDS limit to `bytes` when they exceed the
+// default 64 KiB; false when the device or the runtime refuses (env
+// ORX_REFUSE_LDS_RAISE=1 simulates a refusal, for tests), so the caller
+// launches a form that does not need them.
+bool raise_lds(const void* fn, uint32_t bytes) {
+  if (bytes <= kMaxLdsTiles) return true;
+  if (bytes > device_lds_per_block()) return false;
+  const char* e = getenv("ORX_REFUSE_LDS_RAISE");
+  if (e && e[0] == '1') return false;
+  if (!fn) return true;  // (orx_rollout_shape: whether a raise is needed and allowed)
+  if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) !=
+      hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return true;
+}
+
+// Threads per paired-rollout workgroup: kRolloutBlock, or 512 for a bank
+// whose tiles leave room for one workgroup per CU (more than half the LDS):
+// then the CU's one copy of the tiles serves 8 waves, two per SIMD, the
+// occupancy the paired plan's games per wave assume.  Env
+// ORX_ROLLOUT_THREADS (64 / 128 / 256, and 512 for banks) overrides.
+uint32_t pair_threads(const orx_cfg_t* cfg, uint32_t lanes, uint32_t lds_n) {
+  (void)lanes;
+  const char* e = getenv("ORX_ROLLOUT_THREADS");
+  const int x = e ? atoi(e) : 0;
+  if (x == 64 || x == 128 || x == 256 || (x == 512 && cfg->n_layouts > 0)) return (uint32_t)x;
+  if (cfg->n_layouts > 0 && 2ull * lds_n > device_lds_per_block()) return 512u;
+  return (uint32_t)kRolloutBlock;
 }
 
 // The form, games per wave and store policy of an orx_rollout launch.
@@ -4260,8 +4507,18 @@ RolloutPlan plan_rollout(const orx_cfg_t* cfg, int pm, uint32_t B, uint32_t conc
   const bool bank_ok = cfg->n_layouts == 0 ||
                        (!(pm == 2 && (cfg->flags & ORX_EXT_SEPARATION_DAMAGE) != 0) &&
                         bank_in_lds(cfg));
+  // StaircaseBots (PM 2) also pair where the one-lane rule fills whole
+  // waves, when the batch shares the device with another launch and the
+  // device's games come to at most four 32-game waves per SIMD: C5's 131,072
+  // games as two 65,536-game stream shards, 177-179 us per 128-tick step
+  // paired against 183-192 one-lane (242 / 254 with separation damage;
+  // profiles/r05_v1/c5_forms.jsonl)
+  const uint64_t simds4 = 4ull * 32ull * (uint64_t)device_simds();
+  const bool pm2_full = pm == 2 && p.lanes == 64u && concurrency >= 2 &&
+                        (uint64_t)B * concurrency <= simds4 && !lanes_override();
   p.paired = ncap_for(cfg->n_npcs) != kDense && bank_ok && pm >= 1 && pm <= 3 &&
-             cfg->width <= 256 && cfg->height <= 256 && p.lanes <= 32u && paired_enabled();
+             cfg->width <= 256 && cfg->height <= 256 && (p.lanes <= 32u || pm2_full) &&
+             paired_enabled();
   if (p.paired) {
     if (const int o = lanes_override()) {
       p.lanes = o < 32 ? (uint32_t)o : 32u;
@@ -4275,8 +4532,12 @@ RolloutPlan plan_rollout(const orx_cfg_t* cfg, int pm, uint32_t B, uint32_t conc
   p.nt = p.lanes * 4u >= 128u;  // a wave's row segment is a whole line
   return p;
 }
+#endif  // ORX_HOST_TU
 
-}  // namespace
+}  // namespace orx_dev
+
+#if ORX_HOST_TU
+using namespace orx_dev;
 
 extern "C" {
 
@@ -4304,6 +4565,8 @@ int orx_rollout_shape(const orx_cfg_t* cfg, int32_t policy_p1, int32_t policy_p2
   if (n_games <= 0 || n_games > 0x7FFFFFFFLL) return fail(ORX_EINVAL, "bad n_games");
   if (!out) return fail(ORX_EINVAL, "out is NULL");
   const uint32_t B = (uint32_t)n_games;
+  out->threads_per_block = kBlock;
+  out->lds_bytes = 0;
   if (cfg->rng == ORX_RNG_MT19937) {  // mt_rollout_kernel: one game per lane, full waves
     out->games_per_wave = 64;
     out->lanes_per_game = 1;
@@ -4311,10 +4574,27 @@ int orx_rollout_shape(const orx_cfg_t* cfg, int32_t policy_p1, int32_t policy_p2
     return ORX_OK;
   }
   const int pm = rollout_pm(cfg, policy_p1, policy_p2, B, trajectory != 0);
-  const RolloutPlan p = plan_rollout(cfg, pm, B, (uint32_t)concurrency);
+  RolloutPlan p = plan_rollout(cfg, pm, B, (uint32_t)concurrency);
+  const uint64_t tiles = (uint64_t)cfg->n_layouts * (uint64_t)(cfg->width * cfg->height);
+  uint32_t lds_n = (cfg->n_layouts > 0 && bank_in_lds(cfg)) ? (uint32_t)tiles : 0u;
+  if (p.paired && !raise_lds(nullptr, lds_n)) {  // the launch's fallback (one lane, global tiles)
+    p.paired = false;
+    p.lanes = rollout_lanes(B);
+    p.nt = p.lanes * 4u >= 128u;
+    lds_n = 0u;
+  }
   out->games_per_wave = (int32_t)p.lanes;
   out->lanes_per_game = p.paired ? 2 : 1;
   out->nontemporal = (pm != 0 && !p.nt) ? 0 : 1;
+  out->threads_per_block = (int32_t)(p.paired ? pair_threads(cfg, p.lanes, lds_n)
+                                              : rollout_threads(B, p.lanes));
+  uint32_t lds = p.paired ? lds_n : (uint32_t)((lds_n + 15u) & ~15u);
+  if (!p.paired && ncap_for(cfg->n_npcs) == kDense && !getenv("ORX_NO_LDS_BITS")) {
+    const uint32_t bb = (uint32_t)((cfg->width * cfg->height + 31) / 32) * 4u;
+    const uint32_t per_block = (uint32_t)out->threads_per_block / 64u * p.lanes;
+    if ((uint64_t)lds + (uint64_t)per_block * bb <= device_lds_per_block()) lds += per_block * bb;
+  }
+  out->lds_bytes = (int32_t)lds;
   return ORX_OK;
 }
 
@@ -4359,8 +4639,7 @@ int orx_reset(const orx_cfg_t* cfg, const orx_state_t* st, const uint8_t* mask, 
 #define ORX_RESET(N, G)                                                                         \
   if (nc == N && grid == G)                                                                     \
     hipLaunchKernelGGL((mt_reset_kernel<N, G>), grid_for(B), dim3(kBlock), 0, s, *cfg, *st, mask, B);
-    ORX_RESET(0, false) ORX_RESET(8, false) ORX_RESET(16, false) ORX_RESET(kDense, false)
-    ORX_RESET(0, true) ORX_RESET(8, true) ORX_RESET(16, true) ORX_RESET(kDense, true)
+    ORX_NG_LIST(ORX_RESET)
 #undef ORX_RESET
     return launch_status("orx_reset");
   }
@@ -4368,8 +4647,7 @@ int orx_reset(const orx_cfg_t* cfg, const orx_state_t* st, const uint8_t* mask, 
   if (nc == N && grid == G)                                                                     \
     hipLaunchKernelGGL((reset_kernel<N, G>), grid_for(B), dim3(kBlock), 0, s, *cfg, *st, mask, B, \
                        k, off);
-  ORX_RESET(0, false) ORX_RESET(8, false) ORX_RESET(16, false) ORX_RESET(kDense, false)
-  ORX_RESET(0, true) ORX_RESET(8, true) ORX_RESET(16, true) ORX_RESET(kDense, true)
+  ORX_NG_LIST(ORX_RESET)
 #undef ORX_RESET
   return launch_status("orx_reset");
 }
@@ -4411,12 +4689,7 @@ static int launch_step(const orx_cfg_t* cfg, const orx_state_t* st, const int8_t
       hipLaunchKernelGGL((step_kernel<NC, E, G>), grid_for(B), dim3(kBlock), 0, s, *cfg, *st,   \
                          actions, B, k, off, events, n_events);                                 \
   }
-  ORX_STEP(0, false, false) ORX_STEP(0, true, false) ORX_STEP(8, false, false)
-  ORX_STEP(8, true, false) ORX_STEP(16, false, false) ORX_STEP(16, true, false)
-  ORX_STEP(0, false, true) ORX_STEP(0, true, true) ORX_STEP(8, false, true)
-  ORX_STEP(8, true, true) ORX_STEP(16, false, true) ORX_STEP(16, true, true)
-  ORX_STEP(kDense, false, false) ORX_STEP(kDense, true, false)
-  ORX_STEP(kDense, false, true) ORX_STEP(kDense, true, true)
+  ORX_STEP_LIST(ORX_STEP)
 #undef ORX_STEP
   return launch_status(name);
 }
@@ -4461,6 +4734,15 @@ int orx_env_step(const orx_cfg_t* cfg, const orx_state_t* st, const void* action
                  int32_t action_bytes, int32_t action_cols, int32_t policy_p2, int8_t* act,
                  int32_t* obs, float* reward, uint8_t* done, int32_t* status, int64_t n_games,
                  uint64_t seed, int64_t game_offset, void* stream) {
+  return orx_env_step_ex(cfg, st, actions, action_bytes, action_cols, policy_p2, act, obs, reward,
+                         done, status, nullptr, n_games, seed, game_offset, stream);
+}
+
+int orx_env_step_ex(const orx_cfg_t* cfg, const orx_state_t* st, const void* actions,
+                    int32_t action_bytes, int32_t action_cols, int32_t policy_p2, int8_t* act,
+                    int32_t* obs, float* reward, uint8_t* done, int32_t* status,
+                    uint32_t* bad_actions, int64_t n_games, uint64_t seed, int64_t game_offset,
+                    void* stream) {
   int r;
   if ((r = check_cfg(cfg)) || (r = check_sizes(n_games, game_offset)) ||
       (r = check_policy(policy_p2)))
@@ -4468,13 +4750,16 @@ int orx_env_step(const orx_cfg_t* cfg, const orx_state_t* st, const void* action
   if (action_bytes != 1 && action_bytes != 2 && action_bytes != 4 && action_bytes != 8)
     return fail(ORX_EINVAL, "action_bytes must be 1, 2, 4 or 8");
   if (action_cols != 1 && action_cols != 2) return fail(ORX_EINVAL, "action_cols must be 1 or 2");
+  if (action_cols == 1 && policy_p2 == ORX_POLICY_NONE)
+    return fail(ORX_EINVAL, "action_cols 1 needs a policy for player 2 (ORX_POLICY_NONE: pass "
+                            "both players' actions, action_cols 2)");
   if (cfg->rng == ORX_RNG_MT19937)
     return fail(ORX_EINVAL, "orx_env_step: stock-seed mode draws the bots' moves from the "
                             "games' own streams; use orx_policy + orx_step");
   if (n_games == 0) return ORX_OK;
   if ((r = check_state(cfg, st, true))) return r;
   if (!actions || !act || !obs || !reward || !done)
-    return fail(ORX_EINVAL, "a pointer is NULL (only status may be)");
+    return fail(ORX_EINVAL, "a pointer is NULL (only status and bad_actions may be)");
   const uint32_t B = (uint32_t)n_games, off = (uint32_t)game_offset;
   const hipStream_t s = (hipStream_t)stream;
   const Key k = make_key(seed);
@@ -4484,13 +4769,10 @@ int orx_env_step(const orx_cfg_t* cfg, const orx_state_t* st, const void* action
   if (nc == N && grid == G && (cfg->flags == 0 || X)) {                                        \
     hipLaunchKernelGGL((env_step_kernel<N, G, X>), grid_for(B), dim3(kBlock), 0, s, *cfg, *st,   \
                        actions, action_bytes, action_cols, policy_p2, act, obs, reward, done,   \
-                       status, B, k, off);                                                      \
+                       status, bad_actions, B, k, off);                                         \
     return launch_status("orx_env_step");                                                      \
   }
-  ORX_ENV(0, false, false) ORX_ENV(8, false, false) ORX_ENV(16, false, false)
-  ORX_ENV(0, false, true) ORX_ENV(8, false, true) ORX_ENV(16, false, true)
-  ORX_ENV(kDense, false, true) ORX_ENV(0, true, true) ORX_ENV(8, true, true)
-  ORX_ENV(16, true, true) ORX_ENV(kDense, true, true)
+  ORX_ENV_LIST(ORX_ENV)
 #undef ORX_ENV
   return fail(ORX_EIO, "orx_env_step: no kernel instance for this configuration");
 }
@@ -4539,8 +4821,7 @@ int orx_rollout_ex(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p
   if (nc == N && grid == G)                                                                     \
     hipLaunchKernelGGL((mt_rollout_kernel<N, G>), grid_for(B), dim3(kBlock), 0, s, *cfg, *st,   \
                        policy_p1, policy_p2, n_ticks, obs, act, B, k, off, obs_format);
-    ORX_ROLLOUT(0, false) ORX_ROLLOUT(8, false) ORX_ROLLOUT(16, false) ORX_ROLLOUT(kDense, false)
-    ORX_ROLLOUT(0, true) ORX_ROLLOUT(8, true) ORX_ROLLOUT(16, true) ORX_ROLLOUT(kDense, true)
+    ORX_NG_LIST(ORX_ROLLOUT)
 #undef ORX_ROLLOUT
     return launch_status("orx_rollout");
   }
@@ -4549,23 +4830,58 @@ int orx_rollout_ex(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p
   // NPCs have compact instances; every other launch takes the generic form,
   // whose writer reads the format at run time
   if (cf && (pm == 3 || grid || nc == kDense)) pm = 0;
-  const RolloutPlan plan = plan_rollout(cfg, pm, B, (uint32_t)concurrency);
+  RolloutPlan plan = plan_rollout(cfg, pm, B, (uint32_t)concurrency);
+  // dynamic LDS: the bank's tiles when they fit the device's per-workgroup
+  // limit (160 KiB on gfx950, above 64 KiB with the opt-in raise)
+  const uint64_t tiles = grid ? (uint64_t)cfg->n_layouts * (uint64_t)(cfg->width * cfg->height) : 0;
+  uint32_t lds_n = (grid && bank_in_lds(cfg)) ? (uint32_t)tiles : 0u;
+  const uint32_t lds_max = device_lds_per_block();
+  // the paired form (two lanes per game, pair_rollout_kernel): K <= 16 NPCs
+  // in registers, a bank only with its tiles in LDS (the paired tick reads
+  // them nowhere else), the RandomBot / StaircaseBot / character trajectory
+  // forms, at most 32 games per wave (env ORX_ROLLOUT_PAIRED=0 turns it off)
+  if (plan.paired) {
+    if (grid && !lds_n) return fail(ORX_EIO, "orx_rollout: a paired bank launch without LDS tiles");
+    const uint32_t lanes = plan.lanes;
+    const uint32_t threads = pair_threads(cfg, lanes, lds_n);
+    const uint32_t per_block = threads / 64u * lanes;
+    const bool nt = plan.nt;
+    const dim3 blocks((B + per_block - 1) / per_block);
+    const bool sepd = pm == 2 && (cfg->flags & ORX_EXT_SEPARATION_DAMAGE) != 0;
+    // a refused limit raise (above the default 64 KiB) drops the launch to
+    // the one-lane form below with the tiles in global memory -- never a
+    // paired launch without them
+    bool refused = false;
+#define ORX_PAIR(N, P, A, S, C, G)                                                              \
+    if (nc == N && pm == P && (A == kStreamAux) == nt && S == sepd && C == cf && G == grid) {   \
+      auto* kfn = &pair_rollout_kernel<N, P, A, S, C, G>;                                       \
+      if (!raise_lds(reinterpret_cast<const void*>(kfn), lds_n)) {                              \
+        refused = true;                                                                         \
+      } else {                                                                                  \
+        hipLaunchKernelGGL(kfn, blocks, dim3(threads), lds_n, s, *cfg, *st, n_ticks, obs, act, B, \
+                           k, off, lanes, lds_n);                                               \
+        return launch_status("orx_rollout");                                                    \
+      }                                                                                         \
+    }
+    ORX_PAIR_LIST(ORX_PAIR)
+#undef ORX_PAIR
+    if (!refused) return fail(ORX_EIO, "orx_rollout: no paired kernel instance for this plan");
+    plan.paired = false;
+    plan.lanes = rollout_lanes(B);
+    plan.nt = plan.lanes * 4u >= 128u;
+    lds_n = 0u;
+  }
   const uint32_t lanes = plan.lanes;
   const uint32_t threads = rollout_threads(B, lanes);
   const uint32_t per_block = threads / 64u * lanes;
   const bool nt = plan.nt;
-  // dynamic LDS: the bank's tiles when they fit (rollout_kernel stages them)
-  const uint64_t tiles = grid ? (uint64_t)cfg->n_layouts * (uint64_t)(cfg->width * cfg->height) : 0;
-  const bool use_lds = grid && bank_in_lds(cfg);
-  const uint32_t lds_n = use_lds ? (uint32_t)tiles : 0u;
-  uint32_t lds = use_lds ? (uint32_t)((tiles + 15u) & ~15ull) : 0u;
+  uint32_t lds = (uint32_t)((lds_n + 15u) & ~15u);
   // dense NPCs: one occupancy bitmap per game of the block after the tiles,
   // when they fit the device's per-workgroup LDS (a workgroup may take all
   // 160 KiB on gfx950); the bitmaps are an optimization -- without them the
   // kernel reads the occupancy grid from HBM -- so a part with less LDS, or
   // a refused limit raise, launches without them instead of failing
   uint32_t lds_bits = 0;
-  const uint32_t lds_max = device_lds_per_block();
   if (nc == kDense && !getenv("ORX_NO_LDS_BITS")) {
     const uint32_t bb = (uint32_t)((cfg->width * cfg->height + 31) / 32) * 4u;
     if ((uint64_t)lds + (uint64_t)per_block * bb <= lds_max) {
@@ -4573,56 +4889,19 @@ int orx_rollout_ex(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p
       lds += per_block * bb;
     }
   }
-  // the paired form (two lanes per game, pair_rollout_kernel): no dense NPCs
-  // (K <= 16 in registers), no bank, the RandomBot or StaircaseBot trajectory
-  // forms, at most 32 games
-  // per wave (env ORX_ROLLOUT_PAIRED=0 turns it off, for measurements)
-  if (plan.paired) {
-    if (grid && !lds_n) return fail(ORX_EIO, "orx_rollout: a paired bank launch without LDS tiles");
-    const dim3 blocks((B + per_block - 1) / per_block);
-    const bool sepd = pm == 2 && (cfg->flags & ORX_EXT_SEPARATION_DAMAGE) != 0;
-    // dynamic LDS: a bank's tiles when they fit (lds_n); above the default
-    // 64 KiB the limit is raised, or the tiles stay in global memory
-#define ORX_PAIR(N, P, A, S, C, G)                                                              \
-    if (nc == N && pm == P && (A == kStreamAux) == nt && S == sepd && C == cf && G == grid) {   \
-      auto* kfn = &pair_rollout_kernel<N, P, A, S, C, G>;                                       \
-      uint32_t pn = lds_n;                                                                      \
-      if (pn > 65536u &&                                                                        \
-          hipFuncSetAttribute(reinterpret_cast<const void*>(kfn),                               \
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)pn) != hipSuccess) { \
-        (void)hipGetLastError();                                                                \
-        pn = 0u;                                                                                \
-      }                                                                                         \
-      hipLaunchKernelGGL(kfn, blocks, dim3(threads), pn, s, *cfg, *st, n_ticks, obs, act, B,    \
-                         k, off, lanes, pn);                                                    \
-      return launch_status("orx_rollout");                                                      \
-    }
-#define ORX_PAIRS_C(N, C)                                                                       \
-    ORX_PAIR(N, 1, kStreamAux, false, C, false) ORX_PAIR(N, 1, kPartialAux, false, C, false)    \
-    ORX_PAIR(N, 2, kStreamAux, false, C, false) ORX_PAIR(N, 2, kPartialAux, false, C, false)    \
-    ORX_PAIR(N, 2, kStreamAux, true, C, false) ORX_PAIR(N, 2, kPartialAux, true, C, false)
-#define ORX_PAIRS_G(N, G)                                                                       \
-    ORX_PAIR(N, 3, kStreamAux, false, false, G) ORX_PAIR(N, 3, kPartialAux, false, false, G)
-#define ORX_PAIRS(N)                                                                            \
-    ORX_PAIRS_C(N, false) ORX_PAIRS_C(N, true) ORX_PAIRS_G(N, false) ORX_PAIRS_G(N, true)        \
-    ORX_PAIR(N, 1, kStreamAux, false, false, true) ORX_PAIR(N, 1, kPartialAux, false, false, true) \
-    ORX_PAIR(N, 2, kStreamAux, false, false, true) ORX_PAIR(N, 2, kPartialAux, false, false, true)
-    ORX_PAIRS(0) ORX_PAIRS(8) ORX_PAIRS(16)
-#undef ORX_PAIRS_C
-#undef ORX_PAIRS_G
-#undef ORX_PAIRS
-#undef ORX_PAIR
-    return fail(ORX_EIO, "orx_rollout: no paired kernel instance for this plan");
-  }
+  // a refused limit raise: first without the bitmaps, then without the tiles
+  // (rollout_kernel reads a bank's tiles from global memory when lds_n is 0)
 #define ORX_ROLLOUT_AC(N, P, G, A, C)                                                           \
   if (nc == N && pm == P && grid == G && (P == 0 || (A == kStreamAux) == nt) &&                 \
       (P == 0 || C == cf)) {                                                                    \
-    if (lds > 65536u &&                                                                         \
-        hipFuncSetAttribute(reinterpret_cast<const void*>(&rollout_kernel<N, P, G, A, C>),      \
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) { \
-      (void)hipGetLastError();                                                                  \
-      if (lds_bits) { lds -= per_block * lds_bits; lds_bits = 0; }                              \
-      if (lds > 65536u) return fail(ORX_EIO, "orx_rollout: cannot raise the LDS limit");        \
+    const void* kfn = reinterpret_cast<const void*>(&rollout_kernel<N, P, G, A, C>);            \
+    if (!raise_lds(kfn, lds) && lds_bits) {                                                     \
+      lds -= per_block * lds_bits;                                                              \
+      lds_bits = 0;                                                                             \
+    }                                                                                           \
+    if (!raise_lds(kfn, lds)) {                                                                 \
+      lds_n = 0u;                                                                               \
+      lds = 0u;                                                                                 \
     }                                                                                           \
     hipLaunchKernelGGL((rollout_kernel<N, P, G, A, C>), dim3((B + per_block - 1) / per_block),  \
                        dim3(threads), lds, s, *cfg, *st,                                        \
@@ -4630,27 +4909,7 @@ int orx_rollout_ex(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p
                        lds_bits, obs_format);                                                   \
     return launch_status("orx_rollout");                                                        \
   }
-#define ORX_ROLLOUT_A(N, P, G, A) ORX_ROLLOUT_AC(N, P, G, A, false)
-// the buffer-store forms in both store policies (PM 1 / 2 without a bank also
-// in the compact format); the generic form (PM 0) in one, any format
-#define ORX_ROLLOUT(N, P, G)                                                                    \
-  ORX_ROLLOUT_A(N, P, G, kStreamAux)                                                            \
-  if (P != 0) { ORX_ROLLOUT_A(N, P, G, kPartialAux) }                                           \
-  if ((P == 1 || P == 2) && !G && N != kDense) {                                                \
-    ORX_ROLLOUT_AC(N, P, false, kStreamAux, true) ORX_ROLLOUT_AC(N, P, false, kPartialAux, true) \
-  }
-  ORX_ROLLOUT(0, 0, false) ORX_ROLLOUT(0, 1, false) ORX_ROLLOUT(0, 2, false)
-  ORX_ROLLOUT(8, 0, false) ORX_ROLLOUT(8, 1, false) ORX_ROLLOUT(8, 2, false)
-  ORX_ROLLOUT(16, 0, false) ORX_ROLLOUT(16, 1, false) ORX_ROLLOUT(16, 2, false)
-  ORX_ROLLOUT(0, 0, true) ORX_ROLLOUT(0, 1, true) ORX_ROLLOUT(0, 2, true)
-  ORX_ROLLOUT(8, 0, true) ORX_ROLLOUT(8, 1, true) ORX_ROLLOUT(8, 2, true)
-  ORX_ROLLOUT(16, 0, true) ORX_ROLLOUT(16, 1, true) ORX_ROLLOUT(16, 2, true)
-  ORX_ROLLOUT(0, 3, false) ORX_ROLLOUT(8, 3, false) ORX_ROLLOUT(16, 3, false)
-  ORX_ROLLOUT(0, 3, true) ORX_ROLLOUT(8, 3, true) ORX_ROLLOUT(16, 3, true)
-  ORX_ROLLOUT(kDense, 0, false) ORX_ROLLOUT(kDense, 1, false) ORX_ROLLOUT(kDense, 2, false)
-  ORX_ROLLOUT(kDense, 0, true) ORX_ROLLOUT(kDense, 1, true) ORX_ROLLOUT(kDense, 2, true)
-#undef ORX_ROLLOUT
-#undef ORX_ROLLOUT_A
+  ORX_ROLLOUT_LIST(ORX_ROLLOUT_AC)
 #undef ORX_ROLLOUT_AC
   return fail(ORX_EIO, "orx_rollout: no rollout kernel instance for this plan");
 }
@@ -4703,3 +4962,4 @@ int orx_dungeon_stairs(const orx_cfg_t* cfg, const uint32_t* game_ids, const int
 }
 
 }  // extern "C"
+#endif  // ORX_HOST_TU

@@ -52,6 +52,18 @@ def _ptr(t: Optional[torch.Tensor]):
     return None if t is None else ctypes.c_void_p(t.data_ptr())
 
 
+def cuda_device(device=None) -> torch.device:
+    """``device`` with its index made explicit (``"cuda"`` / None -> the current
+    device), so engines built with ``"cuda"`` and ``"cuda:0"`` compare equal and
+    share the shard streams."""
+    if device is None:
+        return torch.device("cuda", torch.cuda.current_device())
+    device = torch.device(device)
+    if device.type == "cuda" and device.index is None:
+        return torch.device("cuda", torch.cuda.current_device())
+    return device
+
+
 class BatchedEngine:
     """SoA state of ``n_games`` games and the launches that advance it.
 
@@ -68,9 +80,7 @@ class BatchedEngine:
         code = self.lib.orx_validate_cfg(ctypes.byref(self._ccfg))
         if code != 0:
             raise ValueError(self.lib.orx_last_error().decode())
-        if device is None:
-            device = torch.device("cuda", torch.cuda.current_device())
-        device = torch.device(device)
+        device = cuda_device(device)
         if device.type != "cuda":
             raise RuntimeError("BatchedEngine runs on a ROCm GPU only (no CPU path)")
         self.device = device
@@ -209,13 +219,15 @@ class BatchedEngine:
                       trajectory: bool = True) -> dict:
         """The shape orx_rollout launches these arguments with
         (orx_rollout_shape): games per wave, lanes per game (2 = the paired
-        form), nontemporal trajectory stores."""
+        form), nontemporal trajectory stores, threads per workgroup and
+        dynamic LDS bytes per workgroup (a bank's staged tiles)."""
         out = _lib.OrxRolloutShape()
         code = self.lib.orx_rollout_shape(self._pcfg, int(p1), int(p2), self.B, int(trajectory),
                                           int(self.concurrency), ctypes.byref(out))
         _lib.check("orx_rollout_shape", code)
         return {"games_per_wave": out.games_per_wave, "lanes_per_game": out.lanes_per_game,
-                "nontemporal": bool(out.nontemporal)}
+                "nontemporal": bool(out.nontemporal), "threads_per_block": out.threads_per_block,
+                "lds_bytes": out.lds_bytes}
 
     # -- the C-ABI entry points -------------------------------------------
     def seed_rng(self, seed: Optional[int] = None) -> None:
@@ -269,36 +281,61 @@ class BatchedEngine:
     _ACTION_BYTES = {torch.int8: 1, torch.int16: 2, torch.int32: 4, torch.int64: 8}
 
     def env_step(self, actions: torch.Tensor, p2: int, obs: torch.Tensor, reward: torch.Tensor,
-                 done: torch.Tensor, status: torch.Tensor) -> None:
-        """orx_env_step: one learner tick in one launch.  ``actions``: integer
-        [n_games] (player 1; player 2 moved by policy ``p2``) or [n_games, 2],
-        any integer width, contiguous, on the engine's device (values outside
-        the Move codes stop that game with STATUS_BAD_ACTION).  Writes the
-        pair played into ``self.actions``, then obs int32 [n_games, 14],
-        reward float32, done bool and status int32 [n_games]."""
+                 done: torch.Tensor, status: torch.Tensor,
+                 bad_actions: Optional[torch.Tensor] = None) -> None:
+        """orx_env_step_ex: one learner tick in one launch.  ``actions``:
+        integer [n_games] (player 1; player 2 moved by policy ``p2``, not
+        Policy.NONE) or [n_games, 2], any integer width, contiguous, on the
+        engine's device (values outside the Move codes stop that game with
+        STATUS_BAD_ACTION).  Writes the pair played into ``self.actions``,
+        then obs int32 [n_games, 14], reward float32, done bool and status
+        int32 [n_games]; ``bad_actions`` (int32 [1] on the device, or None)
+        is incremented by the number of games whose actions were refused."""
         nb = self._ACTION_BYTES.get(actions.dtype)
         if nb is None or tuple(actions.shape) not in ((self.B,), (self.B, 2)) \
                 or not actions.is_contiguous() or actions.device != self.device:
             raise ValueError(f"actions must be a contiguous integer [n_games] or [n_games, 2] "
                              f"tensor on {self.device}")
-        for t, dt, shape in ((obs, torch.int32, (self.B, len(OBS_FIELDS))),
-                             (reward, torch.float32, (self.B,)), (done, torch.bool, (self.B,)),
-                             (status, torch.int32, (self.B,))):
+        outs = [(obs, torch.int32, (self.B, len(OBS_FIELDS))), (reward, torch.float32, (self.B,)),
+                (done, torch.bool, (self.B,)), (status, torch.int32, (self.B,))]
+        if bad_actions is not None:
+            outs.append((bad_actions, torch.int32, (1,)))
+        for t, dt, shape in outs:
             if t.dtype != dt or tuple(t.shape) != shape or not t.is_contiguous() \
                     or t.device != self.device:
                 raise ValueError(f"env_step output must be a contiguous {dt} {shape} tensor")
-        self._env_step_raw(actions, nb, int(p2), obs, reward, done, status)
+        self._env_step_raw(actions, nb, int(p2), obs, reward, done, status, bad_actions)
 
-    def _env_step_raw(self, actions, nb, p2, obs, reward, done, status=None) -> None:
-        """orx_env_step on tensors already checked (VecEnv.step's own buffers):
-        one ctypes call; status may be None (it is obs[:, 9])."""
-        code = self.lib.orx_env_step(
+    def _env_step_raw(self, actions, nb, p2, obs, reward, done, status=None,
+                      bad_actions=None) -> None:
+        """orx_env_step_ex on tensors already checked: one ctypes call; status
+        and bad_actions may be None."""
+        code = self.lib.orx_env_step_ex(
             self._pcfg, self._pst, actions.data_ptr(), nb, actions.dim(), p2,
             self.actions.data_ptr(), obs.data_ptr(), reward.data_ptr(), done.data_ptr(),
-            None if status is None else status.data_ptr(), self.B, self.seed, self.game_offset,
-            torch.cuda.current_stream(self.device).cuda_stream)
+            None if status is None else status.data_ptr(),
+            None if bad_actions is None else bad_actions.data_ptr(), self.B, self.seed,
+            self.game_offset, torch.cuda.current_stream(self.device).cuda_stream)
         if code:
-            _lib.check("orx_env_step", code)
+            _lib.check("orx_env_step_ex", code)
+
+    def env_step_launcher(self, p2: int):
+        """A callable ``launch(actions, nb, cols, obs, reward, done, status, bad)``
+        -- orx_env_step_ex with every argument that does not change between
+        ticks bound once (VecEnv.step's eager path: one ctypes call, the
+        pointers as plain integers).  The caller has checked the tensors."""
+        fn, check = self.lib.orx_env_step_ex, _lib.check
+        pcfg, pst, act = self._pcfg, self._pst, self.actions.data_ptr()
+        B, seed, off, p2 = self.B, self.seed, self.game_offset, int(p2)
+        cur = torch.cuda.current_stream
+        dev = self.device
+
+        def launch(a_ptr, nb, cols, obs, rew, done, status, bad):
+            code = fn(pcfg, pst, a_ptr, nb, cols, p2, act, obs, rew, done, status, bad, B, seed,
+                      off, cur(dev).cuda_stream)
+            if code:
+                check("orx_env_step_ex", code)
+        return launch
 
     def policy(self, p1: int = Policy.Random, p2: int = Policy.Random,
                out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -559,7 +596,8 @@ _SHARD_STREAMS: dict = {}
 
 def shard_streams(device: torch.device, n: int) -> list:
     """The process's first ``n`` shard streams on ``device`` (created on first use)."""
-    have = _SHARD_STREAMS.setdefault(torch.device(device), [])
+    device = cuda_device(device)
+    have = _SHARD_STREAMS.setdefault(device, [])
     while len(have) < n:
         have.append(torch.cuda.Stream(device=device))
     return have[:n]
@@ -582,9 +620,7 @@ class StreamShardedEngine:
     def __init__(self, cfg: EnvConfig, n_games: int, seed: int = 0, game_offset: int = 0,
                  device: Optional[torch.device] = None, n_streams: int = 2):
         from .parallel import shard
-        if device is None:
-            device = torch.device("cuda", torch.cuda.current_device())
-        self.device = torch.device(device)
+        self.device = cuda_device(device)
         self.B = int(n_games)
         n_streams = max(1, min(int(n_streams), self.B))
         self.streams = shard_streams(self.device, n_streams)

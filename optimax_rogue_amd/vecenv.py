@@ -19,7 +19,7 @@ Player 2 is the learner's opponent: a device policy (``Policy.Random``,
 """
 from __future__ import annotations
 
-from typing import Optional
+from typing import Optional, Union
 
 import torch
 
@@ -31,20 +31,46 @@ _STATUS = OBS_FIELDS.index("status")
 
 
 class VecEnv:
+    """reset / step / rollout over one BatchedEngine.
+
+    ``check_actions`` -- what happens to actions outside the Move codes (e.g.
+    a 0-based argmax); the engine always stops such a game with
+    STATUS_BAD_ACTION (done, reward 0: a truncation; it restarts on the next
+    step):
+
+    * ``"deferred"`` (default): the launch also counts refused actions into a
+      device counter, and every ``check_every`` steps ``step`` reads it back
+      asynchronously (pinned memory and an event, no host sync); once a read
+      shows new refusals, a later ``step`` raises ValueError.  Detection lags
+      by at most two check periods; ``bad_actions()`` reads the count now
+      (synchronizing).
+    * ``True``: a host check before every launch raises ValueError at once
+      (a device-to-host sync per step).
+    * ``False``: no detection.
+
+    ``out_buffers`` -- 0 (default): every step returns fresh tensors; k > 0:
+    the outputs come from a ring of k preallocated sets, so a step's tensors
+    are overwritten k steps later (copy what must outlive that); this spares
+    four allocations per step on the eager path.
+    """
+
     def __init__(self, cfg: EnvConfig, n_games: int, seed: int = 0, game_offset: int = 0,
                  device: Optional[torch.device] = None,
-                 opponent: Optional[int] = Policy.Random, check_actions: bool = False):
+                 opponent: Optional[int] = Policy.Random,
+                 check_actions: Union[bool, str] = "deferred", out_buffers: int = 0,
+                 check_every: int = 64):
         if not int(cfg.autoreset):
             raise ValueError("VecEnv needs cfg.autoreset = 1 (finished games restart)")
+        if check_actions not in (True, False, "deferred"):
+            raise ValueError('check_actions must be True, False or "deferred"')
         self.engine = BatchedEngine(cfg, n_games, seed=seed, game_offset=game_offset,
                                     device=device)
         self.B = self.engine.B
         self.device = self.engine.device
         self.opponent = None if opponent is None else int(opponent)
-        # True: step() raises ValueError on a non-Move action (a host check, so
-        # every step synchronizes); False (default): the engine stops that game
-        # with STATUS_BAD_ACTION, which step() reports as done (a truncation)
-        self.check_actions = bool(check_actions)
+        self.check_actions = check_actions
+        self.check_every = max(1, int(check_every))
+        self.out_buffers = max(0, int(out_buffers))
         self._init_step_consts()
 
     def _init_step_consts(self) -> None:
@@ -53,6 +79,23 @@ class VecEnv:
         self._shape2 = torch.Size([self.B, 2])
         self._obs_shape = (self.B, len(OBS_FIELDS))
         self._p2 = int(Policy.NONE if self.opponent is None else self.opponent)
+        # refused-action counter (device) and its asynchronous read-back
+        self._bad_dev = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self._bad_host = torch.zeros(1, dtype=torch.int32).pin_memory() \
+            if self.check_actions == "deferred" else None
+        self._bad_event = None
+        self._bad_seen = 0
+        self._steps = 0
+        self._ring = [self._alloc_out() for _ in range(self.out_buffers)]
+        self._slot = 0
+        self._launch = None   # the pre-bound orx_env_step_ex, made at the first step
+
+    def _alloc_out(self):
+        d = self.device
+        return (torch.empty(self._obs_shape, dtype=torch.int32, device=d),
+                torch.empty(self.B, dtype=torch.float32, device=d),
+                torch.empty(self.B, dtype=torch.bool, device=d),
+                torch.empty(self.B, dtype=torch.int32, device=d))
 
     # -- observation -----------------------------------------------------------
     def observe(self) -> torch.Tensor:
@@ -75,6 +118,35 @@ class VecEnv:
                              - (after == UpdateResult.Player2Win).float(),
                              torch.zeros((), device=after.device))
         return reward, done
+
+    # -- refused actions ---------------------------------------------------------
+    def bad_actions(self) -> int:
+        """Games whose actions were refused (outside the Move codes) since this
+        VecEnv was made, by orx_env_step (synchronizes)."""
+        return int(self._bad_dev.item())
+
+    def _bad_message(self, n: int) -> str:
+        return (f"{n} game(s) got actions outside the Move values 1..{self._max_move()} (an "
+                "argmax over logits is 0-based: add 1); the engine stopped them with "
+                "STATUS_BAD_ACTION (done, reward 0)")
+
+    def _poll_bad(self) -> None:
+        """Deferred check: reads the counter's last asynchronous copy if it
+        has landed, raises on new refusals, and queues the next copy."""
+        if torch.cuda.is_current_stream_capturing():
+            return
+        ev = self._bad_event
+        if ev is not None:
+            if not ev.query():
+                return
+            n = int(self._bad_host[0])
+            self._bad_event = None
+            if n > self._bad_seen:
+                new, self._bad_seen = n - self._bad_seen, n
+                raise ValueError(self._bad_message(new))
+        self._bad_host.copy_(self._bad_dev, non_blocking=True)
+        self._bad_event = torch.cuda.Event()
+        self._bad_event.record()
 
     # -- reset / step / rollout ----------------------------------------------------
     def reset(self, mask: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -101,11 +173,11 @@ class VecEnv:
         (1..6 with EXT_HEAL), any integer dtype.  A value outside them (e.g. a
         0-based argmax) stops that game with STATUS_BAD_ACTION: it is done
         with reward 0 this step (a truncation) and restarts on the next one;
-        with ``check_actions=True`` it raises ValueError instead (a host check:
-        that step synchronizes).  One launch (orx_env_step) and no host sync
-        otherwise.  Returns (observation, reward, done, status), all fresh
-        tensors (status is the observation's status column, a view)."""
-        e = self.engine
+        ``check_actions`` decides whether and when ValueError is raised for
+        it (class docstring).  One launch (orx_env_step_ex) and no host sync
+        (unless check_actions=True).  Returns (observation int32 [n_games,
+        14], reward float32, done bool, status int32 [n_games]): separate
+        tensors, fresh ones unless ``out_buffers`` > 0."""
         shape = actions.shape
         if shape != self._shape1 and shape != self._shape2:   # no silent broadcasting
             raise ValueError(f"actions must be [n_games] or [n_games, 2], got {tuple(shape)}")
@@ -117,18 +189,30 @@ class VecEnv:
         a = actions if actions.device == self.device else actions.to(self.device)
         if not a.is_contiguous():
             a = a.contiguous()
-        if self.check_actions:
+        if self.check_actions is True:
             hi = self._max_move()
             if bool(((a < 1) | (a > hi)).any()):
                 raise ValueError(f"actions must be Move values 1..{hi} (an argmax over logits is "
                                  "0-based: add 1)")
-        if e.mt_py is not None:
-            return self._step_stock(a)
-        obs = torch.empty(self._obs_shape, dtype=torch.int32, device=self.device)
-        reward = torch.empty(self.B, dtype=torch.float32, device=self.device)
-        done = torch.empty(self.B, dtype=torch.bool, device=self.device)
-        e._env_step_raw(a, nb, self._p2, obs, reward, done)
-        return obs, reward, done, obs[:, _STATUS]
+        if self._launch is None:
+            if getattr(self.engine, "mt_py", None) is not None:   # stock-seed mode
+                return self._step_stock(a)
+            self._launch = self.engine.env_step_launcher(self._p2)
+        if self._ring:
+            out = self._ring[self._slot]
+            self._slot = (self._slot + 1) % len(self._ring)
+        else:
+            out = self._alloc_out()
+        obs, reward, done, status = out
+        deferred = self._bad_host is not None
+        self._launch(a.data_ptr(), nb, len(shape), obs.data_ptr(), reward.data_ptr(),
+                     done.data_ptr(), status.data_ptr(),
+                     self._bad_dev.data_ptr() if deferred else None)
+        if deferred:
+            self._steps += 1
+            if self._steps % self.check_every == 0:
+                self._poll_bad()
+        return obs, reward, done, status
 
     def _step_stock(self, a: torch.Tensor):
         """Stock-seed mode (the bots draw from each game's own MT19937 stream):
@@ -146,6 +230,12 @@ class VecEnv:
         before = e.status.clone()
         status = e.step(e.actions).clone()
         reward, done = self.outcome(before, status)
+        if self._bad_host is not None:   # the deferred check, counted with torch ops here
+            self._bad_dev += ((before == UpdateResult.InProgress)
+                              & (status == STATUS_BAD_ACTION)).sum(dtype=torch.int32)
+            self._steps += 1
+            if self._steps % self.check_every == 0:
+                self._poll_bad()
         return self.observe(), reward, done, status
 
     def rollout(self, n_ticks: int, p1: int = Policy.Random, p2: Optional[int] = None) -> dict:

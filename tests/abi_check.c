@@ -31,6 +31,16 @@ int main(void) {
                    NULL) != ORX_OK) { printf("empty env step failed\n"); return 9; }
   if (orx_env_step(&c, NULL, NULL, 3, 1, ORX_POLICY_RANDOM, NULL, NULL, NULL, NULL, NULL, 16, 1, 0,
                    NULL) != ORX_EINVAL) { printf("3-byte actions accepted\n"); return 10; }
+  /* ABI 6: the refused-action count; one action column needs a policy for player 2 */
+  if (orx_env_step_ex(&c, NULL, NULL, 8, 1, ORX_POLICY_RANDOM, NULL, NULL, NULL, NULL, NULL, NULL,
+                      0, 1, 0, NULL) != ORX_OK) { printf("empty env step ex failed\n"); return 13; }
+  if (orx_env_step_ex(&c, NULL, NULL, 8, 1, ORX_POLICY_NONE, NULL, NULL, NULL, NULL, NULL, NULL,
+                      16, 1, 0, NULL) != ORX_EINVAL) { printf("player 2 without a move accepted\n"); return 14; }
+  {
+    orx_rollout_shape_t sh;
+    if (orx_rollout_shape(&c, ORX_POLICY_RANDOM, ORX_POLICY_RANDOM, 65536, 1, 1, &sh) != ORX_OK ||
+        sh.threads_per_block <= 0 || sh.lds_bytes != 0) { printf("rollout shape failed\n"); return 15; }
+  }
   if (orx_rollout_ex(&c, NULL, ORX_POLICY_RANDOM, ORX_POLICY_RANDOM, 5, NULL, NULL, ORX_OBS_COMPACT,
                      0, 1, 0, 1, NULL) != ORX_OK) { printf("empty compact rollout failed\n"); return 11; }
   if (orx_rollout_ex(&c, NULL, ORX_POLICY_RANDOM, ORX_POLICY_RANDOM, 5, NULL, NULL, 7, 16, 1, 0, 1,

@@ -41,7 +41,7 @@ def test_library_exports_every_declared_symbol(lib):
                            "orx_dungeon_stairs", "orx_dungeon_spawn", "orx_seed_mt",
                            "orx_build_id", "orx_rollout_lanes", "orx_dstore_depths",
                            "orx_rollout_shape", "orx_rollout_concurrent", "orx_env_step",
-                           "orx_rollout_ex"])
+                           "orx_rollout_ex", "orx_env_step_ex"])
     from optimax_rogue_amd import _lib
     assert sorted(_lib.EXPORTS) == decl
     for name in decl:
@@ -216,8 +216,43 @@ def test_rollout_shape_rules(lib):
     assert shape(EnvConfig(width=12, height=10, flags=1, sep_period=2), 4096, 2, 2,
                  n_layouts=4)[1] == 1
     assert shape(EnvConfig(width=300, height=200), 4096, 2, 2)[1] == 1  # packed cells: <= 256
+    # round 5: C5's 131,072 games on one GPU as two 65,536-game stream shards
+    # pair at 32 games per wave (StaircaseBots; one launch stays one-lane)
+    assert shape(EnvConfig.c5(), 65536, 2, 2, conc=2) == (32, 2, 1)
+    assert shape(EnvConfig.c5(), 131072, 2, 2, conc=2)[1] == 1     # 8 waves per SIMD: no
+    assert shape(EnvConfig.c3(), 65536, conc=2) == (64, 1, 1)       # RandomBots: not measured
     bad = OrxRolloutShape()
     assert lib.orx_rollout_shape(ctypes.byref(EnvConfig.c2().to_c()), 9, 1, 64, 1, 1,
                                  ctypes.byref(bad)) == -22
     assert lib.orx_rollout_shape(ctypes.byref(EnvConfig.c2().to_c()), 1, 1, 64, 1, 0,
                                  ctypes.byref(bad)) == -22
+
+
+def test_rollout_shape_bank_lds(lib, monkeypatch):
+    """Round 5: a dungeon bank stays paired with its tiles in LDS up to the
+    device's per-workgroup limit (160 KiB on gfx950, assumed here without a
+    GPU); above half of it the paired workgroup is 512 threads (one per CU,
+    two waves per SIMD); a larger bank, or a refused limit raise
+    (ORX_REFUSE_LDS_RAISE=1), takes the one-lane form with its tiles in
+    global memory -- never a paired launch without them."""
+    from optimax_rogue_amd import EnvConfig
+    from optimax_rogue_amd._lib import OrxRolloutShape
+
+    def shape(n_layouts, B=32768, conc=2):
+        out = OrxRolloutShape()
+        c = EnvConfig.c3().to_c()
+        c.n_layouts = n_layouts
+        assert lib.orx_rollout_shape(ctypes.byref(c), 1, 1, B, 1, conc, ctypes.byref(out)) == 0
+        return (out.games_per_wave, out.lanes_per_game, out.threads_per_block, out.lds_bytes)
+
+    assert shape(16) == (32, 2, 256, 65536)        # the bench's bank: exactly 64 KiB
+    assert shape(20) == (32, 2, 256, 81920)        # two workgroups per CU still fit
+    assert shape(24) == (32, 2, 512, 98304)        # one per CU: 512 threads
+    assert shape(40) == (32, 2, 512, 163840)       # the whole 160 KiB
+    assert shape(41)[1:] == (1, 256, 0)            # too large: one lane, global tiles
+    monkeypatch.setenv("ORX_REFUSE_LDS_RAISE", "1")
+    assert shape(16) == (32, 2, 256, 65536)        # no raise needed
+    assert shape(24)[1:] == (1, 256, 0)            # refused: one lane, global tiles
+    monkeypatch.delenv("ORX_REFUSE_LDS_RAISE")
+    monkeypatch.setenv("ORX_ROLLOUT_THREADS", "256")
+    assert shape(24) == (32, 2, 256, 98304)        # the override (measurements)

@@ -420,3 +420,56 @@ def test_vecenv_bad_actions_truncate_on_device():
     strict = VecEnv(EnvConfig(width=10, height=10), 8, seed=2, device=dev, check_actions=True)
     with pytest.raises(ValueError, match="Move values"):
         strict.step(torch.tensor([1, 2, 3, 4, 5, 0, 1, 1], device=dev))
+
+
+def test_vecenv_deferred_bad_action_check():
+    """The default check_actions="deferred": refused actions are counted on
+    the device by orx_env_step_ex (no host sync) and a later step raises
+    ValueError once the asynchronous read-back shows them (within a few
+    check periods); correct actions never raise, and a caught error is not
+    raised again for the same refusals.  bad_actions() reads the count."""
+    import torch
+    from optimax_rogue_amd import EnvConfig, VecEnv
+    dev = torch.device("cuda", 0)
+    B = 256
+    env = VecEnv(EnvConfig(width=10, height=10, max_ticks=50), B, seed=5, device=dev,
+                 check_every=4)
+    good = torch.full((B,), 2, dtype=torch.int64, device=dev)
+    for _ in range(40):
+        env.step(good)
+    assert env.bad_actions() == 0
+    bad = good.clone()
+    bad[[1, 7, 200]] = 0                       # a 0-based argmax in three games
+    env.step(bad)
+    raised = 0
+    for _ in range(60):
+        try:
+            env.step(good)
+        except ValueError as e:
+            assert "3 game(s)" in str(e) and "0-based" in str(e)
+            raised += 1
+        torch.cuda.synchronize()
+    assert raised == 1
+    assert env.bad_actions() == 3
+
+
+def test_vecenv_out_buffers_ring():
+    """out_buffers=k: the same results as fresh tensors, from a ring of k
+    preallocated sets (step t's tensors are step t+k's)."""
+    import torch
+    from optimax_rogue_amd import EnvConfig, VecEnv
+    dev = torch.device("cuda", 0)
+    B = 1000
+    cfg = EnvConfig(width=8, height=8, n_npcs=3, max_ticks=30, player_health=3)
+    fresh = VecEnv(cfg, B, seed=8, device=dev)
+    ring = VecEnv(cfg, B, seed=8, device=dev, out_buffers=3)
+    g = torch.Generator(device="cpu").manual_seed(1)
+    ptrs = []
+    for t in range(20):
+        a = torch.randint(1, 6, (B,), generator=g).to(dev)
+        want = [x.clone() for x in fresh.step(a)]
+        got = ring.step(a)
+        for w, x in zip(want, got):
+            assert torch.equal(w, x), t
+        ptrs.append(got[0].data_ptr())
+    assert len(set(ptrs)) == 3 and ptrs[0] == ptrs[3] == ptrs[6]

@@ -484,19 +484,20 @@ def test_c3_full_size_properties(oracle_lib):
 
 
 def _timed_form_vs_oracle(oracle_lib, eng, parts, obs, act, launch, cfg, pol, seed, T, L,
-                          starts):
+                          starts, offset=0):
     """Runs ``launch`` (a pre-bound rollout launcher over ``parts``, each with
     its obs/act buffers) L times as bench.py issues it, and replays 8-game
-    windows of consecutive global ids starting at ``starts`` on the oracle
-    tick by tick: every tick's 14-field observation row and both actions of
-    every launch, and the whole state after each launch.  Returns the last
-    snapshot and the sampled global ids."""
+    windows of consecutive games starting at local index ``starts`` (global
+    id = ``offset`` + local) on the oracle tick by tick: every tick's
+    14-field observation row and both actions of every launch, and the whole
+    state after each launch.  Returns the last snapshot and the sampled
+    local indices."""
     import torch
     dev = parts[0].device
-    gids = np.concatenate([np.arange(s, s + 8) for s in starts])
+    gids = np.concatenate([np.arange(s, s + 8) for s in starts]) + offset
     oras = []
     for s in starts:
-        o = oracle_lib.Oracle(cfg.to_dict(), 8, seed, s)
+        o = oracle_lib.Oracle(cfg.to_dict(), 8, seed, s + offset, layouts=cfg.layouts)
         o.reset(episode=np.zeros(8, np.int32))
         oras.append(o)
     # per shard: which sampled ids it holds, at which local index
@@ -527,7 +528,7 @@ def _timed_form_vs_oracle(oracle_lib, eng, parts, obs, act, launch, cfg, pol, se
             assert np.array_equal(g_obs[:, :, cols], w_obs), f"{where}: observation rows"
             got = {k: v[..., s:s + 8] for k, v in snap.items()}
             compare_state(got, ora.export(), cfg.n_npcs, f"{where}: state")
-    return snap, gids
+    return snap, gids - offset
 
 
 def _window_starts(B, shard_size, n_random, seed):
@@ -540,33 +541,35 @@ def _window_starts(B, shard_size, n_random, seed):
     return sorted(set(ends) | {int(x) for x in rng.choice(pool, n_random, replace=False)})
 
 
-def test_bench_timed_path_vs_oracle(oracle_lib):
+@pytest.mark.parametrize("offset", [0, 458752])
+def test_bench_timed_path_vs_oracle(offset, oracle_lib):
     """bench.py's timed path exactly: StreamShardedEngine(C3, 65,536 games,
     seed 3, two stream shards of 32,768) launched through rollout_launcher
     with both trajectory buffers -- pair_rollout_kernel<8, 1, 2, false> (two
     lanes per game, register NPCs, RandomBots, nontemporal stores) at 32
     games per wave -- for 9 back-to-back 128-tick launches (1,152 ticks: every
     game crosses the max_ticks-1000 autoreset), as bench.py issues them (fork,
-    launches, join).  128 games -- 16 windows of 8 consecutive global ids,
-    including both ends of each shard -- are replayed on the oracle tick by
-    tick: every tick's 14-field observation row and both actions of every
-    launch, and the whole state after each launch."""
+    launches, join); at game offset 0 (rank 0) and 458,752 (rank 7 of C4's
+    eight 65,536-game ranks).  128 games -- 16 windows of 8 consecutive
+    global ids, including both ends of each shard -- are replayed on the
+    oracle tick by tick: every tick's 14-field observation row and both
+    actions of every launch, and the whole state after each launch."""
     import torch
     from optimax_rogue_amd import EnvConfig
     from optimax_rogue_amd.engine import StreamShardedEngine
     cfg = EnvConfig.c3()
     B, T, L, seed = 65536, 128, 9, 3
     dev = torch.device("cuda", 0)
-    eng = StreamShardedEngine(cfg, B, seed=seed, game_offset=0, device=dev, n_streams=2)
+    eng = StreamShardedEngine(cfg, B, seed=seed, game_offset=offset, device=dev, n_streams=2)
     assert [e.B for e in eng.parts] == [32768, 32768]
-    assert [e.game_offset for e in eng.parts] == [0, 32768]
-    assert eng.rollout_shape(1, 1) == {"games_per_wave": 32, "lanes_per_game": 2,
-                                       "nontemporal": True}   # the form bench.py times
+    assert [e.game_offset for e in eng.parts] == [offset, offset + 32768]
+    sh = eng.rollout_shape(1, 1)
+    assert (sh["games_per_wave"], sh["lanes_per_game"], sh["nontemporal"]) == (32, 2, True)
     obs, act = eng.trajectory_buffers(T)
     launch = eng.rollout_launcher(T, 1, 1, obs=obs, act=act)
     starts = _window_starts(B, 32768, 12, 7)
     snap, gids = _timed_form_vs_oracle(oracle_lib, eng, eng.parts, obs, act, launch, cfg,
-                                       (1, 1), seed, T, L, starts)
+                                       (1, 1), seed, T, L, starts, offset)
     # every sampled game went through the max_ticks autoreset in the timed form
     assert (snap["ep_count"][gids] >= 1).all() and (snap["episode"][gids] >= 1).all()
 
@@ -590,8 +593,8 @@ def test_bench_c5_share_stream_shards_vs_oracle(sep, oracle_lib):
     eng = StreamShardedEngine(cfg, B, seed=seed, game_offset=0, device=torch.device("cuda", 0),
                               n_streams=2)
     assert [e.B for e in eng.parts] == [8192, 8192]
-    assert eng.rollout_shape(2, 2) == {"games_per_wave": 8, "lanes_per_game": 2,
-                                       "nontemporal": False}
+    sh = eng.rollout_shape(2, 2)
+    assert (sh["games_per_wave"], sh["lanes_per_game"], sh["nontemporal"]) == (8, 2, False)
     obs, act = eng.trajectory_buffers(T)
     launch = eng.rollout_launcher(T, 2, 2, obs=obs, act=act)
     starts = _window_starts(B, 8192, 6, 17)
@@ -599,6 +602,126 @@ def test_bench_c5_share_stream_shards_vs_oracle(sep, oracle_lib):
                                        (2, 2), seed, T, L, starts)
     assert (snap["ep_count"][gids] >= 1).all()
     assert snap["counters"][1][gids].sum() > 100   # the StaircaseBots went deep
+
+
+# bench.py's sharded extras at their exact timed shapes (bench.extras:
+# rollout_rate(..., streams=2), seed 5): StreamShardedEngine over two stream
+# shards, 9 back-to-back 128-tick launches (fork, launches, join)
+SHARDED_EXTRAS = {
+    # the dungeon bank: 16 random 64x64 layouts (bench.py: DungeonBank.random(
+    # 64, 64, 16, seed=7)) = exactly 64 KiB of tiles staged in LDS, the
+    # paired pair_rollout_kernel<8, 1, 2, false, false, true> at 32 per wave
+    "bank": ("bank", 65536, 2, (1, 1), 65536),
+    # C3 with the character mechanics (EXT_RPG): pair_rollout_kernel<8, 3, ...>
+    "c3_rpg": ("c3_rpg", 65536, 2, (1, 1), 0),
+    # C5's 131,072 games on one GPU as two 65,536-game shards (round 5: the
+    # paired StaircaseBot form at 32 games per wave), separation damage off / on
+    "c5_131072_sep_off": ("c5", 131072, 2, (2, 2), 0),
+    "c5_131072_sep_on": ("c5sep", 131072, 2, (2, 2), 0),
+}
+
+
+def _extras_cfg(which):
+    from optimax_rogue_amd import DungeonBank, EnvConfig
+    from optimax_rogue_amd.enums import EXT_RPG, EXT_SEPARATION_DAMAGE
+    if which == "bank":
+        bank = DungeonBank.random(64, 64, 16, seed=7)
+        return EnvConfig(width=64, height=64, n_npcs=8, layouts=bank.layouts)
+    if which == "c3_rpg":
+        return EnvConfig(width=64, height=64, n_npcs=8, flags=EXT_RPG)
+    cfg = EnvConfig.c5()
+    if which == "c5sep":
+        cfg.flags, cfg.sep_period = EXT_SEPARATION_DAMAGE, 8
+    return cfg
+
+
+@pytest.mark.parametrize("name", sorted(SHARDED_EXTRAS))
+def test_bench_sharded_extras_vs_oracle(name, oracle_lib):
+    """The bench's two-stream-shard extras in the exact form they are timed:
+    the shape (two lanes per game, 32 games per wave, nontemporal stores,
+    256-thread workgroups, the bank's 65,536 B LDS stage -- the staging loop's
+    boundary), then 9 launches of 128 ticks with >= 64 sampled games (8-game
+    windows incl. both ends of each shard) replayed on the oracle: every
+    tick's observation row, both actions and the state after each launch
+    (worldgen.py:9-26, world.py:41-66 for the bank; readme.md:44-48,69-74 for
+    the character mechanics, parity unpinned; staircasebot.py:9-21)."""
+    import torch
+    from optimax_rogue_amd.engine import StreamShardedEngine
+    which, B, streams, pol, lds = SHARDED_EXTRAS[name]
+    cfg = _extras_cfg(which)
+    T, L, seed = 128, 9, 5
+    eng = StreamShardedEngine(cfg, B, seed=seed, game_offset=0, device=torch.device("cuda", 0),
+                              n_streams=streams)
+    sh = eng.rollout_shape(*pol)
+    assert (sh["games_per_wave"], sh["lanes_per_game"], sh["nontemporal"],
+            sh["threads_per_block"], sh["lds_bytes"]) == (32, 2, True, 256, lds), sh
+    obs, act = eng.trajectory_buffers(T)
+    launch = eng.rollout_launcher(T, *pol, obs=obs, act=act)
+    starts = _window_starts(B, B // streams, 6, 13)
+    snap, gids = _timed_form_vs_oracle(oracle_lib, eng, eng.parts, obs, act, launch, cfg, pol,
+                                       seed, T, L, starts)
+    assert len(gids) >= 64
+    assert (snap["ep_count"][gids] >= 1).all()
+    if which.startswith("c5"):
+        assert snap["counters"][1][gids].sum() > 100   # the StaircaseBots went deep
+    else:
+        assert snap["counters"][0][gids].sum() > 0     # combats happened
+
+
+# round 5: banks above the default 64 KiB of LDS stay paired with the tiles
+# staged (the kernel's limit raised; 512-thread workgroups above half the
+# LDS), and a refused raise takes the one-lane form with global tiles
+BIG_BANKS = {
+    # 24 x 64x64 = 96 KiB: 512 threads; RandomBots with NPCs, StaircaseBots
+    "bank96_random_npcs": (dict(width=64, height=64, n_npcs=8, max_ticks=120), (1, 1), 24, None,
+                           (2, 512, 98304)),
+    "bank96_stairs": (dict(width=64, height=64, max_ticks=150, despawn=2), (2, 2), 24, None,
+                      (2, 512, 98304)),
+    # 20 x 64x64 = 80 KiB: two workgroups per CU, 256 threads
+    "bank80_random": (dict(width=64, height=64, n_npcs=4, max_ticks=100), (1, 1), 20, None,
+                      (2, 256, 81920)),
+    # 40 x 64x64 = the whole 160 KiB
+    "bank160_random": (dict(width=64, height=64, n_npcs=8, max_ticks=100), (1, 1), 40, None,
+                       (2, 512, 163840)),
+    # the refused raise (forced): one lane per game, tiles read from global memory
+    "bank96_refused": (dict(width=64, height=64, n_npcs=8, max_ticks=100), (1, 1), 24,
+                       {"ORX_REFUSE_LDS_RAISE": "1"}, (1, 256, 0)),
+    # the 512-thread choice overridden: 256-thread workgroups, one per CU
+    "bank96_threads256": (dict(width=64, height=64, n_npcs=8, max_ticks=100), (1, 1), 24,
+                          {"ORX_ROLLOUT_THREADS": "256"}, (2, 256, 98304)),
+}
+
+
+@pytest.mark.parametrize("name", sorted(BIG_BANKS))
+def test_big_bank_forms_vs_oracle(name, oracle_lib, monkeypatch):
+    """Dungeon banks of 80-160 KiB: the launch form (lanes per game, threads
+    per workgroup, LDS bytes) and 4 x 40-tick rollouts of 2,048 games against
+    the oracle's literal tile model (rows, actions, state; worldgen.py:9-26,
+    world.py:41-66)."""
+    import torch
+    from optimax_rogue_amd.enums import OBS_FIELDS
+    cfg, pol, L, env, want_shape = BIG_BANKS[name]
+    for k, v in (env or {}).items():
+        monkeypatch.setenv(k, v)
+    lay = _bank(64, 64, L, 90 + L, (1, 2))
+    B, seed, T = 2048, 91, 40
+    ora = oracle_lib.Oracle(cfg, B, seed, 3, layouts=lay)
+    ora.reset(episode=np.zeros(B, np.int32))
+    eng = _engine(cfg, B, seed, 3, layouts=lay)
+    sh = eng.rollout_shape(*pol)
+    assert (sh["lanes_per_game"], sh["threads_per_block"], sh["lds_bytes"]) == want_shape, sh
+    obs = torch.zeros((T, len(OBS_FIELDS), B), dtype=torch.int32, device=eng.device)
+    act = torch.zeros((T, B, 2), dtype=torch.int8, device=eng.device)
+    for launch in range(4):
+        want_act, want_obs = _replay(ora, T, pol)
+        eng.rollout(T, *pol, obs=obs, act=act)
+        compare_state(eng.snapshot(), ora.export(), ora.K, f"{name} launch {launch}")
+        assert np.array_equal(act.cpu().numpy(), want_act), f"{name} actions {launch}"
+        assert np.array_equal(obs.cpu().numpy(), want_obs), f"{name} obs {launch}"
+    s = eng.snapshot()
+    assert int(s["episode"].sum()) > 0 or pol == (2, 2)
+    assert s["counters"][1].sum() > 0 or pol == (1, 1)   # StaircaseBots descended
+    torch.cuda.synchronize()
 
 
 # bench.py's extras at their timed shapes (bench.extras: rollout_rate, seed 5,

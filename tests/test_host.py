@@ -29,6 +29,7 @@ def test_vecenv_step_rejects_non_moves(bad):
     env = VecEnv.__new__(VecEnv)
     env.engine = _bare_engine(EnvConfig(), 3)
     env.B, env.device, env.opponent, env.check_actions = 3, torch.device("cpu"), 1, True
+    env.check_every, env.out_buffers = 64, 0
     env._init_step_consts()
     with pytest.raises(ValueError, match="Move values"):
         env.step(torch.tensor(bad, dtype=torch.int32))
@@ -113,12 +114,15 @@ def test_engine_refuses_snapshots_off_the_grid():
 
 
 @pytest.mark.parametrize("bad", [[0, 1, 2], [1, 2, 257], [-1, 2, 3]])
-def test_vecenv_step_passes_bad_actions_to_the_engine(bad):
-    """check_actions=False (the default): no host check and no sync -- the
-    learner's tensor goes to orx_env_step as it is (full width: 257 is not
-    cast to int8, where it would wrap to a legal 1); the engine stops those
-    games with STATUS_BAD_ACTION and step() reports them done (GPU tests:
-    test_vecenv_bad_actions_truncate_on_device)."""
+@pytest.mark.parametrize("ring", [0, 2])
+def test_vecenv_step_passes_bad_actions_to_the_engine(bad, ring):
+    """check_actions=False: no host check and no sync -- the learner's tensor
+    goes to orx_env_step_ex as it is (its own pointer at full width: 257 is
+    not cast to int8, where it would wrap to a legal 1); the engine stops
+    those games with STATUS_BAD_ACTION and step() reports them done (GPU
+    tests: test_vecenv_bad_actions_truncate_on_device).  Status is its own
+    tensor (not a view of the observation); with out_buffers=k the outputs
+    come from a ring of k sets."""
     import torch
     from optimax_rogue_amd import EnvConfig
     from optimax_rogue_amd.vecenv import VecEnv
@@ -127,18 +131,28 @@ def test_vecenv_step_passes_bad_actions_to_the_engine(bad):
     class Eng:
         cfg, mt_py = EnvConfig(), None
 
-        def _env_step_raw(self, a, nb, p2, obs, reward, done, status=None):
-            calls.append((a.clone(), nb, p2, obs.shape, obs.dtype, reward.dtype, done.dtype))
+        def env_step_launcher(self, p2):
+            def launch(a_ptr, nb, cols, obs, rew, done, status, bad_ptr):
+                calls.append((a_ptr, nb, cols, p2, obs, rew, done, status, bad_ptr))
+            return launch
 
     env = VecEnv.__new__(VecEnv)
     env.engine, env.check_actions = Eng(), False
     env.B, env.device, env.opponent = 3, torch.device("cpu"), 2
+    env.check_every, env.out_buffers = 64, ring
     env._init_step_consts()
-    obs, reward, done, status = env.step(torch.tensor(bad, dtype=torch.int64))
-    a, nb, p2, shape, od, rd, dd = calls[0]
-    assert a.dtype == torch.int64 and a.tolist() == bad and nb == 8 and p2 == 2
-    assert shape == (3, 14) and od == torch.int32 and rd == torch.float32 and dd == torch.bool
-    assert status.data_ptr() == obs[:, 9].data_ptr()   # the observation's status column
+    a = torch.tensor(bad, dtype=torch.int64)
+    outs = [env.step(a) for _ in range(3)]
+    a_ptr, nb, cols, p2, optr, rptr, dptr, sptr, bptr = calls[0]
+    assert a_ptr == a.data_ptr() and nb == 8 and cols == 1 and p2 == 2 and bptr is None
+    obs, reward, done, status = outs[0]
+    assert (optr, rptr, dptr, sptr) == (obs.data_ptr(), reward.data_ptr(), done.data_ptr(),
+                                        status.data_ptr())
+    assert obs.shape == (3, 14) and obs.dtype == torch.int32 and reward.dtype == torch.float32
+    assert done.dtype == torch.bool and status.dtype == torch.int32 and status.shape == (3,)
+    assert status.data_ptr() != obs[:, 9].data_ptr()
+    same = outs[2][0].data_ptr() == outs[0][0].data_ptr()
+    assert same == (ring == 2)   # the ring of two comes round on the third step
     with pytest.raises(ValueError, match="integer"):
         env.step(torch.tensor([1.0, 2.0, 3.0]))
 
