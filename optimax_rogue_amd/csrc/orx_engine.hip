@@ -2135,14 +2135,19 @@ __global__ void __launch_bounds__(256) policy_kernel(orx_state_t st, int32_t pol
 // tick; an engine stop code >= 16 is a truncation) -- VecEnv.outcome on
 // device, no host sync.  Every state word is loaded once up front and the
 // row comes from registers (step_game's output callback): one HBM round trip
-// per launch.  bad_count (may be NULL): += the games whose actions were
-// refused this tick (one atomic per wave that has any).
+// per launch.  The rows [B][14] are written through LDS (lds_rows): each
+// thread parks its 14 words, and the workgroup then stores its 256 rows as
+// one contiguous 14 KiB run, every store instruction a full 256-byte
+// segment -- written directly, a lane's 14 stores land 56 B apart and each
+// instruction touches 28 cache lines.  bad_count (may be NULL): += the games
+// whose actions were refused this tick (one atomic per wave that has any).
 template <int NCAP, bool GRID, bool EXT>
 __global__ void __launch_bounds__(256) env_step_kernel(
     orx_cfg_t hc, orx_state_t st, const void* __restrict__ actions, int32_t dsize, int32_t cols,
     int32_t pol2, int8_t* __restrict__ act, int32_t* __restrict__ obs, float* __restrict__ reward,
     uint8_t* __restrict__ done, int32_t* __restrict__ status_out, uint32_t* __restrict__ bad_count,
-    uint32_t B, Key key, uint32_t off) {
+    uint32_t B, Key key, uint32_t off, int32_t lds_rows) {
+  __shared__ int32_t rows_lds[256 * ORX_OBS_FIELDS];
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const bool live = i < B;
   bool bad = false;
@@ -2176,8 +2181,14 @@ __global__ void __launch_bounds__(256) env_step_kernel(
     auto out = [&](const Player& p1, const Player& p2, int32_t tick, int32_t after) {
       const int32_t row[ORX_OBS_FIELDS] = {p1.x, p1.y, p1.d, p1.hp, p2.x, p2.y, p2.d, p2.hp,
                                            tick, after, p1.sx, p1.sy, p2.sx, p2.sy};
+      if (lds_rows) {  // (uniform)
 #pragma unroll
-      for (int f = 0; f < ORX_OBS_FIELDS; ++f) obs[(size_t)i * ORX_OBS_FIELDS + f] = row[f];
+        for (int f = 0; f < ORX_OBS_FIELDS; ++f)
+          rows_lds[threadIdx.x * ORX_OBS_FIELDS + f] = row[f];
+      } else {
+#pragma unroll
+        for (int f = 0; f < ORX_OBS_FIELDS; ++f) obs[(size_t)i * ORX_OBS_FIELDS + f] = row[f];
+      }
       const bool ended = before == ORX_IN_PROGRESS && after >= ORX_PLAYER1_WIN &&
                          (after <= ORX_TIE || after >= ORX_STATUS_BAD_ACTION);
       done[i] = ended ? 1 : 0;
@@ -2189,6 +2200,17 @@ __global__ void __launch_bounds__(256) env_step_kernel(
     before = st.status[i];
     step_game<NCAP, false, GRID, EXT>(hc, st, get_action, B, i, key, off, nullptr, nullptr, out);
     reinterpret_cast<uint16_t*>(act)[i] = pair;
+  }
+  if (lds_rows) {  // the workgroup's rows as one contiguous run (uniform)
+    __syncthreads();
+    const uint32_t g0 = blockIdx.x * blockDim.x;
+    const uint32_t n = (min(B - g0, (uint32_t)blockDim.x)) * ORX_OBS_FIELDS;
+    int32_t* base = obs + (size_t)g0 * ORX_OBS_FIELDS;
+#pragma unroll
+    for (int k = 0; k < ORX_OBS_FIELDS; ++k) {
+      const uint32_t j = (uint32_t)k * blockDim.x + threadIdx.x;
+      if (j < n) base[j] = rows_lds[j];
+    }
   }
   if (bad_count) {  // uniform
     const uint64_t m = __builtin_amdgcn_ballot_w64(bad);
@@ -3510,10 +3532,12 @@ __global__ void __launch_bounds__(GRID ? 512 : kRolloutBlock) ORX_PAIR_ATTR pair
 #endif
         }
       }
-      if constexpr (PM == 1) {
+      if constexpr (PM == 1 || PM == 3) {
         // a meet without a staircase or an NPC hit: rare_tick's lean meet,
         // the two moves in the drawn order (the tick block's word a; an
-        // all-reject word takes the ordered tick), from each lane's side
+        // all-reject word takes the ordered tick), from each lane's side;
+        // PM 3: each attacker's own damage and mana (rpg_attack), no item
+        // underfoot (an item rides in an NPC slot, so hit_me / hit_o cover it)
         const uint32_t sa = ~(tb.a >> 1) & 0x55555555u;
         if (in_progress & meet & !st_me & (st_o == 0) & !hit_me & (hit_o == 0) & (sa != 0u)) {
           const bool p1_first = ((tb.a >> __builtin_ctz(sa)) & 1u) != 0;
@@ -3527,8 +3551,14 @@ __global__ void __launch_bounds__(GRID ? 512 : kRolloutBlock) ORX_PAIR_ATTR pair
           const bool occs = (bx == fx) & (by == fy);    // the second attacks the first
           me.x = me_first ? fx : (occs ? sx0 : bx);
           me.y = me_first ? fy : (occs ? sy0 : by);
-          const int32_t dmg = c.player_dmg_net > 0 ? c.player_dmg_net : 0;
-          me.hp -= (me_first ? occs : occf) ? dmg : 0;
+          if constexpr (PM == 3) {  // my attack spends my mana; the other's hits me
+            const bool i_attack = me_first ? occf : occs;
+            const int32_t d_me = i_attack ? rpg_attack(c, me) : 0;
+            me.hp -= pair_swap(d_me);
+          } else {
+            const int32_t dmg = c.player_dmg_net > 0 ? c.player_dmg_net : 0;
+            me.hp -= (me_first ? occs : occf) ? dmg : 0;
+          }
           dl.combat += (occf ? 1 : 0) + (occs ? 1 : 0);
           dl.eps += end ? 1 : 0;
           tick = ft;
@@ -4136,7 +4166,7 @@ __global__ void __launch_bounds__(256) stairs_kernel(orx_cfg_t hc, orx_state_t s
 #define ORX_I_ENV(N, G, X)                                                                      \
   ORX_INST template __global__ void env_step_kernel<N, G, X>(                                   \
       orx_cfg_t, orx_state_t, const void*, int32_t, int32_t, int32_t, int8_t*, int32_t*, float*, \
-      uint8_t*, int32_t*, uint32_t*, uint32_t, Key, uint32_t);
+      uint8_t*, int32_t*, uint32_t*, uint32_t, Key, uint32_t, int32_t);
 #define ORX_I_PAIR(N, P, A, S, C, G)                                                            \
   ORX_INST template __global__ void pair_rollout_kernel<N, P, A, S, C, G>(                      \
       orx_cfg_t, orx_state_t, int32_t, int32_t*, int8_t*, uint32_t, Key, uint32_t, uint32_t,     \
@@ -4765,11 +4795,14 @@ int orx_env_step_ex(const orx_cfg_t* cfg, const orx_state_t* st, const void* act
   const Key k = make_key(seed);
   const int nc = ncap_for(cfg->n_npcs);
   const bool grid = cfg->n_layouts > 0;
+  // the rows through LDS (env ORX_ENV_DIRECT_ROWS=1: direct stores, for measurements)
+  const char* dr = getenv("ORX_ENV_DIRECT_ROWS");
+  const int32_t lds_rows = (dr && dr[0] == '1') ? 0 : 1;
 #define ORX_ENV(N, G, X)                                                                        \
   if (nc == N && grid == G && (cfg->flags == 0 || X)) {                                        \
     hipLaunchKernelGGL((env_step_kernel<N, G, X>), grid_for(B), dim3(kBlock), 0, s, *cfg, *st,   \
                        actions, action_bytes, action_cols, policy_p2, act, obs, reward, done,   \
-                       status, bad_actions, B, k, off);                                         \
+                       status, bad_actions, B, k, off, lds_rows);                               \
     return launch_status("orx_env_step");                                                      \
   }
   ORX_ENV_LIST(ORX_ENV)

@@ -484,14 +484,15 @@ def test_c3_full_size_properties(oracle_lib):
 
 
 def _timed_form_vs_oracle(oracle_lib, eng, parts, obs, act, launch, cfg, pol, seed, T, L,
-                          starts, offset=0):
+                          starts, offset=0, compact=False):
     """Runs ``launch`` (a pre-bound rollout launcher over ``parts``, each with
     its obs/act buffers) L times as bench.py issues it, and replays 8-game
     windows of consecutive games starting at local index ``starts`` (global
     id = ``offset`` + local) on the oracle tick by tick: every tick's
     14-field observation row and both actions of every launch, and the whole
-    state after each launch.  Returns the last snapshot and the sampled
-    local indices."""
+    state after each launch (``compact``: the launch writes ORX_OBS_COMPACT
+    rows, decoded before the comparison).  Returns the last snapshot and the
+    sampled local indices."""
     import torch
     dev = parts[0].device
     gids = np.concatenate([np.arange(s, s + 8) for s in starts]) + offset
@@ -517,7 +518,11 @@ def _timed_form_vs_oracle(oracle_lib, eng, parts, obs, act, launch, cfg, pol, se
         g_obs = np.zeros((T, 14, len(gids)), np.int32)
         g_act = np.zeros((T, len(gids), 2), np.int8)
         for (pos, li), o, a in zip(sel, obs, act):
-            g_obs[:, :, pos] = o.index_select(2, li).cpu().numpy()
+            rows = o.index_select(2, li)
+            if compact:
+                from optimax_rogue_amd.engine import decode_compact
+                rows = decode_compact(rows)
+            g_obs[:, :, pos] = rows.cpu().numpy()
             g_act[:, pos] = a.index_select(1, li).cpu().numpy()
         snap = eng.snapshot()
         for w, (s, ora) in enumerate(zip(starts, oras)):
@@ -1026,6 +1031,32 @@ COMPACT_FORMS = {
     "dense_generic": (dict(width=12, height=12, n_npcs=30, max_ticks=60), (1, 2), 2048, 1, 1),
     "stock_mt": (dict(width=10, height=9, n_npcs=4, max_ticks=60, rng=1), (1, 2), 1024, 1, 1),
 }
+
+
+@pytest.mark.parametrize("name", sorted(COMPACT_FORMS))
+def test_compact_rows_vs_oracle(name, oracle_lib):
+    """Round 5: every compact-row launch form against the oracle first hand
+    (not only against the engine's own int32 rows): 3 launches, sampled
+    8-game windows (both ends of each shard) replayed tick by tick -- the
+    decoded rows, both actions and the state after each launch."""
+    import torch
+    from optimax_rogue_amd import DungeonBank, EnvConfig
+    from optimax_rogue_amd.engine import StreamShardedEngine
+    from optimax_rogue_amd.enums import OBS_COMPACT
+    cfgd, pol, B, streams, lanes = COMPACT_FORMS[name]
+    layouts = DungeonBank.random(20, 16, 6, seed=3, n_stairs=2).layouts \
+        if name == "bank_generic" else None
+    cfg = EnvConfig.from_dict(cfgd, layouts=layouts)
+    T, L, seed, off = (64 if B >= 65536 else 100), 3, 21, 3
+    eng = StreamShardedEngine(cfg, B, seed=seed, game_offset=off, device=torch.device("cuda", 0),
+                              n_streams=streams)
+    if name != "stock_mt":
+        assert eng.rollout_shape(*pol)["lanes_per_game"] == lanes, name
+    obs, act = eng.trajectory_buffers(T, OBS_COMPACT)
+    launch = eng.rollout_launcher(T, *pol, obs=obs, act=act, obs_format=OBS_COMPACT)
+    starts = _window_starts(B - B % 8, max(8, (B // streams) // 8 * 8), 4, 29)
+    _timed_form_vs_oracle(oracle_lib, eng, eng.parts, obs, act, launch, cfg, pol, seed, T, L,
+                          starts, off, compact=True)
 
 
 @pytest.mark.parametrize("name", sorted(COMPACT_FORMS))

@@ -67,6 +67,8 @@ def main():
                     torch.cuda.empty_cache()
         os.environ.pop("ORX_ROLLOUT_LANES", None)
     if "env" in which:
+      for direct in ("0", "1", "0"):   # rows through LDS (the default) / direct stores
+        os.environ["ORX_ENV_DIRECT_ROWS"] = direct
         for B in (65536, 1 << 21):
             cfg = EnvConfig.c3()
             eng = BatchedEngine(cfg, B, seed=3, device=dev)
@@ -86,7 +88,8 @@ def main():
                 evs.append((a, b))
             torch.cuda.synchronize()
             d = sorted(a.elapsed_time(b) * 1e3 for a, b in evs)
-            print(json.dumps({"env_step_games": B, "us_median": round(d[len(d) // 2], 2),
+            print(json.dumps({"env_step_games": B, "direct_rows": direct,
+                              "us_median": round(d[len(d) // 2], 2),
                               "us_min": round(d[0], 2)}), flush=True)
             del eng, acts, obs, rew, done, stat
             torch.cuda.empty_cache()

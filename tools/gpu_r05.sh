@@ -1,0 +1,41 @@
+#!/bin/bash
+# One GPU call (round 5): the GPU test suite, the bench command, the
+# character-mechanics stamps at the bench's shard shape and the dungeon-bank
+# forms A/B.  Each step is time-limited; a fault, abort or time-out (exit
+# 124 / 134 / 137 / 139) ends the call, a failing test or tool does not.
+#   gpurun --timeout 1500 -- bash tools/gpu_r05.sh <tag> [steps...]
+TAG=${1:?tag}; shift
+STEPS=${*:-"pytest bench stamps banks env"}
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/$TAG
+mkdir -p $O
+cd $R
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+fatal() { case $1 in 124|134|137|139) echo "step $2 ended with $1: stopping"; exit $1;; esac; }
+for s in $STEPS; do
+  case $s in
+    pytest)
+      timeout -k 10 900 python3 -u -m pytest tests -m gpu -q --maxfail=10 --timeout 300 \
+        --timeout-method thread > $O/pytest.log 2>&1
+      rc=$?; echo "pytest rc=$rc"; tail -25 $O/pytest.log; fatal $rc pytest;;
+    bench)
+      timeout -k 10 420 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err
+      rc=$?; echo "bench rc=$rc"; cut -c1-300 $O/bench.json; fatal $rc bench;;
+    stamps)
+      for c in c3_rpg c3; do
+        ORX_ROLLOUT_LANES=32 STAMPS_CFG=$c timeout -k 10 120 python3 tools/stamps.py \
+          tools/ab_libs/stamps.so 32768 128 > $O/stamps_${c}_32768.json 2> $O/stamps_$c.err
+        rc=$?; echo "stamps $c rc=$rc"; fatal $rc stamps
+      done;;
+    banks)
+      timeout -k 10 400 python3 tools/bank_forms.py > $O/bank_forms.jsonl 2> $O/bank_forms.err
+      rc=$?; echo "banks rc=$rc"; fatal $rc banks;;
+    env)
+      C5_FORMS=env timeout -k 10 300 python3 tools/c5_forms.py > $O/env_forms.jsonl 2> $O/env_forms.err
+      rc=$?; echo "env rc=$rc"; fatal $rc env;;
+    c5)
+      timeout -k 10 400 python3 tools/c5_forms.py > $O/c5_forms.jsonl 2> $O/c5_forms.err
+      rc=$?; echo "c5 rc=$rc"; fatal $rc c5;;
+  esac
+done
+exit 0
