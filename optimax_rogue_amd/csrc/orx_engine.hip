@@ -1025,6 +1025,42 @@ __device__ __forceinline__ void setup_game(const Cfg& c, Key key, Src& src, Play
       }
     }
   }
+  if constexpr (!Src::kMt && !GRID && NCAP > 0 && NCAP != kDense) {
+    // the register NPCs from the INIT stream's first twelve words as straight
+    // selects (the loop below takes the same words one at a time, drawing a
+    // block at every fourth behind a branch): blocks 1 and 2 drawn side by
+    // side, each word placing the next NPC unless it is rejected or its cell
+    // is taken; the loop resumes at word 12 when fewer than K were placed
+    // (~4% of games at 64x64).  An episode start (C3's synchronized resets,
+    // the character mechanics' deaths) pays a third of the loop's cost.
+    if (placed == 2 && placed < total) {
+      W4 b1 = philox(src.game, src.ep, 0u, tag(PUR_INIT, 0) | 1u, key);
+      W4 b2 = philox(src.game, src.ep, 0u, tag(PUR_INIT, 0) | 2u, key);
+      launder_w4(b1);
+      launder_w4(b2);
+      const W4 w0 = s.w;  // block 0 (the players' words)
+      const bool p2_here = p2.d == p1.d;
+#pragma unroll
+      for (uint32_t j = 0; j < 12; ++j) {
+        const W4& b = j < 4 ? w0 : j < 8 ? b1 : b2;
+        const uint32_t k = j & 3u;
+        const uint32_t word = k == 0 ? b.a : k == 1 ? b.b : k == 2 ? b.c : b.d;
+        const uint32_t v = word & g1.mask;
+        int32_t x, y;
+        ground_cell<false>(c, v, -1, p1.sx, p1.sy, x, y);
+        const uint32_t cell = pack_xy(x, y);
+        const bool occ = (x == p1.x && y == p1.y) || (p2_here && x == p2.x && y == p2.y) ||
+                         npc.any(cell);
+        const bool take = j >= t_start && placed < total && v <= g1.rng && !occ;
+        npc.push_top(cell, take);
+        npc.alive |= take ? 1u << (placed - 2) : 0u;
+        placed += take ? 1 : 0;
+      }
+      s.w = b2;
+      s.idx = 12u;
+      t_start = 12u;
+    }
+  }
   for (uint32_t t = t_start; t < kWordCap && placed < total; ++t) {
     // placement 0: player 1, 1: player 2, 2+k: NPC k (all NPCs on p1's depth)
     const bool is_p2 = placed == 1;
@@ -4619,10 +4655,15 @@ int orx_rollout_shape(const orx_cfg_t* cfg, int32_t policy_p1, int32_t policy_p2
   out->threads_per_block = (int32_t)(p.paired ? pair_threads(cfg, p.lanes, lds_n)
                                               : rollout_threads(B, p.lanes));
   uint32_t lds = p.paired ? lds_n : (uint32_t)((lds_n + 15u) & ~15u);
-  if (!p.paired && ncap_for(cfg->n_npcs) == kDense && !getenv("ORX_NO_LDS_BITS")) {
-    const uint32_t bb = (uint32_t)((cfg->width * cfg->height + 31) / 32) * 4u;
-    const uint32_t per_block = (uint32_t)out->threads_per_block / 64u * p.lanes;
-    if ((uint64_t)lds + (uint64_t)per_block * bb <= device_lds_per_block()) lds += per_block * bb;
+  if (!p.paired) {  // as the one-lane launch: bitmaps, then tiles, dropped on a refused raise
+    uint32_t bits = 0;
+    if (ncap_for(cfg->n_npcs) == kDense && !getenv("ORX_NO_LDS_BITS")) {
+      const uint32_t bb = (uint32_t)((cfg->width * cfg->height + 31) / 32) * 4u;
+      const uint32_t per_block = (uint32_t)out->threads_per_block / 64u * p.lanes;
+      if ((uint64_t)lds + (uint64_t)per_block * bb <= device_lds_per_block()) bits = per_block * bb;
+    }
+    if (raise_lds(nullptr, lds + bits)) lds += bits;
+    if (!raise_lds(nullptr, lds)) lds = 0u;
   }
   out->lds_bytes = (int32_t)lds;
   return ORX_OK;

@@ -52,6 +52,17 @@ def _ptr(t: Optional[torch.Tensor]):
     return None if t is None else ctypes.c_void_p(t.data_ptr())
 
 
+def _raw_stream_getter(device: torch.device):
+    """A zero-argument callable returning the raw handle of ``device``'s current
+    stream (torch's private getter when this build has it: no Stream object per
+    call on the eager path)."""
+    raw = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+    idx = device.index
+    if raw is not None:
+        return lambda: raw(idx)
+    return lambda: torch.cuda.current_stream(device).cuda_stream
+
+
 def cuda_device(device=None) -> torch.device:
     """``device`` with its index made explicit (``"cuda"`` / None -> the current
     device), so engines built with ``"cuda"`` and ``"cuda:0"`` compare equal and
@@ -327,12 +338,11 @@ class BatchedEngine:
         fn, check = self.lib.orx_env_step_ex, _lib.check
         pcfg, pst, act = self._pcfg, self._pst, self.actions.data_ptr()
         B, seed, off, p2 = self.B, self.seed, self.game_offset, int(p2)
-        cur = torch.cuda.current_stream
-        dev = self.device
+        stream = _raw_stream_getter(self.device)
 
         def launch(a_ptr, nb, cols, obs, rew, done, status, bad):
             code = fn(pcfg, pst, a_ptr, nb, cols, p2, act, obs, rew, done, status, bad, B, seed,
-                      off, cur(dev).cuda_stream)
+                      off, stream())
             if code:
                 check("orx_env_step_ex", code)
         return launch

@@ -81,12 +81,14 @@ class VecEnv:
         self._p2 = int(Policy.NONE if self.opponent is None else self.opponent)
         # refused-action counter (device) and its asynchronous read-back
         self._bad_dev = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self._bad_ptr = self._bad_dev.data_ptr()
         self._bad_host = torch.zeros(1, dtype=torch.int32).pin_memory() \
             if self.check_actions == "deferred" else None
         self._bad_event = None
         self._bad_seen = 0
         self._steps = 0
         self._ring = [self._alloc_out() for _ in range(self.out_buffers)]
+        self._ring_ptrs = [tuple(t.data_ptr() for t in out) for out in self._ring]
         self._slot = 0
         self._launch = None   # the pre-bound orx_env_step_ex, made at the first step
 
@@ -198,21 +200,23 @@ class VecEnv:
             if getattr(self.engine, "mt_py", None) is not None:   # stock-seed mode
                 return self._step_stock(a)
             self._launch = self.engine.env_step_launcher(self._p2)
+        deferred = self._bad_host is not None
+        bad = self._bad_ptr if deferred else None
         if self._ring:
-            out = self._ring[self._slot]
-            self._slot = (self._slot + 1) % len(self._ring)
+            k = self._slot
+            out = self._ring[k]
+            self._slot = (k + 1) % len(self._ring)
+            self._launch(a.data_ptr(), nb, len(shape), *self._ring_ptrs[k], bad)
         else:
             out = self._alloc_out()
-        obs, reward, done, status = out
-        deferred = self._bad_host is not None
-        self._launch(a.data_ptr(), nb, len(shape), obs.data_ptr(), reward.data_ptr(),
-                     done.data_ptr(), status.data_ptr(),
-                     self._bad_dev.data_ptr() if deferred else None)
+            obs, reward, done, status = out
+            self._launch(a.data_ptr(), nb, len(shape), obs.data_ptr(), reward.data_ptr(),
+                         done.data_ptr(), status.data_ptr(), bad)
         if deferred:
             self._steps += 1
             if self._steps % self.check_every == 0:
                 self._poll_bad()
-        return obs, reward, done, status
+        return out
 
     def _step_stock(self, a: torch.Tensor):
         """Stock-seed mode (the bots draw from each game's own MT19937 stream):

@@ -27,9 +27,13 @@ def child(arg, steps, warmup=5, T=128, B=65536):
         else:
             os.environ[k] = v
     sys.path.insert(0, ROOT)
+    import ctypes
     import torch
     from optimax_rogue_amd import _lib, EnvConfig
     _lib.LIB_PATH = os.path.abspath(lib)
+    # an older build (another ABI) runs too: this step calls only entry
+    # points whose signatures every ABI since 4 shares
+    _lib.ABI_VERSION = ctypes.CDLL(_lib.LIB_PATH).orx_abi_version()
     from optimax_rogue_amd.engine import StreamShardedEngine
     dev = torch.device("cuda", 0)
     eng = StreamShardedEngine(EnvConfig.c3(), B, seed=0, device=dev,
