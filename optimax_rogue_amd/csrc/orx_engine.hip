@@ -125,6 +125,15 @@ constexpr int kRolloutBlock = ORX_ROLLOUT_BLOCK;  // rollout_kernel workgroup si
 #ifndef ORX_XCD_REMAP
 #define ORX_XCD_REMAP 1
 #endif
+#ifndef ORX_SPLIT_TICK
+// pair_rollout_kernel's RandomBot tick blocks (PM 1), one Philox pass per two
+// ticks: lane 2j draws tick t's block and lane 2j+1 tick t+1's, the pair
+// swaps them, and the next trip uses the held block (a reset redraws).  1:
+// the compact-row form only (bound by its tick chain); 2: every PM 1 form;
+// 0: none.  (The int32 forms are bound by their store stream, and C2's lone
+// waves measured slower with it in round 3: profiles/r03_v11.)
+#define ORX_SPLIT_TICK 1
+#endif
 #ifndef ORX_LEAN
 // pair_rollout_kernel's lean StaircaseBot spans: off (measured slower, DESIGN
 // s7.2: the launch is set by its slowest waves, which run few lean ticks and
@@ -3262,6 +3271,13 @@ __global__ void __launch_bounds__(GRID ? 512 : kRolloutBlock) ORX_PAIR_ATTR pair
   // separation damage (its ceil(k / period) carried as quotient and remainder,
   // no division) and the row, nothing else.
   constexpr bool kLean = ORX_LEAN && PM == 2 && NCAP == 0 && !GRID && (ORX_DIAG & (16 | 32 | 64 | 128)) == 0;
+  // split tick blocks (ORX_SPLIT_TICK): the held block of the next tick and
+  // its key (episode, tick); n_tick -1: none held
+  constexpr bool kSplit = PM == 1 && (ORX_DIAG & 64) == 0 &&
+                          (ORX_SPLIT_TICK == 2 || (ORX_SPLIT_TICK == 1 && CF));
+  W4 nb = {0u, 0u, 0u, 0u};
+  uint32_t nh0 = 0u, nh3 = 0u, n_ep = 0u;
+  int32_t n_tick = -1;
   int32_t span = 0;
   int32_t l_od = 0, l_q = 0, l_r = 0;  // SEP: the other's depth; the next tick's damage and phase
   int32_t t = 0;
@@ -3318,6 +3334,28 @@ __global__ void __launch_bounds__(GRID ? 512 : kRolloutBlock) ORX_PAIR_ATTR pair
       if constexpr ((ORX_DIAG & 64) != 0) {  // diagnostic: a cheap hash for the tick block
         const uint32_t hsh = (game * 0x9E3779B9u) ^ ((uint32_t)tick * 0x85EBCA6Bu) ^ ep;
         tb = W4{hsh * 0xC2B2AE35u, hsh ^ (hsh >> 15), 0u, 0u};
+      } else if constexpr (kSplit) {
+        const bool have = (ep == n_ep) & (tick == n_tick);
+        if (__builtin_amdgcn_ballot_w64(!have) == 0) {  // uniform: every game holds its block
+          tb = nb;
+          h0 = nh0;
+          h3 = nh3;
+          n_tick = -1;
+        } else {  // one pass for two ticks: lane 2j this tick's block, lane 2j+1 the next's
+          uint32_t m0, m3;
+          const W4 m = philox_ab(game, ep, (uint32_t)(tick + (int32_t)who), tag(PUR_TICK, 0),
+                                 key, m0, m3);
+          const uint32_t oa = (uint32_t)pair_swap((int32_t)m.a), ob = (uint32_t)pair_swap((int32_t)m.b);
+          const uint32_t o0 = (uint32_t)pair_swap((int32_t)m0), o3 = (uint32_t)pair_swap((int32_t)m3);
+          tb = W4{isB ? oa : m.a, isB ? ob : m.b, 0u, 0u};
+          h0 = isB ? o0 : m0;
+          h3 = isB ? o3 : m3;
+          nb = W4{isB ? m.a : oa, isB ? m.b : ob, 0u, 0u};
+          nh0 = isB ? m0 : o0;
+          nh3 = isB ? m3 : o3;
+          n_ep = ep;
+          n_tick = tick + 1;
+        }
       } else {
         tb = philox_ab(game, ep, (uint32_t)tick, tag(PUR_TICK, 0), key, h0, h3);
       }

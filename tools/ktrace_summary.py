@@ -13,7 +13,7 @@ def main(path, only=None, segments=False):
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     segs = []
     for r in rows:
-        name = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "")
+        name = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("orx_dev::", "").replace("void ", "")
         name = name.split("(")[0]
         if only and only not in name:
             continue

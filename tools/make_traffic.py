@@ -31,7 +31,7 @@ def load(d, counter):
     for r in csv.DictReader(open(f)):
         if r["Counter_Name"] != counter:
             continue
-        name = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "")
+        name = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("orx_dev::", "").replace("void ", "")
         agg[(name.split("(")[0], int(r["Grid_Size"]))].append(float(r["Counter_Value"]))
     return {k: (sum(v) / len(v), len(v)) for k, v in agg.items()}
 
