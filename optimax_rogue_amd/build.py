@@ -39,8 +39,8 @@ VARIANTS = {
     "diag64": ("ORX_DIAG=64",),   # the paired RandomBot tick block without Philox
     "noremap": ("ORX_XCD_REMAP=0",),  # workgroups in dispatch order (no XCD-aware remap)
     "lean": ("ORX_LEAN=1",),      # the paired StaircaseBot form with its lean spans (rejected)
-    "split0": ("ORX_SPLIT_TICK=0",),  # no split tick blocks (the compact form as round 4)
-    "split2": ("ORX_SPLIT_TICK=2",),  # split tick blocks in every paired RandomBot form
+    "split1": ("ORX_SPLIT_TICK=1",),  # split tick blocks in the compact form (rejected)
+    "split2": ("ORX_SPLIT_TICK=2",),  # split tick blocks in every paired RandomBot form (rejected)
 }
 
 

@@ -129,10 +129,12 @@ constexpr int kRolloutBlock = ORX_ROLLOUT_BLOCK;  // rollout_kernel workgroup si
 // pair_rollout_kernel's RandomBot tick blocks (PM 1), one Philox pass per two
 // ticks: lane 2j draws tick t's block and lane 2j+1 tick t+1's, the pair
 // swaps them, and the next trip uses the held block (a reset redraws).  1:
-// the compact-row form only (bound by its tick chain); 2: every PM 1 form;
-// 0: none.  (The int32 forms are bound by their store stream, and C2's lone
-// waves measured slower with it in round 3: profiles/r03_v11.)
-#define ORX_SPLIT_TICK 1
+// the compact-row form only; 2: every PM 1 form; 0 (the product): none --
+// measured in round 5 (profiles/r05_v5/ab_forms.jsonl, three rounds on one
+// box): compact rows 73.2-74.3 us with it against 73.1-75.1 without, the
+// int32 headline step 88.1-89.1 against 85.0-86.5 and C2 49.7-50.0 against
+// 47.9-48.5 (as in round 3, profiles/r03_v11).
+#define ORX_SPLIT_TICK 0
 #endif
 #ifndef ORX_LEAN
 // pair_rollout_kernel's lean StaircaseBot spans: off (measured slower, DESIGN
