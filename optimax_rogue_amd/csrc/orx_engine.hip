@@ -2062,10 +2062,15 @@ __device__ __forceinline__ void step_game(const orx_cfg_t& hc, const orx_state_t
   int32_t tick = 0;
   uint32_t ep = 0;
   uint16_t a = 0;
-  if constexpr (kOut) {
+  Items<NCAP> items;
+  int32_t sep = -1;
+  if constexpr (kOut) {  // every state word in one round trip (a reset discards some)
     load_players<GRID>(st, B, i, p1, p2);
     tick = st.tick[i];
     ep = (uint32_t)st.episode[i];
+    load_npcs(st, c, B, i, npc);
+    load_rpg(st, c, B, i, p1, p2, npc, items);
+    if (c.ext & ORX_EXT_SEPARATION_DAMAGE) sep = st.sep_start[i];
     a = get_action(p1, p2, tick, ep);
   }
   if (status != ORX_IN_PROGRESS) {
@@ -2077,7 +2082,6 @@ __device__ __forceinline__ void step_game(const orx_cfg_t& hc, const orx_state_t
     const uint32_t ep1 = (kOut ? ep : (uint32_t)st.episode[i]) + 1u;
     setup_game<NCAP, GRID>(c, key, game, ep1, p1, p2, npc, tick, status);
     store_players<GRID>(st, B, i, p1, p2, true);
-    Items<NCAP> items;
     items.clear();
     store_rpg(st, c, B, i, p1, p2, npc, items);
     st.tick[i] = tick;
@@ -2104,16 +2108,15 @@ __device__ __forceinline__ void step_game(const orx_cfg_t& hc, const orx_state_t
     ep = (uint32_t)st.episode[i];
     tick = st.tick[i];
     load_players<GRID>(st, B, i, p1, p2);
+    load_npcs(st, c, B, i, npc);
+    load_rpg(st, c, B, i, p1, p2, npc, items);
+    if (c.ext & ORX_EXT_SEPARATION_DAMAGE) sep = st.sep_start[i];
   }
-  load_npcs(st, c, B, i, npc);
-  Items<NCAP> items;
-  load_rpg(st, c, B, i, p1, p2, npc, items);
   NpcMem m{st.npc_pos, st.npc_health, B, i};
   Deltas dl = {0, 0, 0, 0, 0, 0};
   Events<EV> ev{EV ? events + (size_t)i * ORX_MAX_EVENTS * 4 : nullptr, 0};
   bool err = false;
   const bool p1_first = p1_first_draw(key, game, ep, tick, err);
-  int32_t sep = (c.ext & ORX_EXT_SEPARATION_DAMAGE) ? st.sep_start[i] : -1;
   tick_game<NCAP, EV, GRID>(c, key, game, ep, p1_first, p1, p2, npc, items, m, tick, status, err,
                             dl, ev, sep);
   if (c.ext & ORX_EXT_SEPARATION_DAMAGE) st.sep_start[i] = sep;
