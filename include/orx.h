@@ -409,6 +409,20 @@ int orx_reset(const orx_cfg_t* cfg, const orx_state_t* st, const uint8_t* mask,
 int orx_step(const orx_cfg_t* cfg, const orx_state_t* st, const int8_t* actions,
              int64_t n_games, uint64_t seed, int64_t game_offset, void* stream);
 
+/* n_ticks x orx_step in one launch (ABI 6): tick t plays actions[(t * n_games
+ * + b) * 2 + p] (int8, [n_ticks][n_games][2]: a recorded or precomputed move
+ * log), the state kept in registers between ticks; a non-Move value stops
+ * that game with ORX_STATUS_BAD_ACTION and a finished game is reset to its
+ * next episode when cfg->autoreset, as orx_step does tick by tick (results
+ * are identical, tested).  obs (may be NULL) receives each tick's post-step
+ * observation as orx_rollout_ex writes it, in obs_format.  Philox mode only
+ * (stock-seed mode: orx_step per tick).  Replaces the server loop
+ * server/main.py:110-113 over Updater.update (updater.py:76-162) fed from a
+ * move log -- SURVEY.md s8(b)'s orx_step(..., n_ticks). */
+int orx_step_n(const orx_cfg_t* cfg, const orx_state_t* st, const int8_t* actions,
+               int32_t n_ticks, int32_t* obs, int32_t obs_format, int64_t n_games, uint64_t seed,
+               int64_t game_offset, void* stream);
+
 /* orx_step plus the update-event list of the tick: for game b,
  * events[(b * ORX_MAX_EVENTS + j) * 4 + 0..3], j < n_events[b], in the order
  * Updater.update appends them to its result list (updater.py:133-145).

@@ -43,7 +43,7 @@ EXPORTS = ("orx_abi_version", "orx_last_error", "orx_validate_cfg", "orx_reset",
            "orx_step_events", "orx_policy", "orx_rollout", "orx_dungeon_stairs",
            "orx_dungeon_spawn", "orx_seed_mt", "orx_build_id", "orx_rollout_lanes", "orx_dstore_depths",
            "orx_rollout_shape", "orx_rollout_concurrent", "orx_env_step",
-           "orx_rollout_ex", "orx_env_step_ex")
+           "orx_rollout_ex", "orx_env_step_ex", "orx_step_n")
 
 
 def load() -> ctypes.CDLL:
@@ -106,6 +106,9 @@ def load() -> ctypes.CDLL:
         L.orx_env_step_ex.restype = ctypes.c_int
         L.orx_env_step_ex.argtypes = [P(OrxCfg), P(OrxState), vp, i32, i32, i32, vp, vp, vp, vp,
                                       vp, vp, i64, u64, i64, vp]
+    if hasattr(L, "orx_step_n"):
+        L.orx_step_n.restype = ctypes.c_int
+        L.orx_step_n.argtypes = [P(OrxCfg), P(OrxState), vp, i32, vp, i32, i64, u64, i64, vp]
     if hasattr(L, "orx_dstore_depths"):
         L.orx_dstore_depths.restype = ctypes.c_int
         L.orx_dstore_depths.argtypes = [P(OrxCfg)]

@@ -4130,6 +4130,80 @@ __global__ void __launch_bounds__(256) mt_rollout_kernel(orx_cfg_t hc, orx_state
   flush_deltas(st, B, i, dl);
 }
 
+// orx_step_n: n_ticks x orx_step with given actions (actions[t][b] = the
+// pair of tick t, player 1 in the low byte) in one launch, the state in
+// registers between ticks -- the multi-tick Updater.update loop of a replay
+// (server/main.py:110-113 fed from a recorded or precomputed move log):
+// per tick a game in progress validates its pair (a non-Move value stops it
+// with ORX_STATUS_BAD_ACTION, as orx_step), draws its initiative from the
+// tick block and runs tick_game; a finished game is reset to its next
+// episode when cfg.autoreset.  obs (may be NULL): each tick's post-step row,
+// in format fmt.  One lane per game (any dungeon, any NPC count, any
+// extension flag: the generic tick).
+template <int NCAP, bool GRID>
+__global__ void __launch_bounds__(256) step_n_kernel(orx_cfg_t hc, orx_state_t st,
+                                                     const int8_t* __restrict__ actions,
+                                                     int32_t n_ticks, int32_t* __restrict__ obs,
+                                                     uint32_t B, Key key, uint32_t off,
+                                                     int32_t fmt) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B) return;
+  const Cfg c = make_cfg(hc, st);
+  const uint32_t game = off + i;
+  Player p1, p2;
+  load_players<GRID>(st, B, i, p1, p2);
+  int32_t tick = st.tick[i];
+  int32_t status = st.status[i];
+  uint32_t ep = (uint32_t)st.episode[i];
+  Npcs<NCAP> npc;
+  npc.bind(st, c, B, i);
+  load_npcs(st, c, B, i, npc);
+  NpcMem m{st.npc_pos, st.npc_health, B, i};
+  Items<NCAP> items;
+  load_rpg(st, c, B, i, p1, p2, npc, items);
+  Deltas dl = {0, 0, 0, 0, 0, 0};
+  int32_t sep = (c.ext & ORX_EXT_SEPARATION_DAMAGE) ? st.sep_start[i] : -1;
+  bool stairs_dirty = false, npc_dirty = false;
+  TrajWriter<false> traj(obs, nullptr, B, i, fmt);
+  const uint16_t* a16 = reinterpret_cast<const uint16_t*>(actions) + i;
+  for (int32_t t = 0; t < n_ticks; ++t) {
+    const uint16_t a = a16[(size_t)t * B];
+    const int32_t a1 = (int8_t)(a & 0xFF), a2 = (int8_t)(a >> 8);
+    if (status == ORX_IN_PROGRESS) {
+      p1.move = a1;
+      p2.move = a2;
+      if (!valid_move(c, a1) || !valid_move(c, a2)) {
+        status = ORX_STATUS_BAD_ACTION;
+      } else {
+        bool err = false;
+        const int32_t descents = dl.descend;
+        const bool p1_first = p1_first_draw(key, game, ep, tick, err);
+        Events<false> ev{nullptr, 0};
+        tick_game<NCAP, false, GRID>(c, key, game, ep, p1_first, p1, p2, npc, items, m, tick,
+                                     status, err, dl, ev, sep);
+        stairs_dirty |= dl.descend != descents;
+      }
+    } else if (c.autoreset) {
+      ep += 1;
+      setup_game<NCAP, GRID>(c, key, game, ep, p1, p2, npc, tick, status);
+      items.clear();
+      if constexpr (NCAP > 0) store_new_npcs(st, c, B, i, npc);
+      stairs_dirty = true;
+      npc_dirty = true;
+      sep = -1;
+    }
+    traj.write(t, p1, p2, tick, status, a1, a2);
+  }
+  store_players<GRID>(st, B, i, p1, p2, stairs_dirty);
+  store_rpg(st, c, B, i, p1, p2, npc, items);
+  st.tick[i] = tick;
+  st.status[i] = status;
+  st.episode[i] = (int32_t)ep;
+  if (c.ext & ORX_EXT_SEPARATION_DAMAGE) st.sep_start[i] = sep;
+  if (NCAP > 0 && (npc_dirty || dl.npc_death)) npc.store_alive(st.npc_alive, B, i);
+  flush_deltas(st, B, i, dl);
+}
+
 template <bool GRID>
 __global__ void __launch_bounds__(256) stairs_kernel(orx_cfg_t hc, orx_state_t st,
                                                      const uint32_t* __restrict__ games,
@@ -4158,7 +4232,7 @@ __global__ void __launch_bounds__(256) stairs_kernel(orx_cfg_t hc, orx_state_t s
 // X-macro lists shared by the host dispatch (below) and the split build's
 // explicit instantiations, so the two cannot drift apart.
 // ---------------------------------------------------------------------------
-// (NCAP, GRID): reset_kernel, mt_reset_kernel, mt_rollout_kernel
+// (NCAP, GRID): reset_kernel, mt_reset_kernel, mt_rollout_kernel, step_n_kernel
 #define ORX_NG_LIST(X)                                                                          \
   X(0, false) X(8, false) X(16, false) X(kDense, false)                                         \
   X(0, true) X(8, true) X(16, true) X(kDense, true)
@@ -4254,6 +4328,10 @@ __global__ void __launch_bounds__(256) stairs_kernel(orx_cfg_t hc, orx_state_t s
   ORX_INST template __global__ void rollout_kernel<N, P, G, A, C>(                              \
       orx_cfg_t, orx_state_t, int32_t, int32_t, int32_t, int32_t*, int8_t*, uint32_t, Key,      \
       uint32_t, uint32_t, uint32_t, uint32_t, int32_t);
+#define ORX_I_STEP_N(N, G)                                                                      \
+  ORX_INST template __global__ void step_n_kernel<N, G>(orx_cfg_t, orx_state_t, const int8_t*,  \
+                                                        int32_t, int32_t*, uint32_t, Key,       \
+                                                        uint32_t, int32_t);
 #define ORX_I_STAIRS(G)                                                                         \
   ORX_INST template __global__ void stairs_kernel<G>(orx_cfg_t, orx_state_t, const uint32_t*,    \
                                                      const int32_t*, const int32_t*,            \
@@ -4303,6 +4381,7 @@ ORX_STEP_LIST(ORX_I_MT_STEP)
 ORX_NG_LIST(ORX_I_RESET)
 ORX_NG_LIST(ORX_I_MT_RESET)
 ORX_NG_LIST(ORX_I_MT_ROLLOUT)
+ORX_NG_LIST(ORX_I_STEP_N)
 ORX_I_STAIRS(false)
 ORX_I_STAIRS(true)
 #endif
@@ -4821,6 +4900,36 @@ int orx_step_events(const orx_cfg_t* cfg, const orx_state_t* st, const int8_t* a
     return fail(ORX_EINVAL, "orx_step_events needs events and n_events");
   return launch_step(cfg, st, actions, events, n_events, n_games, seed, game_offset, stream,
                      "orx_step_events");
+}
+
+int orx_step_n(const orx_cfg_t* cfg, const orx_state_t* st, const int8_t* actions,
+               int32_t n_ticks, int32_t* obs, int32_t obs_format, int64_t n_games, uint64_t seed,
+               int64_t game_offset, void* stream) {
+  int r;
+  if ((r = check_cfg(cfg)) || (r = check_sizes(n_games, game_offset))) return r;
+  if (n_ticks < 0) return fail(ORX_EINVAL, "n_ticks < 0");
+  if (obs_format != ORX_OBS_INT32 && obs_format != ORX_OBS_COMPACT)
+    return fail(ORX_EINVAL, "unknown obs_format");
+  if (obs && obs_format == ORX_OBS_COMPACT && (r = check_compact(cfg))) return r;
+  if (cfg->rng == ORX_RNG_MT19937)
+    return fail(ORX_EINVAL, "orx_step_n: stock-seed mode steps tick by tick (orx_step)");
+  if (n_games == 0 || n_ticks == 0) return ORX_OK;
+  if ((r = check_state(cfg, st, true))) return r;
+  if (!actions) return fail(ORX_EINVAL, "actions is NULL");
+  const uint32_t B = (uint32_t)n_games, off = (uint32_t)game_offset;
+  const hipStream_t s = (hipStream_t)stream;
+  const Key k = make_key(seed);
+  const int nc = ncap_for(cfg->n_npcs);
+  const bool grid = cfg->n_layouts > 0;
+#define ORX_STEP_N(N, G)                                                                        \
+  if (nc == N && grid == G) {                                                                   \
+    hipLaunchKernelGGL((step_n_kernel<N, G>), grid_for(B), dim3(kBlock), 0, s, *cfg, *st,       \
+                       actions, n_ticks, obs, B, k, off, obs_format);                           \
+    return launch_status("orx_step_n");                                                        \
+  }
+  ORX_NG_LIST(ORX_STEP_N)
+#undef ORX_STEP_N
+  return fail(ORX_EIO, "orx_step_n: no kernel instance for this configuration");
 }
 
 int orx_policy(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p1, int32_t policy_p2,

@@ -289,6 +289,22 @@ class BatchedEngine:
                    self.game_offset, self._stream())
         return self.status, self._ev, self._nev
 
+    def step_n(self, actions: torch.Tensor, obs: Optional[torch.Tensor] = None,
+               obs_format: int = OBS_INT32) -> torch.Tensor:
+        """orx_step_n: ``actions`` int8 [T, n_games, 2] (a move log: tick t plays
+        actions[t]) stepped in one launch, exactly as T calls of ``step`` would;
+        ``obs`` (int32 [T, obs_rows(obs_format), n_games], optional) receives
+        every tick's observation.  Returns the status tensor."""
+        if actions.dtype != torch.int8 or actions.dim() != 3 or actions.shape[1:] != (self.B, 2) \
+                or not actions.is_contiguous() or actions.device != self.device:
+            raise ValueError(f"actions must be a contiguous int8 [T, n_games, 2] tensor on "
+                             f"{self.device}")
+        T = int(actions.shape[0])
+        self._check_traj(T, obs, None, obs_format)
+        self._call("orx_step_n", _ptr(actions), T, _ptr(obs), int(obs_format), self.B, self.seed,
+                   self.game_offset, self._stream())
+        return self.status
+
     _ACTION_BYTES = {torch.int8: 1, torch.int16: 2, torch.int32: 4, torch.int64: 8}
 
     def env_step(self, actions: torch.Tensor, p2: int, obs: torch.Tensor, reward: torch.Tensor,

@@ -36,6 +36,13 @@ int main(void) {
                       0, 1, 0, NULL) != ORX_OK) { printf("empty env step ex failed\n"); return 13; }
   if (orx_env_step_ex(&c, NULL, NULL, 8, 1, ORX_POLICY_NONE, NULL, NULL, NULL, NULL, NULL, NULL,
                       16, 1, 0, NULL) != ORX_EINVAL) { printf("player 2 without a move accepted\n"); return 14; }
+  /* ABI 6: n ticks of given actions in one launch */
+  if (orx_step_n(&c, NULL, NULL, 5, NULL, ORX_OBS_INT32, 0, 1, 0, NULL) != ORX_OK) {
+    printf("empty step_n failed\n"); return 16;
+  }
+  if (orx_step_n(&c, NULL, NULL, -1, NULL, ORX_OBS_INT32, 16, 1, 0, NULL) != ORX_EINVAL) {
+    printf("negative n_ticks accepted\n"); return 17;
+  }
   {
     orx_rollout_shape_t sh;
     if (orx_rollout_shape(&c, ORX_POLICY_RANDOM, ORX_POLICY_RANDOM, 65536, 1, 1, &sh) != ORX_OK ||

@@ -1096,3 +1096,75 @@ def test_compact_rows_equal_int32_rows(name):
     for k in s0:
         assert np.array_equal(s0[k], s1[k]), (name, k)
     assert s0["ep_count"].sum() > 0 or name.startswith("c3_bench") or name.startswith("c5")
+
+
+@pytest.mark.parametrize("name", case_names())
+def test_golden_step_n(name):
+    """orx_step_n: a fixture's whole recorded move log in one launch -- every
+    tick's observation row and the final state equal the reference's
+    (server/main.py:110-113 over updater.py:76-162).  Keyed-stream fixtures
+    only: in stock-seed mode the bots' draws share the game's stream, which a
+    replay of given moves does not draw (orx_step_n refuses that mode)."""
+    import torch
+    from optimax_rogue_amd.enums import OBS_FIELDS
+    fx = Fixture(name)
+    if fx.stock:
+        pytest.skip("stock-seed fixture: replayed tick by tick (test_golden_step_given_actions)")
+    eng = _engine(fx.cfg, fx.G, fx.seed, fx.game_offset, layouts=fx.layouts)
+    acts = torch.from_numpy(np.ascontiguousarray(fx.actions)).to(eng.device)
+    obs = torch.zeros((fx.T, len(OBS_FIELDS), fx.G), dtype=torch.int32, device=eng.device)
+    eng.step_n(acts, obs=obs)
+    o = obs.cpu().numpy()
+    for t in range(fx.T):
+        assert np.array_equal(o[t], _obs_rows(fx.state(t + 1))), f"{name} obs t={t + 1}"
+    compare_state(eng.snapshot(), fx.state(fx.T), fx.K, f"{name} final")
+
+
+STEP_N_CASES = {
+    "npc8": (dict(width=16, height=16, n_npcs=8, max_ticks=90), None),
+    "dense30": (dict(width=12, height=12, n_npcs=30, npc_health=2, max_ticks=70), None),
+    "bank_unused": (dict(width=12, height=10, n_npcs=3, max_ticks=60, despawn=2, start_mode=2,
+                         p1_depth=1, p2_depth=0), (12, 10, 5, 88, (1, 2))),
+    "rpg_readme": (dict(width=9, height=9, n_npcs=6, max_ticks=60, flags=4 | 8 | 16 | 32 | 64,
+                        player_health=6), None),
+    "sep_double": (dict(width=7, height=7, start_mode=2, p1_depth=0, p2_depth=1, max_ticks=0,
+                        flags=3, sep_period=2, player_health=4), None),
+}
+
+
+@pytest.mark.parametrize("name", sorted(STEP_N_CASES))
+def test_step_n_equals_step(name):
+    """orx_step_n over 160 ticks of random moves (~1% of them invalid: the
+    game stops with STATUS_BAD_ACTION and restarts) equals 160 orx_step calls:
+    the state after every tick (its observation row) and at the end; the
+    compact rows decode to the same rows."""
+    import torch
+    from optimax_rogue_amd.engine import decode_compact
+    from optimax_rogue_amd.enums import EXT_HEAL, OBS_COMPACT, OBS_FIELDS
+    cfg, bank = STEP_N_CASES[name]
+    lay = _bank(*bank) if bank else None
+    B, T, seed = 1500, 160, 7
+    hi = 6 if cfg.get("flags", 0) & EXT_HEAL else 5
+    rs = np.random.RandomState(3)
+    acts = rs.randint(1, hi + 1, size=(T, B, 2)).astype(np.int8)
+    bad = rs.rand(T, B, 2) < 0.005
+    acts[bad] = rs.choice([0, -3, hi + 1, 100], size=int(bad.sum())).astype(np.int8)
+    a = torch.from_numpy(acts).to("cuda:0")
+    ref = _engine(cfg, B, seed, 11, layouts=lay)
+    eng = _engine(cfg, B, seed, 11, layouts=lay)
+    obs = torch.zeros((T, len(OBS_FIELDS), B), dtype=torch.int32, device=eng.device)
+    eng.step_n(a, obs=obs)
+    o = obs.cpu().numpy()
+    stops = 0
+    for t in range(T):
+        st = ref.step(a[t].contiguous())
+        snap = ref.snapshot()
+        assert np.array_equal(o[t], _obs_rows(snap)), f"{name} t={t}"
+        stops += int((snap["status"] == 16).sum())
+    compare_state(eng.snapshot(), ref.snapshot(), int(cfg.get("n_npcs", 0)), f"{name} final")
+    assert stops > 0
+    if int(cfg.get("max_ticks", 0)) > 0 and not cfg.get("flags", 0) & 1:
+        eng2 = _engine(cfg, B, seed, 11, layouts=lay)
+        c_obs = torch.zeros((T, 6, B), dtype=torch.int32, device=eng.device)
+        eng2.step_n(a, obs=c_obs, obs_format=OBS_COMPACT)
+        assert np.array_equal(decode_compact(c_obs).cpu().numpy(), o), name
