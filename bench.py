@@ -305,6 +305,26 @@ def extras(torch, cfg, dev, B_cfg, K, large_rollout=False):
                                   "HIP graph"}
     del env, pool, gv
     torch.cuda.empty_cache()
+    # (1c) a replay: orx_step_n over a 128-tick move log (int8 [128, B, 2],
+    # uniform 1..5) at the config batch, every tick's observation rows
+    # written -- the generic one-lane tick, one launch per 128 ticks
+    eng = BatchedEngine(cfg, B_cfg, seed=3, device=dev)
+    T = 128
+    log = torch.randint(1, 6, (T, B_cfg, 2), dtype=torch.int8, device=dev)
+    robs = torch.empty((T, len(OBS_FIELDS), B_cfg), dtype=torch.int32, device=dev)
+    eng.step_n(log, obs=robs)
+    rs = timed_launches(torch, lambda: eng.step_n(log, obs=robs), 10)
+    rmed = sorted(rs)[len(rs) // 2]
+    rb = (bytes_per_game("rollout", K, T) + T * ACT_BYTES) * B_cfg   # + the log read
+    out["replay_step_n"] = {"games": B_cfg, "ticks_per_launch": T, "us_per_launch": rmed * 1e6,
+                            "env_steps_per_s": B_cfg * T / rmed,
+                            "achieved_GBps": rb / rmed / 1e9,
+                            "frac": rb / rmed / 1e9 / HBM_PEAK_GBS,
+                            "note": "orx_step_n: a 128-tick move log of both players replayed in "
+                                    "one launch with every tick's observation rows (one lane per "
+                                    "game, the generic tick); median of 10 launches"}
+    del eng, log, robs
+    torch.cuda.empty_cache()
     # (2) large batch: the chip full (2^21 games)
     BL = 1 << 21
     eng = BatchedEngine(cfg, BL, seed=3, device=dev)

@@ -41,6 +41,7 @@ VARIANTS = {
     "lean": ("ORX_LEAN=1",),      # the paired StaircaseBot form with its lean spans (rejected)
     "split1": ("ORX_SPLIT_TICK=1",),  # split tick blocks in the compact form (rejected)
     "split2": ("ORX_SPLIT_TICK=2",),  # split tick blocks in every paired RandomBot form (rejected)
+    "sepw0": ("ORX_SEP_WAVES=0",),    # the separation-damage StaircaseBot form uncapped (131 VGPRs)
 }
 
 

@@ -3165,13 +3165,21 @@ struct PairWriter {
 #ifndef ORX_PAIR_ATTR
 #define ORX_PAIR_ATTR
 #endif
+// the StaircaseBot form with separation damage held to four waves per SIMD
+// (128 VGPRs; 131 otherwise, three waves): C5's 131,072 games as two paired
+// shards are four 32-game waves per SIMD
+#ifndef ORX_SEP_WAVES
+#define ORX_SEP_WAVES 1
+#endif
 // GRID (round 4): a dungeon bank -- each lane reads its target's tile (its
 // player's layout; LDS-staged when the bank fits, lds_n bytes), a Wall or the
 // grid's edge blocks, ANY staircase tile makes the tick rare; descends and
 // resets take rare_tick's bank forms (the closed-form fast paths are for
 // empty dungeons).
 template <int NCAP, int PM, int AUX, bool SEP, bool CF = false, bool GRID = false>
-__global__ void __launch_bounds__(GRID ? 512 : kRolloutBlock) ORX_PAIR_ATTR pair_rollout_kernel(orx_cfg_t hc, orx_state_t st,
+__global__ void __launch_bounds__(GRID ? 512 : kRolloutBlock) ORX_PAIR_ATTR
+    __attribute__((amdgpu_waves_per_eu(ORX_SEP_WAVES && PM == 2 && SEP ? 4 : 1)))
+    pair_rollout_kernel(orx_cfg_t hc, orx_state_t st,
                                                                      int32_t n_ticks,
                                                                      int32_t* __restrict__ obs,
                                                                      int8_t* __restrict__ act,
