@@ -41,9 +41,9 @@ class VecEnv:
     * ``"deferred"`` (default): the launch also counts refused actions into a
       device counter, and every ``check_every`` steps ``step`` reads it back
       asynchronously (pinned memory and an event, no host sync); once a read
-      shows new refusals, a later ``step`` raises ValueError.  Detection lags
-      by at most two check periods; ``bad_actions()`` reads the count now
-      (synchronizing).
+      shows new refusals, a later ``step`` raises ValueError (before playing
+      its own tick).  Detection lags by at most two check periods;
+      ``bad_actions()`` reads the count now (synchronizing).
     * ``True``: a host check before every launch raises ValueError at once
       (a device-to-host sync per step).
     * ``False``: no detection.
@@ -202,6 +202,10 @@ class VecEnv:
             self._launch = self.engine.env_step_launcher(self._p2)
         deferred = self._bad_host is not None
         bad = self._bad_ptr if deferred else None
+        if deferred:   # (before the launch: a call that raises plays no tick)
+            self._steps += 1
+            if self._steps % self.check_every == 0:
+                self._poll_bad()
         if self._ring:
             k = self._slot
             out = self._ring[k]
@@ -212,10 +216,6 @@ class VecEnv:
             obs, reward, done, status = out
             self._launch(a.data_ptr(), nb, len(shape), obs.data_ptr(), reward.data_ptr(),
                          done.data_ptr(), status.data_ptr(), bad)
-        if deferred:
-            self._steps += 1
-            if self._steps % self.check_every == 0:
-                self._poll_bad()
         return out
 
     def _step_stock(self, a: torch.Tensor):
