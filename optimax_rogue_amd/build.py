@@ -107,7 +107,7 @@ def build(force: bool = False, verbose: bool = False, defines: Iterable[str] = (
 # their share of the explicit instantiations, orx_engine.hip "Kernel
 # instances"), then linked -- about a minute on 8 cores instead of ~6 for one
 # translation unit.
-NPARTS = 13
+NPARTS = 14
 
 
 def _build_parts(base, out, verbose=False, jobs=None):

@@ -3260,7 +3260,13 @@ __global__ void __launch_bounds__(GRID ? 512 : kRolloutBlock) ORX_PAIR_ATTR
   }
   Deltas dl = {0, 0, 0, 0, 0, 0};
   bool restarted = false;
-  constexpr int need = (PM == 1 || PM == 3) ? 2 : 0;
+  // PM 4 / 5 (round 5): one RandomBot and one StaircaseBot -- 4: player 1
+  // is the RandomBot, 5: player 2 -- (a learner's baseline evaluation);
+  // the RandomBot lane takes the tick block's first accepted field, as
+  // rollout_tick's single random player
+  constexpr bool kMixed = PM == 4 || PM == 5;
+  const bool rb_lane = kMixed && (isB == (PM == 5));
+  constexpr int need = (PM == 1 || PM == 3) ? 2 : kMixed ? 1 : 0;
   PairWriter<AUX, CF> traj(obs, act, B, i, who);
   // every state load resolved before the tick loop: a value first read in the
   // loop leaves its load pending at the loop head, and that wait then also
@@ -3384,6 +3390,22 @@ __global__ void __launch_bounds__(GRID ? 512 : kRolloutBlock) ORX_PAIR_ATTR
         moves_from_block(tb, 2, key, game, ep, tick, r0, r1, err);
         move = isB ? r1 : r0;
       }
+    } else if constexpr (kMixed) {
+      tb = philox_ab(game, ep, (uint32_t)tick, tag(PUR_TICK, 0), key, h0, h3);
+      const uint32_t acc = accepted3(tb.b);
+      const int32_t rmove = (int32_t)__builtin_amdgcn_ubfe(tb.b, ffbl(acc), 3u) + 1;
+      const int32_t dx = me.sx - me.x, dy = me.sy - me.y;
+      const int32_t adx = dx < 0 ? -dx : dx, ady = dy < 0 ? -dy : dy;
+      const int32_t smove = adx > ady ? (dx > 0 ? ORX_MOVE_RIGHT : ORX_MOVE_LEFT)
+                                      : (dy > 0 ? ORX_MOVE_DOWN : ORX_MOVE_UP);
+      move = rb_lane ? rmove : smove;
+      if (ORX_UNLIKELY(acc == 0u)) {  // the game's word b holds no accepted field
+        int32_t r0 = ORX_MOVE_STAY, r1 = ORX_MOVE_STAY;
+        bool err = false;
+        finish_cd(tb, h0, h3, key);
+        moves_from_block(tb, 1, key, game, ep, tick, r0, r1, err);
+        move = rb_lane ? r0 : smove;
+      }
     } else {
       const int32_t dx = me.sx - me.x, dy = me.sy - me.y;
       const int32_t adx = dx < 0 ? -dx : dx, ady = dy < 0 ? -dy : dy;
@@ -3439,7 +3461,7 @@ __global__ void __launch_bounds__(GRID ? 512 : kRolloutBlock) ORX_PAIR_ATTR
       ORX_COUNT(dl.n_rare);
       ORX_CYC_BEGIN(cy0);
 #endif
-      if constexpr (PM == 1 || PM == 3) {  // the tick block's words c, d (rare_tick's fallbacks)
+      if constexpr (PM == 1 || PM == 3 || kMixed) {  // the tick block's words c, d (rare_tick's fallbacks)
         asm volatile("" : "+v"(h0), "+v"(h3));
         finish_cd(tb, h0, h3, key);
       }
@@ -3476,7 +3498,7 @@ __global__ void __launch_bounds__(GRID ? 512 : kRolloutBlock) ORX_PAIR_ATTR
       // instruction stream for both -- and the lanes swap them.
       bool fast = false;
       const int32_t osx = pair_swap(me.sx), osy = pair_swap(me.sy);
-      if constexpr (PM == 2 && NCAP == 0 && !GRID) {
+      if constexpr ((PM == 2 || kMixed) && NCAP == 0 && !GRID) {
         if (!in_progress & (c.autoreset != 0)) {  // uniform over the pair
           // The next episode (setup_game's keyed first-block form), its two
           // starting dungeons split over the pair: each lane draws its own
@@ -3533,7 +3555,7 @@ __global__ void __launch_bounds__(GRID ? 512 : kRolloutBlock) ORX_PAIR_ATTR
           }
         }
       }
-      if constexpr (PM == 1 && NCAP > 0) {
+      if constexpr ((PM == 1 || kMixed) && NCAP > 0) {
         // NPC hits without a meet or a staircase (C3's common rare tick): the
         // attackers stay, the other player moves; both lanes apply both hits
         // to their identical NPC registers (npc_hits: order-free without the
@@ -3619,7 +3641,7 @@ __global__ void __launch_bounds__(GRID ? 512 : kRolloutBlock) ORX_PAIR_ATTR
 #endif
         }
       }
-      if constexpr (PM == 1 || PM == 3) {
+      if constexpr (PM == 1 || PM == 3 || kMixed) {
         // a meet without a staircase or an NPC hit: rare_tick's lean meet,
         // the two moves in the drawn order (the tick block's word a; an
         // all-reject word takes the ordered tick), from each lane's side;
@@ -3664,7 +3686,7 @@ __global__ void __launch_bounds__(GRID ? 512 : kRolloutBlock) ORX_PAIR_ATTR
 #endif
         }
       }
-      if (PM == 2 && !GRID &&
+      if ((PM == 2 || kMixed) && !GRID &&
           (in_progress & !meet & (st_me != (st_o != 0)) & !hit_me & (hit_o == 0))) {
 #ifdef ORX_STAMPS
         ORX_CYC_BEGIN(cyf);
@@ -4269,9 +4291,14 @@ __global__ void __launch_bounds__(256) stairs_kernel(orx_cfg_t hc, orx_state_t s
   X(N, 3, kStreamAux, false, false, true) X(N, 3, kPartialAux, false, false, true)              \
   X(N, 1, kStreamAux, false, false, true) X(N, 1, kPartialAux, false, false, true)              \
   X(N, 2, kStreamAux, false, false, true) X(N, 2, kPartialAux, false, false, true)
+// PM 4 / 5 (a RandomBot against a StaircaseBot), empty dungeons, int32 rows
+#define ORX_PAIR_LIST_M(X, N)                                                                   \
+  X(N, 4, kStreamAux, false, false, false) X(N, 4, kPartialAux, false, false, false)            \
+  X(N, 5, kStreamAux, false, false, false) X(N, 5, kPartialAux, false, false, false)
 #define ORX_PAIR_LIST(X)                                                                        \
   ORX_PAIR_LIST_A(X, 0) ORX_PAIR_LIST_B(X, 0) ORX_PAIR_LIST_A(X, 8) ORX_PAIR_LIST_B(X, 8)       \
-  ORX_PAIR_LIST_A(X, 16) ORX_PAIR_LIST_B(X, 16)
+  ORX_PAIR_LIST_A(X, 16) ORX_PAIR_LIST_B(X, 16) ORX_PAIR_LIST_M(X, 0) ORX_PAIR_LIST_M(X, 8)     \
+  ORX_PAIR_LIST_M(X, 16)
 // (NCAP, PM, GRID, AUX, CF): rollout_kernel -- the generic form (PM 0) in one
 // store policy and any row format; the buffer-store forms (PM 1 / 2 / 3) in
 // both policies; PM 1 / 2 without a bank or dense NPCs also in compact rows
@@ -4347,7 +4374,8 @@ __global__ void __launch_bounds__(256) stairs_kernel(orx_cfg_t hc, orx_state_t s
                                                      int32_t*, uint32_t, Key);
 // the parts: 1-6 the paired rollouts (NCAP 0 / 8 / 16, halves A and B), 7-9
 // the one-lane rollouts per NCAP, 10 the dense rollouts and env_step, 11 the
-// step kernels, 12 the rest; each costs a few tens of seconds of hipcc
+// step kernels, 12 the rest, 13 the mixed-bot paired rollouts; each costs a
+// few tens of seconds of hipcc
 #define ORX_OWNS(k) (ORX_PART == 0 || ORX_PART == (k))
 #if ORX_OWNS(1)
 ORX_PAIR_LIST_A(ORX_I_PAIR, 0)
@@ -4384,6 +4412,11 @@ ORX_ENV_LIST(ORX_I_ENV)
 ORX_STEP_LIST(ORX_I_STEP)
 ORX_STEP_REF_LIST(ORX_I_STEP_REF)
 ORX_STEP_LIST(ORX_I_MT_STEP)
+#endif
+#if ORX_OWNS(13)
+ORX_PAIR_LIST_M(ORX_I_PAIR, 0)
+ORX_PAIR_LIST_M(ORX_I_PAIR, 8)
+ORX_PAIR_LIST_M(ORX_I_PAIR, 16)
 #endif
 #if ORX_OWNS(12)
 ORX_NG_LIST(ORX_I_RESET)
@@ -4631,6 +4664,10 @@ int rollout_pm(const orx_cfg_t* cfg, int32_t p1, int32_t p2, uint32_t B, bool tr
             p2 == ORX_POLICY_STAIRCASE) ? 2
          : ((cfg->flags | ORX_EXT_HEAL) == ORX_EXT_RPG && both_random &&
             ncap_for(cfg->n_npcs) != kDense) ? 3   // (no dense-NPC instance of PM 3)
+         // one RandomBot against one StaircaseBot: paired forms only (PM 4 /
+         // 5; a launch that does not pair takes the generic form)
+         : (cfg->flags == 0 && p1 == ORX_POLICY_RANDOM && p2 == ORX_POLICY_STAIRCASE) ? 4
+         : (cfg->flags == 0 && p1 == ORX_POLICY_STAIRCASE && p2 == ORX_POLICY_RANDOM) ? 5
          : 0;
 }
 
@@ -4701,7 +4738,7 @@ RolloutPlan plan_rollout(const orx_cfg_t* cfg, int pm, uint32_t B, uint32_t conc
   // a dungeon bank: PM 1 / 3, and PM 2 without separation damage, with the
   // tiles staged in LDS (the paired form reads them only there)
   const bool bank_ok = cfg->n_layouts == 0 ||
-                       (!(pm == 2 && (cfg->flags & ORX_EXT_SEPARATION_DAMAGE) != 0) &&
+                       (!(pm == 2 && (cfg->flags & ORX_EXT_SEPARATION_DAMAGE) != 0) && pm <= 3 &&
                         bank_in_lds(cfg));
   // StaircaseBots (PM 2) also pair where the one-lane rule fills whole
   // waves, when the batch shares the device with another launch and the
@@ -4712,7 +4749,7 @@ RolloutPlan plan_rollout(const orx_cfg_t* cfg, int pm, uint32_t B, uint32_t conc
   const uint64_t simds4 = 4ull * 32ull * (uint64_t)device_simds();
   const bool pm2_full = pm == 2 && p.lanes == 64u && concurrency >= 2 &&
                         (uint64_t)B * concurrency <= simds4 && !lanes_override();
-  p.paired = ncap_for(cfg->n_npcs) != kDense && bank_ok && pm >= 1 && pm <= 3 &&
+  p.paired = ncap_for(cfg->n_npcs) != kDense && bank_ok && pm >= 1 && pm <= 5 &&
              cfg->width <= 256 && cfg->height <= 256 && (p.lanes <= 32u || pm2_full) &&
              paired_enabled();
   if (p.paired) {
@@ -4769,8 +4806,9 @@ int orx_rollout_shape(const orx_cfg_t* cfg, int32_t policy_p1, int32_t policy_p2
     out->nontemporal = 1;
     return ORX_OK;
   }
-  const int pm = rollout_pm(cfg, policy_p1, policy_p2, B, trajectory != 0);
+  int pm = rollout_pm(cfg, policy_p1, policy_p2, B, trajectory != 0);
   RolloutPlan p = plan_rollout(cfg, pm, B, (uint32_t)concurrency);
+  if (!p.paired && pm >= 4) pm = 0;  // (the mixed-bot forms are paired only)
   const uint64_t tiles = (uint64_t)cfg->n_layouts * (uint64_t)(cfg->width * cfg->height);
   uint32_t lds_n = (cfg->n_layouts > 0 && bank_in_lds(cfg)) ? (uint32_t)tiles : 0u;
   if (p.paired && !raise_lds(nullptr, lds_n)) {  // the launch's fallback (one lane, global tiles)
@@ -5063,8 +5101,9 @@ int orx_rollout_ex(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p
   // compact rows: the buffer-store forms of PM 1 / 2 without a bank or dense
   // NPCs have compact instances; every other launch takes the generic form,
   // whose writer reads the format at run time
-  if (cf && (pm == 3 || grid || nc == kDense)) pm = 0;
+  if (cf && (pm >= 3 || grid || nc == kDense)) pm = 0;
   RolloutPlan plan = plan_rollout(cfg, pm, B, (uint32_t)concurrency);
+  if (!plan.paired && pm >= 4) pm = 0;  // (the mixed-bot forms are paired only)
   // dynamic LDS: the bank's tiles when they fit the device's per-workgroup
   // limit (160 KiB on gfx950, above 64 KiB with the opt-in raise)
   const uint64_t tiles = grid ? (uint64_t)cfg->n_layouts * (uint64_t)(cfg->width * cfg->height) : 0;
@@ -5101,6 +5140,7 @@ int orx_rollout_ex(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p
 #undef ORX_PAIR
     if (!refused) return fail(ORX_EIO, "orx_rollout: no paired kernel instance for this plan");
     plan.paired = false;
+    if (pm >= 4) pm = 0;
     plan.lanes = rollout_lanes(B);
     plan.nt = plan.lanes * 4u >= 128u;
     lds_n = 0u;

@@ -204,7 +204,13 @@ def test_rollout_shape_rules(lib):
     assert shape(EnvConfig.c3(), 32768) == (16, 2, 0)             # one such launch alone
     assert shape(EnvConfig.c3(), 65536) == (64, 1, 1)             # full waves: one lane per game
     assert shape(EnvConfig(n_npcs=40), 4096) == (16, 1, 0)        # LDS NPC table: one lane per game
-    assert shape(EnvConfig.c5(), 16384, 2, 1) == (16, 1, 1)       # mixed bots: the generic form
+    # round 5: a RandomBot against a StaircaseBot pairs too (PM 4 / 5), not
+    # with extension flags or a dungeon bank (the generic one-lane form)
+    assert shape(EnvConfig.c5(), 16384, 2, 1) == (8, 2, 0)
+    assert shape(EnvConfig.c3(), 32768, 1, 2, conc=2) == (32, 2, 1)
+    assert shape(EnvConfig(width=20, height=20, flags=1, sep_period=3), 4096, 1, 2) == (16, 1, 1)
+    assert shape(EnvConfig(width=12, height=10), 4096, 2, 1, n_layouts=4)[1] == 1
+    assert shape(EnvConfig.c3(), 65536, 1, 2) == (64, 1, 1)       # full waves: one lane
     assert shape(EnvConfig.c2(), 4096, traj=0) == (16, 1, 1)      # no trajectory buffers
     # round 4: the character mechanics and dungeon banks pair too (a bank not
     # with separation damage for StaircaseBots)

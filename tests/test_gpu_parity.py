@@ -930,6 +930,18 @@ PAIRED_CASES.update({
     "stairs_lean_separated": (dict(width=80, height=80, start_mode=2, p1_depth=0, p2_depth=1,
                                    max_ticks=130), (2, 2), 256, 87),
 })
+# round 5: a RandomBot against a StaircaseBot (PM 4: player 1 random, PM 5:
+# player 2), NPC-free and with register NPCs, both starts and despawn rules,
+# short episodes (the reset and descend fast paths, the lean meet, NPC hits)
+PAIRED_CASES.update({
+    "mixed_rs_npcs": (dict(width=10, height=10, n_npcs=6, max_ticks=40), (1, 2), 1000, 91),
+    "mixed_sr_npcs16_unused": (dict(width=9, height=9, n_npcs=14, max_ticks=35, despawn=2),
+                               (2, 1), 1000, 92),
+    "mixed_rs_separated": (dict(width=12, height=10, start_mode=2, p1_depth=1, p2_depth=0,
+                                max_ticks=60), (1, 2), 1000, 93),
+    "mixed_sr_duel": (dict(width=5, height=4, max_ticks=30, player_health=3), (2, 1), 1000, 94),
+    "mixed_rs_c3_shape": (dict(width=64, height=64, n_npcs=8, max_ticks=80), (1, 2), 1024, 95),
+})
 PAIRED_BANKS = {"bank_random_npcs": (20, 16, 6, 81, (1, 2)), "bank_stairs_unused": (12, 10, 5, 82, (1, 2)),
                 "bank_stairs_npcs": (14, 12, 4, 83, (2,)), "bank_rpg": (16, 12, 5, 84, (1, 3))}
 
