@@ -941,6 +941,9 @@ PAIRED_CASES.update({
                                 max_ticks=60), (1, 2), 1000, 93),
     "mixed_sr_duel": (dict(width=5, height=4, max_ticks=30, player_health=3), (2, 1), 1000, 94),
     "mixed_rs_c3_shape": (dict(width=64, height=64, n_npcs=8, max_ticks=80), (1, 2), 1024, 95),
+    # StaircaseBots hitting NPCs on the paired NPC-hit path, with separation damage
+    "stairs_sep_npcs": (dict(width=10, height=9, start_mode=2, p1_depth=0, p2_depth=1, n_npcs=5,
+                             max_ticks=50, flags=1, sep_period=3), (2, 2), 1000, 96),
 })
 PAIRED_BANKS = {"bank_random_npcs": (20, 16, 6, 81, (1, 2)), "bank_stairs_unused": (12, 10, 5, 82, (1, 2)),
                 "bank_stairs_npcs": (14, 12, 4, 83, (2,)), "bank_rpg": (16, 12, 5, 84, (1, 3))}
