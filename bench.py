@@ -385,7 +385,9 @@ def extras(torch, cfg, dev, B_cfg, K, large_rollout=False):
     def rollout_rate(c, games, pol, T=128, reps=6, streams=1):
         """µs per T-tick launch of `games` (median of `reps`); with streams > 1
         the games run as that many stream shards, as the headline step does
-        (StreamShardedEngine; a step = one launch per shard, fork/join)."""
+        (StreamShardedEngine; a step = one launch per shard, fork/join).
+        ``pol``: both players' policy, or a (player 1, player 2) pair."""
+        p1, p2 = (pol, pol) if isinstance(pol, int) else pol
         if streams > 1:
             # as the headline step: the shards' launches back to back on their
             # streams between one fork and one join, HIP events around them all
@@ -393,7 +395,7 @@ def extras(torch, cfg, dev, B_cfg, K, large_rollout=False):
             # overlap the next steps' launches, which a short run under-counts)
             e = StreamShardedEngine(c, games, seed=5, device=dev, n_streams=streams)
             o, a = e.trajectory_buffers(T)
-            go = e.rollout_launcher(T, pol, pol, obs=o, act=a)
+            go = e.rollout_launcher(T, p1, p2, obs=o, act=a)
             e.fork()
             for _ in range(3):
                 go()
@@ -413,11 +415,11 @@ def extras(torch, cfg, dev, B_cfg, K, large_rollout=False):
             e = BatchedEngine(c, games, seed=5, device=dev)
             o = torch.empty((T, len(OBS_FIELDS), games), dtype=torch.int32, device=dev)
             a = torch.empty((T, games, 2), dtype=torch.int8, device=dev)
-            go = e.rollout_launcher(T, pol, pol, obs=o, act=a)
+            go = e.rollout_launcher(T, p1, p2, obs=o, act=a)
             go()
             d = timed_launches(torch, go, reps)
             us = sorted(d)[len(d) // 2]
-        shape = e.rollout_shape(pol, pol)
+        shape = e.rollout_shape(p1, p2)
         del e, o, a, go
         return {"games": games, "ticks_per_launch": T, "games_per_wave": shape["games_per_wave"],
                 "lanes_per_game": shape["lanes_per_game"], "nontemporal": shape["nontemporal"],
@@ -477,6 +479,12 @@ def extras(torch, cfg, dev, B_cfg, K, large_rollout=False):
                               "vs oracle bit-exact, parity unpinned vs the reference); two "
                               "stream shards timed as the headline step (the paired form); "
                               "us_per_launch = one step")
+    # a learner's baseline evaluation: C3 with a RandomBot against a
+    # StaircaseBot (the paired mixed-bot form since round 5)
+    out["c3_mixed"] = dict(rollout_rate(cfg, 65536, (1, 2), streams=2),
+                           policy="RandomBot vs StaircaseBot", grid="64x64, 8 NPCs",
+                           note="two stream shards timed as the headline step (the paired "
+                                "PM 4 form); us_per_launch = one step")
     c5 = {}
     for flag in (0, EXT_SEPARATION_DAMAGE):
         c = EnvConfig.c5()
