@@ -42,6 +42,8 @@ VARIANTS = {
     "split1": ("ORX_SPLIT_TICK=1",),  # split tick blocks in the compact form (rejected)
     "split2": ("ORX_SPLIT_TICK=2",),  # split tick blocks in every paired RandomBot form (rejected)
     "sepw0": ("ORX_SEP_WAVES=0",),    # the separation-damage StaircaseBot form uncapped (131 VGPRs)
+    "envw5": ("ORX_ENV_WAVES=5",),    # orx_env_step_ex held to 5 waves per SIMD
+    "envw6": ("ORX_ENV_WAVES=6",),    # ... to 6
 }
 
 

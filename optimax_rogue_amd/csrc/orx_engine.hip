@@ -2035,13 +2035,15 @@ __global__ void __launch_bounds__(256) reset_kernel(orx_cfg_t hc, orx_state_t st
 // code compiled out -- fewer registers, so more waves per SIMD hide the
 // state loads (the per-tick drop-in's common case)
 // One game's Updater.update (or its autoreset): the per-tick step kernels'
-// body.  get_action(p1, p2, tick, ep) yields the game's packed action pair
+// body.  get_action(p1, p2, tick, ep, tb) yields the game's packed action pair
 // (player 1 in the low byte).  Without an output callback (NoOut: the step
 // kernels) it is called only for a game in progress, with p1 / p2 / tick /
-// ep not loaded.  With one (env_step_kernel) every state word is loaded up
-// front -- one round trip for the whole launch -- get_action sees the
-// pre-tick players for every game, and out(p1, p2, tick, status) receives the
-// post-step state from registers (no re-read of what was just stored).
+// ep / tb not loaded.  With one (env_step_kernel) every state word is loaded
+// up front -- one round trip for the whole launch -- get_action sees the
+// pre-tick players and the tick block for every game (one Philox block serves
+// player 2's RandomBot and the initiative draw), and out(p1, p2, tick,
+// status) receives the post-step state from registers (no re-read of what
+// was just stored).
 struct NoOut {
   __device__ __forceinline__ void operator()(const Player&, const Player&, int32_t, int32_t) {}
 };
@@ -2064,6 +2066,7 @@ __device__ __forceinline__ void step_game(const orx_cfg_t& hc, const orx_state_t
   uint16_t a = 0;
   Items<NCAP> items;
   int32_t sep = -1;
+  W4 tb0{0, 0, 0, 0};  // (kOut) the tick block: player 2's policy and the initiative draw
   if constexpr (kOut) {  // every state word in one round trip (a reset discards some)
     load_players<GRID>(st, B, i, p1, p2);
     tick = st.tick[i];
@@ -2071,7 +2074,8 @@ __device__ __forceinline__ void step_game(const orx_cfg_t& hc, const orx_state_t
     load_npcs(st, c, B, i, npc);
     load_rpg(st, c, B, i, p1, p2, npc, items);
     if (c.ext & ORX_EXT_SEPARATION_DAMAGE) sep = st.sep_start[i];
-    a = get_action(p1, p2, tick, ep);
+    tb0 = tick_block(key, game, ep, tick);
+    a = get_action(p1, p2, tick, ep, tb0);
   }
   if (status != ORX_IN_PROGRESS) {
     if (EV) n_events[i] = 0;
@@ -2095,7 +2099,7 @@ __device__ __forceinline__ void step_game(const orx_cfg_t& hc, const orx_state_t
     out(p1, p2, tick, status);
     return;
   }
-  if constexpr (!kOut) a = get_action(p1, p2, tick, ep);
+  if constexpr (!kOut) a = get_action(p1, p2, tick, ep, tb0);
   p1.move = (int8_t)(a & 0xFF);
   p2.move = (int8_t)(a >> 8);
   if (!valid_move(c, p1.move) || !valid_move(c, p2.move)) {
@@ -2116,7 +2120,8 @@ __device__ __forceinline__ void step_game(const orx_cfg_t& hc, const orx_state_t
   Deltas dl = {0, 0, 0, 0, 0, 0};
   Events<EV> ev{EV ? events + (size_t)i * ORX_MAX_EVENTS * 4 : nullptr, 0};
   bool err = false;
-  const bool p1_first = p1_first_draw(key, game, ep, tick, err);
+  const bool p1_first = kOut ? first_from_packed(tb0.a, key, game, ep, tick, err)
+                             : p1_first_draw(key, game, ep, tick, err);
   tick_game<NCAP, EV, GRID>(c, key, game, ep, p1_first, p1, p2, npc, items, m, tick, status, err,
                             dl, ev, sep);
   if (c.ext & ORX_EXT_SEPARATION_DAMAGE) st.sep_start[i] = sep;
@@ -2140,7 +2145,7 @@ __global__ void __launch_bounds__(256) step_kernel(orx_cfg_t hc, orx_state_t st,
   if (i >= B) return;
   step_game<NCAP, EV, GRID, EXT>(
       hc, st,
-      [&](const Player&, const Player&, int32_t, uint32_t) {
+      [&](const Player&, const Player&, int32_t, uint32_t, const W4&) {
         return reinterpret_cast<const uint16_t*>(actions)[i];
       },
       B, i, key, off, events, n_events);
@@ -2191,8 +2196,12 @@ __global__ void __launch_bounds__(256) policy_kernel(orx_state_t st, int32_t pol
 // segment -- written directly, a lane's 14 stores land 56 B apart and each
 // instruction touches 28 cache lines.  bad_count (may be NULL): += the games
 // whose actions were refused this tick (one atomic per wave that has any).
+#ifndef ORX_ENV_WAVES
+#define ORX_ENV_WAVES 1
+#endif
 template <int NCAP, bool GRID, bool EXT>
-__global__ void __launch_bounds__(256) env_step_kernel(
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORX_ENV_WAVES)))
+env_step_kernel(
     orx_cfg_t hc, orx_state_t st, const void* __restrict__ actions, int32_t dsize, int32_t cols,
     int32_t pol2, int8_t* __restrict__ act, int32_t* __restrict__ obs, float* __restrict__ reward,
     uint8_t* __restrict__ done, int32_t* __restrict__ status_out, uint32_t* __restrict__ bad_count,
@@ -2217,11 +2226,10 @@ __global__ void __launch_bounds__(256) env_step_kernel(
     const int32_t l2 = cols == 2 ? learner(2u * i + 1u) : (int32_t)ORX_MOVE_STAY;
     uint16_t pair = 0;
     int32_t before = ORX_IN_PROGRESS;
-    auto get_action = [&](const Player& p1, const Player& p2, int32_t tick, uint32_t ep) {
+    auto get_action = [&](const Player& p1, const Player& p2, int32_t tick, uint32_t ep,
+                          const W4& tb) {
       int32_t a1 = l1, a2 = l2;
       if (cols == 1 && pol2 != ORX_POLICY_STAY) {  // (orx_env_step refuses POLICY_NONE here)
-        const W4 tb = pol2 == ORX_POLICY_RANDOM ? tick_block(key, off + i, ep, tick)
-                                                : W4{0, 0, 0, 0};
         int32_t keep = a1;
         policy_pair(key, off + i, ep, tick, ORX_POLICY_NONE, pol2, tb, p1, p2, keep, a2);
       }

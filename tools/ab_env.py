@@ -1,0 +1,73 @@
+"""A/B of liborx builds on the learner's tick (diagnostics, round 5): for every
+library given, a fresh child process times orx_env_step_ex as bench.py's
+large_batch extra does (C3, int64 learner actions, RandomBot opponent,
+observation / reward / done / status / refused-action count; median of 30
+launches between HIP events) at 65,536 and 2^21 games, and VecEnv.step
+called eagerly from a ring of two output sets (400 ticks, wall clock).
+Libraries alternate over --reps rounds.
+
+    python tools/ab_env.py lib_a.so lib_b.so [--reps=3]
+"""
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def child(lib):
+    sys.path.insert(0, ROOT)
+    import ctypes
+    import torch
+    from bench import timed_launches
+    from optimax_rogue_amd import _lib, EnvConfig
+    _lib.LIB_PATH = os.path.abspath(lib)
+    _lib.ABI_VERSION = ctypes.CDLL(_lib.LIB_PATH).orx_abi_version()
+    from optimax_rogue_amd import VecEnv, OBS_FIELDS
+    from optimax_rogue_amd.engine import BatchedEngine
+    dev = torch.device("cuda", 0)
+    cfg = EnvConfig.c3()
+    out = {"lib": lib}
+    for B in (65536, 1 << 21):
+        eng = BatchedEngine(cfg, B, seed=3, device=dev)
+        for _ in range(2):
+            eng.step(eng.policy(1, 1))
+        la = torch.randint(1, 6, (B,), dtype=torch.int64, device=dev)
+        lo = torch.empty((B, len(OBS_FIELDS)), dtype=torch.int32, device=dev)
+        lr = torch.empty(B, dtype=torch.float32, device=dev)
+        ld = torch.empty(B, dtype=torch.bool, device=dev)
+        ls = torch.empty(B, dtype=torch.int32, device=dev)
+        lb = torch.zeros(1, dtype=torch.int32, device=dev)
+        t = sorted(timed_launches(torch, lambda: eng.env_step(la, 1, lo, lr, ld, ls, lb), 30))
+        out[f"env_{B}"] = round(t[len(t) // 2] * 1e6, 2)
+        del eng, la, lo, lr, ld, ls, lb
+        torch.cuda.empty_cache()
+    pool = torch.randint(1, 6, (16, 65536), dtype=torch.int64, device=dev)
+    env = VecEnv(cfg, 65536, seed=3, device=dev, opponent=1, out_buffers=2)
+    for k in range(20):
+        env.step(pool[k % 16])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(400):
+        env.step(pool[k % 16])
+    torch.cuda.synchronize()
+    out["vecenv_ring_us"] = round((time.perf_counter() - t0) / 400 * 1e6, 2)
+    print(json.dumps(out), flush=True)
+
+
+def main():
+    opts = dict(a[2:].split("=") for a in sys.argv[1:] if a.startswith("--") and "=" in a)
+    if "--child" in sys.argv:
+        return child(sys.argv[sys.argv.index("--child") + 1])
+    libs = [a for a in sys.argv[1:] if not a.startswith("--")]
+    for _ in range(int(opts.get("reps", 3))):
+        for lib in libs:
+            r = subprocess.run([sys.executable, __file__, "--child", lib], timeout=300)
+            if r.returncode:
+                sys.exit(r.returncode)
+
+
+if __name__ == "__main__":
+    main()

@@ -33,6 +33,14 @@ for s in $STEPS; do
     env)
       C5_FORMS=env timeout -k 10 300 python3 tools/c5_forms.py > $O/env_forms.jsonl 2> $O/env_forms.err
       rc=$?; echo "env rc=$rc"; fatal $rc env;;
+    envtests)
+      timeout -k 10 300 python3 -u -m pytest tests -m gpu -q -k "env_step or vecenv or VecEnv" \
+        --timeout 120 --timeout-method thread > $O/envtests.log 2>&1
+      rc=$?; echo "envtests rc=$rc"; tail -5 $O/envtests.log; fatal $rc envtests;;
+    abenv)
+      timeout -k 10 600 python3 tools/ab_env.py tools/ab_libs/base.so tools/ab_libs/cse.so \
+        tools/ab_libs/envw5.so tools/ab_libs/envw6.so --reps=3 > $O/ab_env.jsonl 2> $O/ab_env.err
+      rc=$?; echo "abenv rc=$rc"; cat $O/ab_env.jsonl; fatal $rc abenv;;
     c5)
       timeout -k 10 400 python3 tools/c5_forms.py > $O/c5_forms.jsonl 2> $O/c5_forms.err
       rc=$?; echo "c5 rc=$rc"; fatal $rc c5;;
