@@ -305,7 +305,11 @@ class BatchedEngine:
                    self.game_offset, self._stream())
         return self.status
 
-    _ACTION_BYTES = {torch.int8: 1, torch.int16: 2, torch.int32: 4, torch.int64: 8}
+    # learner action widths orx_env_step_ex reads (uint8 as int8: 1..6 read
+    # the same, and 128..255 become negative, i.e. refused like any other
+    # value outside the Move codes)
+    _ACTION_BYTES = {torch.int8: 1, torch.uint8: 1, torch.int16: 2, torch.int32: 4,
+                     torch.int64: 8}
 
     def env_step(self, actions: torch.Tensor, p2: int, obs: torch.Tensor, reward: torch.Tensor,
                  done: torch.Tensor, status: torch.Tensor,

@@ -146,9 +146,12 @@ class VecEnv:
             if n > self._bad_seen:
                 new, self._bad_seen = n - self._bad_seen, n
                 raise ValueError(self._bad_message(new))
+        # the copy runs on the counter's device's current stream (the stream
+        # orx_env_step_ex launches on), and the event is recorded there, not
+        # on whichever device happens to be current
         self._bad_host.copy_(self._bad_dev, non_blocking=True)
         self._bad_event = torch.cuda.Event()
-        self._bad_event.record()
+        self._bad_event.record(torch.cuda.current_stream(self.device))
 
     # -- reset / step / rollout ----------------------------------------------------
     def reset(self, mask: Optional[torch.Tensor] = None) -> torch.Tensor:

@@ -391,7 +391,8 @@ def test_vecenv_fused_step_equals_policy_step(case):
 
 def test_vecenv_bad_actions_truncate_on_device():
     """Values outside the Move codes (0, -1, 6 without EXT_HEAL, 257 as
-    int64 -- which an int8 cast would wrap to the legal 1) stop exactly
+    int64 -- which an int8 cast would wrap to the legal 1 -- and 128..255 as
+    uint8) stop exactly
     those games with STATUS_BAD_ACTION: done, reward 0, no host sync; the
     next step starts their next episode.  check_actions=True raises instead."""
     import torch
@@ -417,6 +418,17 @@ def test_vecenv_bad_actions_truncate_on_device():
     ep = env.engine.episode
     assert (ep[idx] == ep0[idx] + 1).all() and (ep[keep] == ep0[keep]).all()
     assert (obs[idx, 8] == 1).all()   # their next episode's first tick
+    # uint8 learner actions (read as int8): 0 and 128..255 are refused
+    u = torch.full((B,), 2, dtype=torch.uint8, device=dev)
+    ubad = {5: 0, 6: 128, 9: 255}
+    for k, v in ubad.items():
+        u[k] = v
+    obs, r, d, st = env.step(u)
+    uidx = torch.tensor(sorted(ubad), device=dev)
+    ukeep = torch.ones(B, dtype=torch.bool, device=dev)
+    ukeep[uidx] = False
+    assert (st[uidx] == STATUS_BAD_ACTION).all() and d[uidx].all()
+    assert (st[ukeep] == 1).all() and not d[ukeep].any()
     strict = VecEnv(EnvConfig(width=10, height=10), 8, seed=2, device=dev, check_actions=True)
     with pytest.raises(ValueError, match="Move values"):
         strict.step(torch.tensor([1, 2, 3, 4, 5, 0, 1, 1], device=dev))
