@@ -4178,14 +4178,18 @@ __global__ void __launch_bounds__(256) mt_rollout_kernel(orx_cfg_t hc, orx_state
 // episode when cfg.autoreset.  obs (may be NULL): each tick's post-step row,
 // in format fmt.  One lane per game (any dungeon, any NPC count, any
 // extension flag: the generic tick).
-template <int NCAP, bool GRID>
-__global__ void __launch_bounds__(256) step_n_kernel(orx_cfg_t hc, orx_state_t st,
-                                                     const int8_t* __restrict__ actions,
-                                                     int32_t n_ticks, int32_t* __restrict__ obs,
-                                                     uint32_t B, Key key, uint32_t off,
-                                                     int32_t fmt) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= B) return;
+//
+// ROWS (0 none, 1 int32, 2 compact) is a compile-time copy of (obs, fmt):
+// every path through the tick then issues the same row stores, so the wait
+// for the next tick's prefetched pair (issued before this tick's stores)
+// leaves this tick's stores in flight -- with the row branch at run time the
+// compiler's wait at the loop head has to assume a path without stores and
+// drains them all every tick.
+template <int NCAP, bool GRID, int ROWS>
+__device__ __forceinline__ void step_n_game(const orx_cfg_t& hc, const orx_state_t& st,
+                                            const int8_t* __restrict__ actions, int32_t n_ticks,
+                                            int32_t* __restrict__ obs, uint32_t B, uint32_t i,
+                                            Key key, uint32_t off) {
   const Cfg c = make_cfg(hc, st);
   const uint32_t game = off + i;
   Player p1, p2;
@@ -4202,10 +4206,21 @@ __global__ void __launch_bounds__(256) step_n_kernel(orx_cfg_t hc, orx_state_t s
   Deltas dl = {0, 0, 0, 0, 0, 0};
   int32_t sep = (c.ext & ORX_EXT_SEPARATION_DAMAGE) ? st.sep_start[i] : -1;
   bool stairs_dirty = false, npc_dirty = false;
-  TrajWriter<false> traj(obs, nullptr, B, i, fmt);
+  if constexpr (ROWS != 0) __builtin_assume(obs != nullptr);
+  TrajWriter<false> traj(ROWS != 0 ? obs : nullptr, nullptr, B, i,
+                         ROWS == 2 ? ORX_OBS_COMPACT : ORX_OBS_INT32);
   const uint16_t* a16 = reinterpret_cast<const uint16_t*>(actions) + i;
+  // the next tick's pair is loaded while this tick runs (a lone wave per SIMD
+  // would otherwise wait one HBM round trip per tick); the last tick re-reads
+  // its own pair instead of branching
+  uint16_t a_next = a16[0];
+  // settled before the loop (with the state loads), so that the loop head's
+  // wait sees only the back edge: the pair loaded one tick earlier, that
+  // tick's row stores issued after it
+  asm volatile("" : "+v"(a_next));
   for (int32_t t = 0; t < n_ticks; ++t) {
-    const uint16_t a = a16[(size_t)t * B];
+    const uint16_t a = a_next;
+    a_next = a16[(size_t)(t + 1 < n_ticks ? t + 1 : t) * B];
     const int32_t a1 = (int8_t)(a & 0xFF), a2 = (int8_t)(a >> 8);
     if (status == ORX_IN_PROGRESS) {
       p1.move = a1;
@@ -4230,7 +4245,7 @@ __global__ void __launch_bounds__(256) step_n_kernel(orx_cfg_t hc, orx_state_t s
       npc_dirty = true;
       sep = -1;
     }
-    traj.write(t, p1, p2, tick, status, a1, a2);
+    if constexpr (ROWS != 0) traj.write(t, p1, p2, tick, status, a1, a2);
   }
   store_players<GRID>(st, B, i, p1, p2, stairs_dirty);
   store_rpg(st, c, B, i, p1, p2, npc, items);
@@ -4240,6 +4255,22 @@ __global__ void __launch_bounds__(256) step_n_kernel(orx_cfg_t hc, orx_state_t s
   if (c.ext & ORX_EXT_SEPARATION_DAMAGE) st.sep_start[i] = sep;
   if (NCAP > 0 && (npc_dirty || dl.npc_death)) npc.store_alive(st.npc_alive, B, i);
   flush_deltas(st, B, i, dl);
+}
+
+template <int NCAP, bool GRID>
+__global__ void __launch_bounds__(256) step_n_kernel(orx_cfg_t hc, orx_state_t st,
+                                                     const int8_t* __restrict__ actions,
+                                                     int32_t n_ticks, int32_t* __restrict__ obs,
+                                                     uint32_t B, Key key, uint32_t off,
+                                                     int32_t fmt) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B) return;
+  if (obs == nullptr)  // (uniform)
+    step_n_game<NCAP, GRID, 0>(hc, st, actions, n_ticks, obs, B, i, key, off);
+  else if (fmt == ORX_OBS_COMPACT)
+    step_n_game<NCAP, GRID, 2>(hc, st, actions, n_ticks, obs, B, i, key, off);
+  else
+    step_n_game<NCAP, GRID, 1>(hc, st, actions, n_ticks, obs, B, i, key, off);
 }
 
 template <bool GRID>

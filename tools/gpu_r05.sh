@@ -41,6 +41,14 @@ for s in $STEPS; do
       timeout -k 10 600 python3 tools/ab_env.py tools/ab_libs/base.so tools/ab_libs/cse.so \
         tools/ab_libs/envw5.so tools/ab_libs/envw6.so --reps=3 > $O/ab_env.jsonl 2> $O/ab_env.err
       rc=$?; echo "abenv rc=$rc"; cat $O/ab_env.jsonl; fatal $rc abenv;;
+    replaytests)
+      timeout -k 10 300 python3 -u -m pytest tests -m gpu -q -k "step_n" \
+        --timeout 120 --timeout-method thread > $O/replaytests.log 2>&1
+      rc=$?; echo "replaytests rc=$rc"; tail -5 $O/replaytests.log; fatal $rc replaytests;;
+    abreplay)
+      timeout -k 10 600 python3 tools/ab_replay.py tools/ab_libs/base.so tools/ab_libs/pf2.so \
+        --reps=3 > $O/ab_replay.jsonl 2> $O/ab_replay.err
+      rc=$?; echo "abreplay rc=$rc"; cat $O/ab_replay.jsonl; fatal $rc abreplay;;
     c5)
       timeout -k 10 400 python3 tools/c5_forms.py > $O/c5_forms.jsonl 2> $O/c5_forms.err
       rc=$?; echo "c5 rc=$rc"; fatal $rc c5;;
