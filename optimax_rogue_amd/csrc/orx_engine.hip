@@ -2367,7 +2367,11 @@ __device__ __forceinline__ bool rare_tick(const Cfg& c, const orx_state_t& st, u
                                           int32_t& status, Deltas& dl, int32_t& sep,
                                           bool& restarted, const W4& tb, int need, int32_t t1x,
                                           int32_t t1y, int32_t t2x, int32_t t2y,
-                                          bool ext_ordered) {
+                                          bool ext_ordered, bool bad_action = false) {
+  if (bad_action) {  // a replay's pair outside the Move codes: the game stops (orx_step)
+    status = ORX_STATUS_BAD_ACTION;
+    return false;
+  }
   launder(t1x, t1y, t2x, t2y);
   launder(p1.x, p1.y, p2.x, p2.y);
   launder(p1.d, p2.d, p1.sx, p1.sy);
@@ -2638,7 +2642,12 @@ __device__ __forceinline__ bool rare_tick(const Cfg& c, const orx_state_t& st, u
 //    second against the first's new cell; an occupied target is a combat
 //    (every CombatFlag deals damage - armor: no Modifier exists) and the
 //    attacker stays; deaths override the status.
-template <int NCAP, bool GRID, class M>
+//
+// LOG (a replay, orx_step_n): the moves are given in a1 / a2 (pol1 = pol2 =
+// ORX_POLICY_NONE) -- a game in progress with a pair outside the Move codes
+// stops with ORX_STATUS_BAD_ACTION (the rare block, nothing else changes), and
+// a heal move (ORX_EXT_HEAL) takes the ordered tick, the only one that heals.
+template <int NCAP, bool GRID, class M, bool LOG = false>
 __device__ __forceinline__ void rollout_tick(const Cfg& c, const orx_state_t& st, uint32_t B,
                                              uint32_t i, Key key, uint32_t game, uint32_t& ep,
                                              int32_t pol1, int32_t pol2, Player& p1,
@@ -2670,7 +2679,9 @@ __device__ __forceinline__ void rollout_tick(const Cfg& c, const orx_state_t& st
   assign_moves(pol1, pol2, r0, r1, p1, p2, a1, a2);
   p1.move = a1;
   p2.move = a2;
-  const bool in_progress = status == ORX_IN_PROGRESS;
+  const bool bad = LOG && status == ORX_IN_PROGRESS && !(valid_move(c, a1) && valid_move(c, a2));
+  const bool heal = LOG && (c.ext & ORX_EXT_HEAL) && (a1 == ORX_MOVE_HEAL || a2 == ORX_MOVE_HEAL);
+  const bool in_progress = status == ORX_IN_PROGRESS && !bad;
 
   // effective targets: the player's own cell when staying or blocked.  Empty
   // dungeons: a move changes one coordinate by one, so a blocked target is
@@ -2722,7 +2733,7 @@ __device__ __forceinline__ void rollout_tick(const Cfg& c, const orx_state_t& st
   // stream fallback of an all-reject word, whose 4,096-word cap is the only
   // way it could matter there (p < 2^-4000) -- is consulted by the rare
   // block only, where the order is used.
-  const bool rare = !in_progress | meet | hit1 | hit2 | st1 | st2 | ext_ordered;
+  const bool rare = !in_progress | meet | hit1 | hit2 | st1 | st2 | ext_ordered | heal;
   const int32_t ft = tick + 1;
   const bool end = c.max_ticks && ft >= c.max_ticks;
 
@@ -2738,7 +2749,7 @@ __device__ __forceinline__ void rollout_tick(const Cfg& c, const orx_state_t& st
 #endif
     took_ordered = rare_tick<NCAP, GRID>(c, st, B, i, key, game, ep, p1, p2, npc, items, hp,
                                          tick, status, dl, sep, restarted, tb, need, t1x,
-                                         t1y, t2x, t2y, ext_ordered);
+                                         t1y, t2x, t2y, ext_ordered | heal, bad);
 #ifdef ORX_STAMPS
     ORX_CYC_END(dl.cy_rare, cy0);
 #endif
@@ -2827,8 +2838,9 @@ __device__ __forceinline__ uint32_t compact_ts(int32_t tick, int32_t status) {
   return (uint32_t)tick | ((uint32_t)status << 27);
 }
 
-// CF: the compact row format (FAST writers; the generic writer reads `fmt`)
-template <bool FAST, int AUX = kStreamAux, bool CF = false>
+// CF: the compact row format (FAST writers; the generic writer reads `fmt`);
+// ACT: a FAST writer also stores the action pair (a replay has its actions)
+template <bool FAST, int AUX = kStreamAux, bool CF = false, bool ACT = true>
 struct TrajWriter {
   static constexpr int kRows = CF ? ORX_OBS_COMPACT_FIELDS : ORX_OBS_FIELDS;
   int32_t* obs;
@@ -2874,10 +2886,13 @@ struct TrajWriter {
         for (int f = 0; f < kRows; ++f)
           __builtin_amdgcn_raw_buffer_store_b32(vals[f], ro, (int32_t)vo[f], 0, AUX);
       }
-      const auto ra = __builtin_amdgcn_make_buffer_rsrc(act, 0, (int32_t)(B * 2u), kBufferDword3);
-      __builtin_amdgcn_raw_buffer_store_b16(pack_actions(a1, a2), ra, (int32_t)va, 0, AUX);
+      if constexpr (ACT) {
+        const auto ra = __builtin_amdgcn_make_buffer_rsrc(act, 0, (int32_t)(B * 2u),
+                                                          kBufferDword3);
+        __builtin_amdgcn_raw_buffer_store_b16(pack_actions(a1, a2), ra, (int32_t)va, 0, AUX);
+        act += (size_t)2 * B;
+      }
       obs += (size_t)kRows * B;
-      act += (size_t)2 * B;
     } else {
       if (obs) {
         if (fmt == ORX_OBS_COMPACT) {
@@ -4273,6 +4288,65 @@ __global__ void __launch_bounds__(256) step_n_kernel(orx_cfg_t hc, orx_state_t s
     step_n_game<NCAP, GRID, 1>(hc, st, actions, n_ticks, obs, B, i, key, off);
 }
 
+// orx_step_n's fast form (register NPCs, empty dungeons: NCAP 0 / 8 / 16,
+// no bank): the rollout's tick (rollout_tick, LOG) on the logged pair -- the
+// order-free common path, every rare case in its out-of-line block, no policy
+// draw at all (the initiative block is drawn only by a game whose order
+// matters) -- with the rollout's register-resident NPC health and buffer-store
+// rows (ROWS 0 none, 1 int32, 2 compact; no action rows: the log is the
+// actions).  The next tick's pair is prefetched as in step_n_kernel.
+template <int NCAP, int ROWS>
+__global__ void __launch_bounds__(kRolloutBlock) replay_kernel(orx_cfg_t hc, orx_state_t st,
+                                                               const int8_t* __restrict__ actions,
+                                                               int32_t n_ticks,
+                                                               int32_t* __restrict__ obs,
+                                                               uint32_t B, Key key, uint32_t off) {
+  const uint32_t i = xcd_block() * blockDim.x + threadIdx.x;
+  if (i >= B) return;
+  const Cfg c = make_cfg(hc, st);
+  const uint32_t game = off + i;
+  Player p1, p2;
+  load_players<false>(st, B, i, p1, p2);
+  int32_t tick = st.tick[i];
+  int32_t status = st.status[i];
+  uint32_t ep = (uint32_t)st.episode[i];
+  Npcs<NCAP> npc;
+  npc.bind(st, c, B, i);
+  load_npcs(st, c, B, i, npc);
+  NpcHpRegs<NCAP> hp;
+  if constexpr (NCAP > 0) hp.load(st.npc_health, c.K, B, i);
+  Items<NCAP> items;
+  load_rpg(st, c, B, i, p1, p2, npc, items);
+  Deltas dl = {0, 0, 0, 0, 0, 0};
+  int32_t sep = (c.ext & ORX_EXT_SEPARATION_DAMAGE) ? st.sep_start[i] : -1;
+  bool restarted = false;
+  TrajWriter<true, kStreamAux, ROWS == 2, false> traj(ROWS != 0 ? obs : nullptr, nullptr, B, i);
+  const uint16_t* a16 = reinterpret_cast<const uint16_t*>(actions) + i;
+  uint16_t a_next = a16[0];   // (issued after the state loads: its wait covers them)
+  asm volatile("" : "+v"(a_next));
+  int32_t t = 0;
+  do {  // n_ticks >= 1: orx_step_n returns before launching 0 ticks
+    const uint16_t a = a_next;
+    a_next = a16[(size_t)(t + 1 < n_ticks ? t + 1 : t) * B];
+    int32_t a1 = (int8_t)(a & 0xFF), a2 = (int8_t)(a >> 8);
+    rollout_tick<NCAP, false, NpcHpRegs<NCAP>, true>(
+        c, st, B, i, key, game, ep, ORX_POLICY_NONE, ORX_POLICY_NONE, p1, p2, npc, items, hp,
+        tick, status, dl, sep, restarted, a1, a2);
+    if constexpr (ROWS != 0) traj.write(t, p1, p2, tick, status, a1, a2);
+  } while (++t < n_ticks);
+  store_players<false>(st, B, i, p1, p2, restarted || dl.descend != 0);
+  store_rpg(st, c, B, i, p1, p2, npc, items);
+  st.tick[i] = tick;
+  st.status[i] = status;
+  st.episode[i] = (int32_t)ep;
+  if (c.ext & ORX_EXT_SEPARATION_DAMAGE) st.sep_start[i] = sep;
+  if constexpr (NCAP > 0) {
+    if (restarted || dl.npc_death) npc.store_alive(st.npc_alive, B, i);
+    if (restarted || dl.combat) hp.store(st.npc_health, c.K, B, i);
+  }
+  flush_deltas(st, B, i, dl);
+}
+
 template <bool GRID>
 __global__ void __launch_bounds__(256) stairs_kernel(orx_cfg_t hc, orx_state_t st,
                                                      const uint32_t* __restrict__ games,
@@ -4313,6 +4387,9 @@ __global__ void __launch_bounds__(256) stairs_kernel(orx_cfg_t hc, orx_state_t s
   X(kDense, false, false) X(kDense, true, false) X(kDense, false, true) X(kDense, true, true)
 // NCAP: step_kernel<NCAP, false, false, false> (the reference's rules only)
 #define ORX_STEP_REF_LIST(X) X(0) X(8) X(16)
+// (NCAP, ROWS): replay_kernel
+#define ORX_REPLAY_LIST(X)                                                                      \
+  X(0, 0) X(0, 1) X(0, 2) X(8, 0) X(8, 1) X(8, 2) X(16, 0) X(16, 1) X(16, 2)
 // (NCAP, GRID, EXT): env_step_kernel
 #define ORX_ENV_LIST(X)                                                                         \
   X(0, false, false) X(8, false, false) X(16, false, false)                                     \
@@ -4406,6 +4483,10 @@ __global__ void __launch_bounds__(256) stairs_kernel(orx_cfg_t hc, orx_state_t s
   ORX_INST template __global__ void step_n_kernel<N, G>(orx_cfg_t, orx_state_t, const int8_t*,  \
                                                         int32_t, int32_t*, uint32_t, Key,       \
                                                         uint32_t, int32_t);
+#define ORX_I_REPLAY(N, R)                                                                      \
+  ORX_INST template __global__ void replay_kernel<N, R>(orx_cfg_t, orx_state_t, const int8_t*,  \
+                                                        int32_t, int32_t*, uint32_t, Key,       \
+                                                        uint32_t);
 #define ORX_I_STAIRS(G)                                                                         \
   ORX_INST template __global__ void stairs_kernel<G>(orx_cfg_t, orx_state_t, const uint32_t*,    \
                                                      const int32_t*, const int32_t*,            \
@@ -4462,6 +4543,7 @@ ORX_NG_LIST(ORX_I_RESET)
 ORX_NG_LIST(ORX_I_MT_RESET)
 ORX_NG_LIST(ORX_I_MT_ROLLOUT)
 ORX_NG_LIST(ORX_I_STEP_N)
+ORX_REPLAY_LIST(ORX_I_REPLAY)
 ORX_I_STAIRS(false)
 ORX_I_STAIRS(true)
 #endif
@@ -5006,6 +5088,21 @@ int orx_step_n(const orx_cfg_t* cfg, const orx_state_t* st, const int8_t* action
   const Key k = make_key(seed);
   const int nc = ncap_for(cfg->n_npcs);
   const bool grid = cfg->n_layouts > 0;
+  // register NPCs on empty dungeons: the rollout's tick on the logged pairs
+  // (ORX_STEP_N_GENERIC=1 forces the generic one, for A/B runs and tests)
+  const char* gen_env = getenv("ORX_STEP_N_GENERIC");
+  if (!grid && nc != kDense && !(gen_env && gen_env[0] == '1')) {
+    const int rows = obs ? (obs_format == ORX_OBS_COMPACT ? 2 : 1) : 0;
+    const dim3 g((unsigned)((B + kRolloutBlock - 1) / kRolloutBlock));
+#define ORX_REPLAY(N, R)                                                                        \
+    if (nc == N && rows == R) {                                                                 \
+      hipLaunchKernelGGL((replay_kernel<N, R>), g, dim3(kRolloutBlock), 0, s, *cfg, *st,        \
+                         actions, n_ticks, obs, B, k, off);                                     \
+      return launch_status("orx_step_n");                                                      \
+    }
+    ORX_REPLAY_LIST(ORX_REPLAY)
+#undef ORX_REPLAY
+  }
 #define ORX_STEP_N(N, G)                                                                        \
   if (nc == N && grid == G) {                                                                   \
     hipLaunchKernelGGL((step_n_kernel<N, G>), grid_for(B), dim3(kBlock), 0, s, *cfg, *st,       \

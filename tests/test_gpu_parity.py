@@ -1,5 +1,6 @@
 """GPU parity: the HIP engine against the reference's golden fixtures and the
 C oracle (bit-exact; all state is integer)."""
+import os
 import numpy as np
 import pytest
 
@@ -1144,6 +1145,12 @@ STEP_N_CASES = {
                         player_health=6), None),
     "sep_double": (dict(width=7, height=7, start_mode=2, p1_depth=0, p2_depth=1, max_ticks=0,
                         flags=3, sep_period=2, player_health=4), None),
+    "c3": (dict(width=64, height=64, n_npcs=8, max_ticks=1000), None),
+    "npc16_unused": (dict(width=20, height=14, n_npcs=16, npc_health=1, despawn=2, start_mode=2,
+                          p1_depth=0, p2_depth=2, max_ticks=120), None),
+    "heal_mana": (dict(width=8, height=8, n_npcs=4, max_ticks=50, flags=4 | 8,
+                       player_health=5), None),
+    "no_autoreset": (dict(width=6, height=6, n_npcs=2, max_ticks=40, autoreset=0), None),
 }
 
 
@@ -1152,7 +1159,11 @@ def test_step_n_equals_step(name):
     """orx_step_n over 160 ticks of random moves (~1% of them invalid: the
     game stops with STATUS_BAD_ACTION and restarts) equals 160 orx_step calls:
     the state after every tick (its observation row) and at the end; the
-    compact rows decode to the same rows."""
+    compact rows decode to the same rows, and a launch without rows ends in
+    the same state.  Register NPCs on empty dungeons take the fast form
+    (replay_kernel: the rollout's tick on the logged pairs), dense NPCs and
+    banks the generic one; ORX_STEP_N_GENERIC=1 forces the generic form on
+    the fast form's cases, with the same result."""
     import torch
     from optimax_rogue_amd.engine import decode_compact
     from optimax_rogue_amd.enums import EXT_HEAL, OBS_COMPACT, OBS_FIELDS
@@ -1178,6 +1189,19 @@ def test_step_n_equals_step(name):
         stops += int((snap["status"] == 16).sum())
     compare_state(eng.snapshot(), ref.snapshot(), int(cfg.get("n_npcs", 0)), f"{name} final")
     assert stops > 0
+    eng3 = _engine(cfg, B, seed, 11, layouts=lay)
+    eng3.step_n(a)
+    compare_state(eng3.snapshot(), ref.snapshot(), int(cfg.get("n_npcs", 0)), f"{name} no rows")
+    if bank is None and int(cfg.get("n_npcs", 0)) <= 16:
+        os.environ["ORX_STEP_N_GENERIC"] = "1"
+        try:
+            eng4 = _engine(cfg, B, seed, 11, layouts=lay)
+            g_obs = torch.zeros_like(obs)
+            eng4.step_n(a, obs=g_obs)
+            torch.cuda.synchronize()
+        finally:
+            del os.environ["ORX_STEP_N_GENERIC"]
+        assert np.array_equal(g_obs.cpu().numpy(), o), f"{name} generic form"
     if int(cfg.get("max_ticks", 0)) > 0 and not cfg.get("flags", 0) & 1:
         eng2 = _engine(cfg, B, seed, 11, layouts=lay)
         c_obs = torch.zeros((T, 6, B), dtype=torch.int32, device=eng.device)
