@@ -205,9 +205,11 @@ N_SEQ = int(os.environ.get("ORX_FUZZ_SEQ", "32"))
 def test_random_call_sequence_vs_oracle(case, oracle_lib, monkeypatch, tmp_path):
     """State hand-over between the entry points: a seeded random sequence of
     orx_step (given actions), orx_policy + orx_step, orx_rollout of 1-40 ticks,
-    masked orx_reset into a chosen episode and checkpoint/resume (save ->
-    load into a new engine) on one random configuration, against the oracle
-    doing the same, compared after every call."""
+    orx_step_n replaying a 1-40 tick move log (about 1% of its moves outside
+    the Move codes; keyed streams only), masked orx_reset into a chosen
+    episode and checkpoint/resume (save -> load into a new engine) on one
+    random configuration, against the oracle doing the same, compared after
+    every call."""
     import torch
     from optimax_rogue_amd import EnvConfig
     from optimax_rogue_amd.engine import BatchedEngine
@@ -224,8 +226,11 @@ def test_random_call_sequence_vs_oracle(case, oracle_lib, monkeypatch, tmp_path)
     hi = 7 if cfg["flags"] & HEAL else 6
     log = []
     for j in range(24):
-        op = rs.choice(["step", "policy", "rollout", "reset", "resume"], p=[.25, .2, .35, .12, .08])
+        op = rs.choice(["step", "policy", "rollout", "replay", "reset", "resume"],
+                       p=[.2, .15, .3, .15, .12, .08])
         p = (int(rs.choice([1, 2, 3])), int(rs.choice([1, 2, 3])))
+        if op == "replay" and cfg.get("rng"):
+            op = "step"   # (orx_step_n refuses stock-seed mode)
         if op == "step":
             a = rs.randint(1, hi, size=(B, 2)).astype(np.int8)
             ora.step(a)
@@ -236,6 +241,15 @@ def test_random_call_sequence_vs_oracle(case, oracle_lib, monkeypatch, tmp_path)
             got = eng.policy(*p)
             assert np.array_equal(got.cpu().numpy(), a), f"{where} {log} policy"
             eng.step(got)
+        elif op == "replay":
+            n = int(rs.randint(1, 41))
+            acts = rs.randint(1, hi, size=(n, B, 2)).astype(np.int8)
+            bad = rs.rand(n, B, 2) < 0.01
+            acts[bad] = rs.choice([0, -1, hi, 99], size=int(bad.sum())).astype(np.int8)
+            for t in range(n):
+                ora.step(acts[t])
+            eng.step_n(torch.from_numpy(acts).to(dev).contiguous())
+            op = f"replay{n}"
         elif op == "rollout":
             n = int(rs.randint(1, 41))
             for _ in range(n):
