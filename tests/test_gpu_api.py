@@ -326,14 +326,14 @@ def test_vecenv_reset_starts_next_episodes(oracle_lib):
 
 
 @pytest.mark.parametrize("case", ["c3_int64", "selfplay_int32", "stairs_opponent", "dense_bank",
-                                  "heal_ext"])
+                                  "heal_ext", "sep_double_npc16"])
 def test_vecenv_fused_step_equals_policy_step(case):
     """VecEnv.step (one orx_env_step launch, no host sync) against the
     unfused engine calls it replaces -- orx_policy for player 2, orx_step,
     then VecEnv.outcome and observe() on the host side of the comparison --
     for int8..int64 learner actions, self-play, both opponent policies,
     register / dense NPCs, a dungeon bank and the character extensions
-    (actions 6 = heal valid)."""
+    (actions 6 = heal valid), separation damage with double deaths."""
     import torch
     from optimax_rogue_amd import DungeonBank, EnvConfig, VecEnv
     from optimax_rogue_amd.engine import BatchedEngine
@@ -342,6 +342,10 @@ def test_vecenv_fused_step_equals_policy_step(case):
     layouts = None
     if case == "c3_int64":
         cfg, opp, dt, hi = EnvConfig(width=64, height=64, n_npcs=8, max_ticks=40), 1, torch.int64, 5
+    elif case == "sep_double_npc16":
+        cfg, opp, dt, hi = EnvConfig(width=9, height=8, n_npcs=14, npc_health=1, max_ticks=0,
+                                     start_mode=2, p1_depth=0, p2_depth=1, flags=1 | 2,
+                                     sep_period=3, player_health=5), 2, torch.int32, 5
     elif case == "selfplay_int32":
         cfg, opp, dt, hi = EnvConfig(width=8, height=7, n_npcs=3, max_ticks=30,
                                      player_health=3), None, torch.int32, 5

@@ -4,6 +4,7 @@ large_batch extra does (C3, int64 learner actions, RandomBot opponent,
 observation / reward / done / status / refused-action count; median of 30
 launches between HIP events) at 65,536 and 2^21 games, and VecEnv.step
 called eagerly from a ring of two output sets (400 ticks, wall clock).
+Also each size as 200 (2^21: 20) back-to-back launches between two events.
 Libraries alternate over --reps rounds.
 
     python tools/ab_env.py lib_a.so lib_b.so [--reps=3]
@@ -40,8 +41,18 @@ def child(lib):
         ld = torch.empty(B, dtype=torch.bool, device=dev)
         ls = torch.empty(B, dtype=torch.int32, device=dev)
         lb = torch.zeros(1, dtype=torch.int32, device=dev)
-        t = sorted(timed_launches(torch, lambda: eng.env_step(la, 1, lo, lr, ld, ls, lb), 30))
+        go = lambda: eng.env_step(la, 1, lo, lr, ld, ls, lb)
+        t = sorted(timed_launches(torch, go, 30))
         out[f"env_{B}"] = round(t[len(t) // 2] * 1e6, 2)
+        # back to back: 200 launches between two events
+        n = 200 if B <= 65536 else 20
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(n):
+            go()
+        b.record()
+        torch.cuda.synchronize()
+        out[f"env_{B}_b2b"] = round(a.elapsed_time(b) * 1e3 / n, 2)
         del eng, la, lo, lr, ld, ls, lb
         torch.cuda.empty_cache()
     pool = torch.randint(1, 6, (16, 65536), dtype=torch.int64, device=dev)

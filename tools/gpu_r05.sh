@@ -38,8 +38,8 @@ for s in $STEPS; do
         --timeout 120 --timeout-method thread > $O/envtests.log 2>&1
       rc=$?; echo "envtests rc=$rc"; tail -5 $O/envtests.log; fatal $rc envtests;;
     abenv)
-      timeout -k 10 600 python3 tools/ab_env.py tools/ab_libs/base.so tools/ab_libs/cse.so \
-        tools/ab_libs/envw5.so tools/ab_libs/envw6.so --reps=3 > $O/ab_env.jsonl 2> $O/ab_env.err
+      timeout -k 10 600 python3 tools/ab_env.py optimax_rogue_amd/liborx.so --reps=3 \
+        > $O/ab_env.jsonl 2> $O/ab_env.err
       rc=$?; echo "abenv rc=$rc"; cat $O/ab_env.jsonl; fatal $rc abenv;;
     replaytests)
       timeout -k 10 300 python3 -u -m pytest tests -m gpu -q -k "step_n" \
