@@ -2865,6 +2865,11 @@ struct TrajWriter {
       asm volatile("" : "+v"(va));
     }
   }
+  // a FAST writer's next rows
+  __device__ __forceinline__ void skip() {
+    obs += (size_t)kRows * B;
+    if constexpr (ACT) act += (size_t)2 * B;
+  }
   // row t, the next row of a FAST writer
   __device__ __forceinline__ void write(int32_t t, const Player& p1, const Player& p2,
                                         int32_t tick, int32_t status, int32_t a1, int32_t a2) {
@@ -2890,9 +2895,8 @@ struct TrajWriter {
         const auto ra = __builtin_amdgcn_make_buffer_rsrc(act, 0, (int32_t)(B * 2u),
                                                           kBufferDword3);
         __builtin_amdgcn_raw_buffer_store_b16(pack_actions(a1, a2), ra, (int32_t)va, 0, AUX);
-        act += (size_t)2 * B;
       }
-      obs += (size_t)kRows * B;
+      skip();
     } else {
       if (obs) {
         if (fmt == ORX_OBS_COMPACT) {
@@ -3014,6 +3018,10 @@ __global__ void __launch_bounds__(kRolloutBlock) rollout_kernel(orx_cfg_t hc, or
 #endif
   ORX_STAMP(1);
   int32_t t = 0;
+  // the FAST writers' exit test on the row pointer (a scalar register; a test
+  // on t gets t a VGPR: 2 VALU a tick, as in pair_rollout_kernel)
+  const int32_t* const obs_end =
+      kTraj ? obs + (size_t)n_ticks * TrajWriter<kTraj, AUX, CF>::kRows * B : nullptr;
   do {  // n_ticks >= 1: orx_rollout returns before launching 0 ticks
 #ifdef ORX_STAMPS
     if (t == 64) { ORX_STAMP(2); }
@@ -3023,7 +3031,9 @@ __global__ void __launch_bounds__(kRolloutBlock) rollout_kernel(orx_cfg_t hc, or
       rollout_tick<NCAP, GRID>(c, st, B, i, key, game, ep, pol1, pol2, p1, p2, npc, items, hp,
                                tick, status, dl, sep, restarted, a1, a2);
     if (!(ORX_DIAG & 16)) traj.write(t, p1, p2, tick, status, a1, a2);
-  } while (++t < n_ticks);
+    else if constexpr (kTraj) traj.skip();
+    ++t;
+  } while (kTraj ? traj.obs != obs_end : t < n_ticks);
   ORX_STAMP(3);
   store_players<GRID>(st, B, i, p1, p2, restarted || dl.descend != 0);
   store_rpg(st, c, B, i, p1, p2, npc, items);
@@ -3175,6 +3185,9 @@ struct PairWriter {
     }
     const auto ra = __builtin_amdgcn_make_buffer_rsrc(act, 0, (int32_t)(B * 2u), kBufferDword3);
     __builtin_amdgcn_raw_buffer_store_b8((uint8_t)move, ra, (int32_t)va, 0, AUX);
+    skip();
+  }
+  __device__ __forceinline__ void skip() {  // the next tick's rows
     obs += (size_t)kRows * B;
     act += (size_t)2 * B;
   }
@@ -3291,6 +3304,7 @@ __global__ void __launch_bounds__(GRID ? 512 : kRolloutBlock) ORX_PAIR_ATTR
   const bool rb_lane = kMixed && (isB == (PM == 5));
   constexpr int need = (PM == 1 || PM == 3) ? 2 : kMixed ? 1 : 0;
   PairWriter<AUX, CF> traj(obs, act, B, i, who);
+  const int32_t* const obs_end = obs + (size_t)n_ticks * PairWriter<AUX, CF>::kRows * B;
   // every state load resolved before the tick loop: a value first read in the
   // loop leaves its load pending at the loop head, and that wait then also
   // covers the previous ticks' row stores (vmcnt counts both) -- each tick
@@ -3858,7 +3872,12 @@ __global__ void __launch_bounds__(GRID ? 512 : kRolloutBlock) ORX_PAIR_ATTR
       span = status == ORX_IN_PROGRESS ? sp : 0;
     }
     if (!(ORX_DIAG & 16)) traj.write(me, kp, ks, isB, tick, status, move);
-    } while (++t < n_ticks);
+    else traj.skip();
+    ++t;
+    // the loop's exit test on the row pointer (a scalar register): a test on
+    // t alone gets t a VGPR and costs 2 VALU a tick (the compiler takes the
+    // counter for divergent in this loop)
+    } while (traj.obs != obs_end);
   ORX_STAMP(3);
   st.p_x[who * B + i] = me.x;
   st.p_y[who * B + i] = me.y;

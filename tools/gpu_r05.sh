@@ -49,6 +49,13 @@ for s in $STEPS; do
       timeout -k 10 600 python3 tools/ab_replay.py optimax_rogue_amd/liborx.so --forms \
         --reps=3 > $O/ab_replay.jsonl 2> $O/ab_replay.err
       rc=$?; echo "abreplay rc=$rc"; cat $O/ab_replay.jsonl; fatal $rc abreplay;;
+    abptr)
+      timeout -k 10 500 python3 tools/ab_forms.py tools/ab_libs/base.so tools/ab_libs/ptr.so \
+        --reps=3 > $O/ab_forms.jsonl 2> $O/ab_forms.err
+      rc=$?; echo "abforms rc=$rc"; cat $O/ab_forms.jsonl; fatal $rc abforms
+      timeout -k 10 500 python3 tools/ab_c5.py tools/ab_libs/base.so tools/ab_libs/ptr.so \
+        --reps=2 > $O/ab_c5.jsonl 2> $O/ab_c5.err
+      rc=$?; echo "abc5 rc=$rc"; cat $O/ab_c5.jsonl; fatal $rc abc5;;
     c5)
       timeout -k 10 400 python3 tools/c5_forms.py > $O/c5_forms.jsonl 2> $O/c5_forms.err
       rc=$?; echo "c5 rc=$rc"; fatal $rc c5;;

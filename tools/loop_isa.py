@@ -16,7 +16,7 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SRC = os.path.join(ROOT, "optimax_rogue_amd", "csrc", "orx_engine.hip")
+SRC = os.environ.get("ORX_SRC", os.path.join(ROOT, "optimax_rogue_amd", "csrc", "orx_engine.hip"))
 
 
 def assemble(defs):
