@@ -4319,8 +4319,13 @@ __global__ void __launch_bounds__(kRolloutBlock) replay_kernel(orx_cfg_t hc, orx
                                                                const int8_t* __restrict__ actions,
                                                                int32_t n_ticks,
                                                                int32_t* __restrict__ obs,
-                                                               uint32_t B, Key key, uint32_t off) {
-  const uint32_t i = xcd_block() * blockDim.x + threadIdx.x;
+                                                               uint32_t B, Key key, uint32_t off,
+                                                               uint32_t lanes) {
+  uint32_t i = xcd_block() * blockDim.x + threadIdx.x;
+  if (lanes < 64u) {  // uniform: lanes >= `lanes` of every wave idle (as rollout_kernel)
+    if ((threadIdx.x & 63u) >= lanes) return;
+    i = (i >> 6) * lanes + (threadIdx.x & 63u);
+  }
   if (i >= B) return;
   const Cfg c = make_cfg(hc, st);
   const uint32_t game = off + i;
@@ -4505,7 +4510,7 @@ __global__ void __launch_bounds__(256) stairs_kernel(orx_cfg_t hc, orx_state_t s
 #define ORX_I_REPLAY(N, R)                                                                      \
   ORX_INST template __global__ void replay_kernel<N, R>(orx_cfg_t, orx_state_t, const int8_t*,  \
                                                         int32_t, int32_t*, uint32_t, Key,       \
-                                                        uint32_t);
+                                                        uint32_t, uint32_t);
 #define ORX_I_STAIRS(G)                                                                         \
   ORX_INST template __global__ void stairs_kernel<G>(orx_cfg_t, orx_state_t, const uint32_t*,    \
                                                      const int32_t*, const int32_t*,            \
@@ -5112,11 +5117,13 @@ int orx_step_n(const orx_cfg_t* cfg, const orx_state_t* st, const int8_t* action
   const char* gen_env = getenv("ORX_STEP_N_GENERIC");
   if (!grid && nc != kDense && !(gen_env && gen_env[0] == '1')) {
     const int rows = obs ? (obs_format == ORX_OBS_COMPACT ? 2 : 1) : 0;
-    const dim3 g((unsigned)((B + kRolloutBlock - 1) / kRolloutBlock));
+    const uint32_t lanes = rollout_lanes(B);  // games per wave, as the rollout's plan
+    const uint64_t threads = (((uint64_t)B + lanes - 1) / lanes) * 64u;
+    const dim3 g((unsigned)((threads + kRolloutBlock - 1) / kRolloutBlock));
 #define ORX_REPLAY(N, R)                                                                        \
     if (nc == N && rows == R) {                                                                 \
       hipLaunchKernelGGL((replay_kernel<N, R>), g, dim3(kRolloutBlock), 0, s, *cfg, *st,        \
-                         actions, n_ticks, obs, B, k, off);                                     \
+                         actions, n_ticks, obs, B, k, off, lanes);                              \
       return launch_status("orx_step_n");                                                      \
     }
     ORX_REPLAY_LIST(ORX_REPLAY)

@@ -4,9 +4,10 @@ library given, a fresh child process replays a 128-tick move log (int8
 replay_step_n extra does (median of 10 launches between HIP events), with
 int32 rows, compact rows and no rows.  Libraries alternate over --reps rounds;
 --forms also times each library with ORX_STEP_N_GENERIC=1 (the generic
-one-lane tick instead of the fast replay form).
+one-lane tick instead of the fast replay form); --lanes=32,64 times each
+games-per-wave override (ORX_ROLLOUT_LANES) in turn.
 
-    python tools/ab_replay.py lib_a.so lib_b.so [--reps=3] [--forms]
+    python tools/ab_replay.py lib_a.so lib_b.so [--reps=3] [--forms] [--lanes=32,64]
 """
 import json
 import os
@@ -28,7 +29,8 @@ def child(lib):
     from optimax_rogue_amd.enums import OBS_COMPACT, OBS_INT32
     dev = torch.device("cuda", 0)
     B, T = 65536, 128
-    out = {"lib": lib, "generic_env": os.environ.get("ORX_STEP_N_GENERIC", "0")}
+    out = {"lib": lib, "generic_env": os.environ.get("ORX_STEP_N_GENERIC", "0"),
+           "lanes_env": os.environ.get("ORX_ROLLOUT_LANES", "")}
     eng = BatchedEngine(EnvConfig.c3(), B, seed=3, device=dev)
     log = torch.randint(1, 6, (T, B, 2), dtype=torch.int8, device=dev)
     for name, fmt in (("int32", OBS_INT32), ("compact", OBS_COMPACT), ("none", None)):
@@ -48,14 +50,18 @@ def main():
         return child(sys.argv[sys.argv.index("--child") + 1])
     libs = [a for a in sys.argv[1:] if not a.startswith("--")]
     envs = ("0", "1") if "--forms" in sys.argv else ("0",)
+    lanes = opts["lanes"].split(",") if "lanes" in opts else [""]
     for _ in range(int(opts.get("reps", 3))):
         for lib in libs:
             for g in envs:
-                env = dict(os.environ, ORX_STEP_N_GENERIC=g)
-                r = subprocess.run([sys.executable, __file__, "--child", lib], timeout=300,
-                                   env=env)
-                if r.returncode:
-                    sys.exit(r.returncode)
+                for ln in lanes:
+                    env = dict(os.environ, ORX_STEP_N_GENERIC=g)
+                    if ln:
+                        env["ORX_ROLLOUT_LANES"] = ln
+                    r = subprocess.run([sys.executable, __file__, "--child", lib], timeout=300,
+                                       env=env)
+                    if r.returncode:
+                        sys.exit(r.returncode)
 
 
 if __name__ == "__main__":

@@ -46,8 +46,8 @@ for s in $STEPS; do
         --timeout 120 --timeout-method thread > $O/replaytests.log 2>&1
       rc=$?; echo "replaytests rc=$rc"; tail -5 $O/replaytests.log; fatal $rc replaytests;;
     abreplay)
-      timeout -k 10 600 python3 tools/ab_replay.py optimax_rogue_amd/liborx.so --forms \
-        --reps=3 > $O/ab_replay.jsonl 2> $O/ab_replay.err
+      timeout -k 10 600 python3 tools/ab_replay.py optimax_rogue_amd/liborx.so \
+        --lanes=64,32,16 --reps=2 > $O/ab_replay.jsonl 2> $O/ab_replay.err
       rc=$?; echo "abreplay rc=$rc"; cat $O/ab_replay.jsonl; fatal $rc abreplay;;
     abptr)
       timeout -k 10 500 python3 tools/ab_forms.py tools/ab_libs/base.so tools/ab_libs/ptr.so \
@@ -56,6 +56,12 @@ for s in $STEPS; do
       timeout -k 10 500 python3 tools/ab_c5.py tools/ab_libs/base.so tools/ab_libs/ptr.so \
         --reps=2 > $O/ab_c5.jsonl 2> $O/ab_c5.err
       rc=$?; echo "abc5 rc=$rc"; cat $O/ab_c5.jsonl; fatal $rc abc5;;
+    stamps5)
+      for c in c5 c5sep; do
+        STAMPS_CFG=$c timeout -k 10 120 python3 tools/stamps.py \
+          tools/ab_libs/stamps.so 16384 128 > $O/stamps_${c}_16384.json 2> $O/stamps_$c.err
+        rc=$?; echo "stamps $c rc=$rc"; fatal $rc stamps
+      done;;
     c5)
       timeout -k 10 400 python3 tools/c5_forms.py > $O/c5_forms.jsonl 2> $O/c5_forms.err
       rc=$?; echo "c5 rc=$rc"; fatal $rc c5;;
