@@ -4314,7 +4314,7 @@ __global__ void __launch_bounds__(256) step_n_kernel(orx_cfg_t hc, orx_state_t s
 // matters) -- with the rollout's register-resident NPC health and buffer-store
 // rows (ROWS 0 none, 1 int32, 2 compact; no action rows: the log is the
 // actions).  The next tick's pair is prefetched as in step_n_kernel.
-template <int NCAP, int ROWS>
+template <int NCAP, int ROWS, bool EXT>
 __global__ void __launch_bounds__(kRolloutBlock) replay_kernel(orx_cfg_t hc, orx_state_t st,
                                                                const int8_t* __restrict__ actions,
                                                                int32_t n_ticks,
@@ -4327,7 +4327,8 @@ __global__ void __launch_bounds__(kRolloutBlock) replay_kernel(orx_cfg_t hc, orx
     i = (i >> 6) * lanes + (threadIdx.x & 63u);
   }
   if (i >= B) return;
-  const Cfg c = make_cfg(hc, st);
+  Cfg c = make_cfg(hc, st);
+  if constexpr (!EXT) c.ext = 0;  // launched only with flags == 0
   const uint32_t game = off + i;
   Player p1, p2;
   load_players<false>(st, B, i, p1, p2);
@@ -4411,9 +4412,12 @@ __global__ void __launch_bounds__(256) stairs_kernel(orx_cfg_t hc, orx_state_t s
   X(kDense, false, false) X(kDense, true, false) X(kDense, false, true) X(kDense, true, true)
 // NCAP: step_kernel<NCAP, false, false, false> (the reference's rules only)
 #define ORX_STEP_REF_LIST(X) X(0) X(8) X(16)
-// (NCAP, ROWS): replay_kernel
-#define ORX_REPLAY_LIST(X)                                                                      \
-  X(0, 0) X(0, 1) X(0, 2) X(8, 0) X(8, 1) X(8, 2) X(16, 0) X(16, 1) X(16, 2)
+// (NCAP, ROWS, EXT): replay_kernel (EXT false: flags 0, the extension tests
+// compiled out of the common tick)
+#define ORX_REPLAY_LIST_E(X, E)                                                                 \
+  X(0, 0, E) X(0, 1, E) X(0, 2, E) X(8, 0, E) X(8, 1, E) X(8, 2, E) X(16, 0, E) X(16, 1, E)      \
+  X(16, 2, E)
+#define ORX_REPLAY_LIST(X) ORX_REPLAY_LIST_E(X, false) ORX_REPLAY_LIST_E(X, true)
 // (NCAP, GRID, EXT): env_step_kernel
 #define ORX_ENV_LIST(X)                                                                         \
   X(0, false, false) X(8, false, false) X(16, false, false)                                     \
@@ -4507,10 +4511,10 @@ __global__ void __launch_bounds__(256) stairs_kernel(orx_cfg_t hc, orx_state_t s
   ORX_INST template __global__ void step_n_kernel<N, G>(orx_cfg_t, orx_state_t, const int8_t*,  \
                                                         int32_t, int32_t*, uint32_t, Key,       \
                                                         uint32_t, int32_t);
-#define ORX_I_REPLAY(N, R)                                                                      \
-  ORX_INST template __global__ void replay_kernel<N, R>(orx_cfg_t, orx_state_t, const int8_t*,  \
-                                                        int32_t, int32_t*, uint32_t, Key,       \
-                                                        uint32_t, uint32_t);
+#define ORX_I_REPLAY(N, R, E)                                                                   \
+  ORX_INST template __global__ void replay_kernel<N, R, E>(orx_cfg_t, orx_state_t,              \
+                                                           const int8_t*, int32_t, int32_t*,    \
+                                                           uint32_t, Key, uint32_t, uint32_t);
 #define ORX_I_STAIRS(G)                                                                         \
   ORX_INST template __global__ void stairs_kernel<G>(orx_cfg_t, orx_state_t, const uint32_t*,    \
                                                      const int32_t*, const int32_t*,            \
@@ -5120,9 +5124,9 @@ int orx_step_n(const orx_cfg_t* cfg, const orx_state_t* st, const int8_t* action
     const uint32_t lanes = rollout_lanes(B);  // games per wave, as the rollout's plan
     const uint64_t threads = (((uint64_t)B + lanes - 1) / lanes) * 64u;
     const dim3 g((unsigned)((threads + kRolloutBlock - 1) / kRolloutBlock));
-#define ORX_REPLAY(N, R)                                                                        \
-    if (nc == N && rows == R) {                                                                 \
-      hipLaunchKernelGGL((replay_kernel<N, R>), g, dim3(kRolloutBlock), 0, s, *cfg, *st,        \
+#define ORX_REPLAY(N, R, E)                                                                     \
+    if (nc == N && rows == R && (cfg->flags != 0) == E) {                                       \
+      hipLaunchKernelGGL((replay_kernel<N, R, E>), g, dim3(kRolloutBlock), 0, s, *cfg, *st,     \
                          actions, n_ticks, obs, B, k, off, lanes);                              \
       return launch_status("orx_step_n");                                                      \
     }

@@ -46,8 +46,8 @@ for s in $STEPS; do
         --timeout 120 --timeout-method thread > $O/replaytests.log 2>&1
       rc=$?; echo "replaytests rc=$rc"; tail -5 $O/replaytests.log; fatal $rc replaytests;;
     abreplay)
-      timeout -k 10 600 python3 tools/ab_replay.py optimax_rogue_amd/liborx.so \
-        --lanes=64,32,16 --reps=2 > $O/ab_replay.jsonl 2> $O/ab_replay.err
+      timeout -k 10 600 python3 tools/ab_replay.py tools/ab_libs/base.so tools/ab_libs/ptr.so \
+        --reps=3 > $O/ab_replay.jsonl 2> $O/ab_replay.err
       rc=$?; echo "abreplay rc=$rc"; cat $O/ab_replay.jsonl; fatal $rc abreplay;;
     abptr)
       timeout -k 10 500 python3 tools/ab_forms.py tools/ab_libs/base.so tools/ab_libs/ptr.so \
