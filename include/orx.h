@@ -221,6 +221,10 @@ extern "C" {
  *   EmptyDungeonGenerator(width, height)           worldgen.py:29-43
  *   Together/SeparatedGameStartGenerator(...)      worldgen.py:61-135
  *   Entity(iden, depth, x, y, 10, 10, 2, 1, ...)   worldgen.py:85-86        */
+/* sep_period's bound: the damage ceil(k / sep_period) stays exact in 31-bit
+ * arithmetic for every tick count below 2^31 - 2^24 */
+#define ORX_SEP_PERIOD_MAX 16777216 /* 2^24 */
+
 typedef struct orx_cfg {
   int32_t width;          /* W >= 4  (np.random.randint(1, W-2) needs W > 3) */
   int32_t height;         /* H >= 4                                          */
@@ -243,7 +247,8 @@ typedef struct orx_cfg {
                              layout bank: spawn_dungeon(depth) returns layout
                              randint(L) of orx_state_t.bank_* (an explicit-
                              grid DungeonGenerator plugin, worldgen.py:9-26) */
-  int32_t sep_period;     /* ORX_EXT_SEPARATION_DAMAGE: ticks per +1 damage   */
+  int32_t sep_period;     /* ORX_EXT_SEPARATION_DAMAGE: ticks per +1 damage,
+                             1..ORX_SEP_PERIOD_MAX                           */
   int32_t rng;            /* ORX_RNG_*                                       */
   /* character mechanics (ORX_EXT_MANA / HEAL / LEVELING / ITEMS)            */
   int32_t mana_max;       /* manabar size (>= 3 with MANA)                   */

@@ -309,6 +309,12 @@ struct Cfg {  // device copy of orx_cfg_t plus derived constants (all wave-unifo
   // n < 2^16 (error < n / 2^32 <= 1/d), so set only when the dividends
   // (interior / grid cell indices) stay below 2^16; 0 = divide
   uint32_t ih_magic, h_magic;
+  // separation damage's ceil(k / sep_period) as a multiply: for every
+  // n < 2^31, n / P == (n * sep_m) >> sep_sh with l = ceil(log2 P),
+  // sep_m = floor(2^(31+l) / P) + 1 < 2^32, sep_sh = 31 + l (the error term
+  // n * (sep_m * P - 2^(31+l)) / (P * 2^(31+l)) stays below 1/P)
+  uint32_t sep_m;
+  int32_t sep_sh;
   NpBound ground;    // randint(n_ground), n_ground = (W-2)(H-2) - 1
   NpBound stair_x;   // randint(1, W-2)
   NpBound stair_y;   // randint(1, H-2)
@@ -1959,6 +1965,12 @@ __device__ __forceinline__ void flush_deltas(const orx_state_t& st, uint32_t B, 
   }
 }
 
+// ceil(k / sep_period) for 1 <= k, k + sep_period - 1 < 2^31 (Cfg::sep_m)
+__device__ __forceinline__ int32_t sep_ceil(const Cfg& c, int32_t k) {
+  const uint32_t n = (uint32_t)(k + c.sep_period - 1);
+  return (int32_t)(((uint64_t)n * c.sep_m) >> c.sep_sh);
+}
+
 __device__ __forceinline__ Cfg make_cfg(const orx_cfg_t& h, const orx_state_t& st) {
   Cfg c;
   c.W = h.width; c.H = h.height; c.despawn = h.despawn; c.max_ticks = h.max_ticks;
@@ -1970,6 +1982,12 @@ __device__ __forceinline__ Cfg make_cfg(const orx_cfg_t& h, const orx_state_t& s
   c.autoreset = h.autoreset;
   c.ext = h.flags;
   c.sep_period = h.sep_period > 0 ? h.sep_period : 1;
+  {
+    const uint32_t P = (uint32_t)c.sep_period;
+    const int32_t l = P > 1u ? 32 - __clz(P - 1u) : 0;
+    c.sep_sh = 31 + l;
+    c.sep_m = (uint32_t)((1ull << (31 + l)) / P) + 1u;
+  }
   c.player_dmg = h.player_damage; c.player_armor = h.player_armor;
   c.mana_max = h.mana_max; c.mana_third = h.mana_max / 3; c.mana_regen = h.mana_regen;
   c.mana_pp = h.mana_per_point > 0 ? h.mana_per_point : 1;
@@ -2784,7 +2802,7 @@ __device__ __forceinline__ void rollout_tick(const Cfg& c, const orx_state_t& st
       if (p1.d != p2.d) {
         if (sep < 0) sep = t0;
         const int32_t k = t0 - sep + 1;
-        const int32_t dmg = (k + c.sep_period - 1) / c.sep_period;
+        const int32_t dmg = sep_ceil(c, k);
         if (p1.d < p2.d) p1.hp -= dmg; else p2.hp -= dmg;
         deaths_over(p1, p2, end, status, dl);
       } else {
@@ -3834,7 +3852,7 @@ __global__ void __launch_bounds__(GRID ? 512 : kRolloutBlock) ORX_PAIR_ATTR
           const int32_t t0 = ft - 1;
           if (sep < 0) sep = t0;
           const int32_t k = t0 - sep + 1;
-          const int32_t dmg = (k + c.sep_period - 1) / c.sep_period;
+          const int32_t dmg = sep_ceil(c, k);
           me.hp -= me.d < od2 ? dmg : 0;
           const int32_t ohp = pair_swap(me.hp);
           const bool d1 = (isB ? ohp : me.hp) <= 0, d2 = (isB ? me.hp : ohp) <= 0;
@@ -4634,8 +4652,9 @@ int check_cfg(const orx_cfg_t* c) {
                                      c->item_bonus < 0 || c->item_slots < 0))
     return fail(ORX_EINVAL, "items need item_drop_pct in [0, 100], item_bonus >= 0, "
                             "item_slots >= 0");
-  if ((c->flags & ORX_EXT_SEPARATION_DAMAGE) && c->sep_period < 1)
-    return fail(ORX_EINVAL, "separation damage needs sep_period >= 1");
+  if ((c->flags & ORX_EXT_SEPARATION_DAMAGE) &&
+      (c->sep_period < 1 || c->sep_period > ORX_SEP_PERIOD_MAX))
+    return fail(ORX_EINVAL, "separation damage needs 1 <= sep_period <= ORX_SEP_PERIOD_MAX");
   if (c->rng != ORX_RNG_PHILOX && c->rng != ORX_RNG_MT19937)
     return fail(ORX_EINVAL, "unknown rng mode");
   if (c->rng == ORX_RNG_MT19937 && (c->width > 256 || c->height > 256))

@@ -109,6 +109,7 @@ OBS_FIELDS = ("p1_x", "p1_y", "p1_depth", "p1_health", "p2_x", "p2_y", "p2_depth
 OBS_INT32, OBS_COMPACT = 0, 1
 OBS_COMPACT_FIELDS = ("cells", "stairs", "health", "p1_depth", "p2_depth", "tick_status")
 COMPACT_MAX_STAT = 8000
+SEP_PERIOD_MAX = 1 << 24   # ORX_SEP_PERIOD_MAX: cfg.sep_period's upper bound
 
 # update-event records of orx_step_events (include/orx.h ORX_EV_*)
 EV_COMBAT, EV_DEATH, EV_POSITION, EV_DUNGEON, EV_HEALTH = 1, 2, 3, 4, 5

@@ -120,6 +120,7 @@ def test_enum_values_match_header():
     assert (enums.EV_COMBAT, enums.EV_DEATH, enums.EV_POSITION, enums.EV_DUNGEON) == (
         val("ORX_EV_COMBAT"), val("ORX_EV_DEATH"), val("ORX_EV_POSITION"), val("ORX_EV_DUNGEON"))
     assert enums.MAX_EVENTS == val("ORX_MAX_EVENTS")
+    assert enums.SEP_PERIOD_MAX == val("ORX_SEP_PERIOD_MAX")
 
 
 def test_validate_cfg(lib):
@@ -141,7 +142,8 @@ def test_validate_cfg(lib):
     ok.append(EnvConfig(width=6, height=5, layouts=np.ones((3, 6, 5), np.uint8)))
     # build extensions: known bits only; separation damage needs a period
     ok.append(EnvConfig(flags=3, sep_period=5))
-    bad += [EnvConfig(flags=1, sep_period=0)]
+    ok.append(EnvConfig(flags=1, sep_period=1 << 24))
+    bad += [EnvConfig(flags=1, sep_period=0), EnvConfig(flags=1, sep_period=(1 << 24) + 1)]
     # the readme's character mechanics: heal needs mana; every parameter in range
     ok += [EnvConfig(flags=4 | 8 | 16 | 32, n_npcs=4), EnvConfig(flags=16, xp_per_kill=0)]
     ok.append(EnvConfig(flags=64))
