@@ -5138,7 +5138,9 @@ int orx_step_n(const orx_cfg_t* cfg, const orx_state_t* st, const int8_t* action
   // register NPCs on empty dungeons: the rollout's tick on the logged pairs
   // (ORX_STEP_N_GENERIC=1 forces the generic one, for A/B runs and tests)
   const char* gen_env = getenv("ORX_STEP_N_GENERIC");
-  if (!grid && nc != kDense && !(gen_env && gen_env[0] == '1')) {
+  // (the buffer-store rows address one tick's rows with 32-bit offsets)
+  const bool rows_fit = (uint64_t)B * ORX_OBS_FIELDS * 4u < (1ull << 31);
+  if (!grid && nc != kDense && rows_fit && !(gen_env && gen_env[0] == '1')) {
     const int rows = obs ? (obs_format == ORX_OBS_COMPACT ? 2 : 1) : 0;
     const uint32_t lanes = rollout_lanes(B);  // games per wave, as the rollout's plan
     const uint64_t threads = (((uint64_t)B + lanes - 1) / lanes) * 64u;
