@@ -2062,6 +2062,9 @@ __global__ void __launch_bounds__(256) reset_kernel(orx_cfg_t hc, orx_state_t st
 // player 2's RandomBot and the initiative draw), and out(p1, p2, tick,
 // status) receives the post-step state from registers (no re-read of what
 // was just stored).
+#ifndef ORX_STEP_EAGER
+#define ORX_STEP_EAGER 1
+#endif
 struct NoOut {
   __device__ __forceinline__ void operator()(const Player&, const Player&, int32_t, int32_t) {}
 };
@@ -2072,6 +2075,10 @@ __device__ __forceinline__ void step_game(const orx_cfg_t& hc, const orx_state_t
                                           int32_t* __restrict__ events,
                                           int32_t* __restrict__ n_events, O out = O{}) {
   constexpr bool kOut = !std::is_same<O, NoOut>::value;
+  // every state word and the action pair in one round trip (a finished game
+  // discards some) -- the step kernels too: loaded behind the status and
+  // action tests, a game in progress waited out three round trips in a row
+  constexpr bool kEager = kOut || ORX_STEP_EAGER;
   Cfg c = make_cfg(hc, st);
   if constexpr (!EXT) c.ext = 0;
   const uint32_t game = off + i;
@@ -2085,14 +2092,14 @@ __device__ __forceinline__ void step_game(const orx_cfg_t& hc, const orx_state_t
   Items<NCAP> items;
   int32_t sep = -1;
   W4 tb0{0, 0, 0, 0};  // (kOut) the tick block: player 2's policy and the initiative draw
-  if constexpr (kOut) {  // every state word in one round trip (a reset discards some)
+  if constexpr (kEager) {
     load_players<GRID>(st, B, i, p1, p2);
     tick = st.tick[i];
     ep = (uint32_t)st.episode[i];
     load_npcs(st, c, B, i, npc);
     load_rpg(st, c, B, i, p1, p2, npc, items);
     if (c.ext & ORX_EXT_SEPARATION_DAMAGE) sep = st.sep_start[i];
-    tb0 = tick_block(key, game, ep, tick);
+    if constexpr (kOut) tb0 = tick_block(key, game, ep, tick);
     a = get_action(p1, p2, tick, ep, tb0);
   }
   if (status != ORX_IN_PROGRESS) {
@@ -2101,7 +2108,7 @@ __device__ __forceinline__ void step_game(const orx_cfg_t& hc, const orx_state_t
       out(p1, p2, tick, status);
       return;
     }
-    const uint32_t ep1 = (kOut ? ep : (uint32_t)st.episode[i]) + 1u;
+    const uint32_t ep1 = (kEager ? ep : (uint32_t)st.episode[i]) + 1u;
     setup_game<NCAP, GRID>(c, key, game, ep1, p1, p2, npc, tick, status);
     store_players<GRID>(st, B, i, p1, p2, true);
     items.clear();
@@ -2117,7 +2124,7 @@ __device__ __forceinline__ void step_game(const orx_cfg_t& hc, const orx_state_t
     out(p1, p2, tick, status);
     return;
   }
-  if constexpr (!kOut) a = get_action(p1, p2, tick, ep, tb0);
+  if constexpr (!kEager) a = get_action(p1, p2, tick, ep, tb0);
   p1.move = (int8_t)(a & 0xFF);
   p2.move = (int8_t)(a >> 8);
   if (!valid_move(c, p1.move) || !valid_move(c, p2.move)) {
@@ -2126,7 +2133,7 @@ __device__ __forceinline__ void step_game(const orx_cfg_t& hc, const orx_state_t
     out(p1, p2, tick, (int32_t)ORX_STATUS_BAD_ACTION);
     return;
   }
-  if constexpr (!kOut) {
+  if constexpr (!kEager) {
     ep = (uint32_t)st.episode[i];
     tick = st.tick[i];
     load_players<GRID>(st, B, i, p1, p2);

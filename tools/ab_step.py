@@ -37,6 +37,22 @@ def child(lib):
         torch.cuda.synchronize()
         us = s.elapsed_time(f) * 1e3 / reps
         out[f"step_B{B}"] = {"us_per_launch": round(us, 2), "env_steps_per_s": B / us * 1e6}
+        # the same launches captured in a HIP graph (no host launch cost)
+        g = torch.cuda.CUDAGraph()
+        sg = torch.cuda.Stream(device=dev)
+        sg.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(sg):
+            with torch.cuda.graph(g, stream=sg):
+                for _ in range(reps):
+                    e.step(e.actions)
+        torch.cuda.current_stream().wait_stream(sg)
+        g.replay()
+        torch.cuda.synchronize()
+        s.record()
+        g.replay()
+        f.record()
+        torch.cuda.synchronize()
+        out[f"step_B{B}"]["graph_us_per_launch"] = round(s.elapsed_time(f) * 1e3 / reps, 2)
     print(json.dumps(out), flush=True)
 
 

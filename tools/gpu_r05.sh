@@ -66,6 +66,10 @@ for s in $STEPS; do
       timeout -k 10 600 python3 tools/ab_c5.py tools/ab_libs/base.so tools/ab_libs/ptr.so \
         --reps=3 > $O/ab_c5.jsonl 2> $O/ab_c5.err
       rc=$?; echo "abc5 rc=$rc"; cat $O/ab_c5.jsonl; fatal $rc abc5;;
+    abstep)
+      timeout -k 10 600 python3 tools/ab_step.py tools/ab_libs/base.so tools/ab_libs/ptr.so \
+        --reps=3 > $O/ab_step.jsonl 2> $O/ab_step.err
+      rc=$?; echo "abstep rc=$rc"; cat $O/ab_step.jsonl; fatal $rc abstep;;
     c5)
       timeout -k 10 400 python3 tools/c5_forms.py > $O/c5_forms.jsonl 2> $O/c5_forms.err
       rc=$?; echo "c5 rc=$rc"; fatal $rc c5;;
