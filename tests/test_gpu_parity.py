@@ -901,6 +901,14 @@ PAIRED_CASES = {
                                    p2_depth=0, max_ticks=50, npc_health=2), (2, 2), 1000, 70),
     "stairs_npcs_k14_unused": (dict(width=9, height=9, n_npcs=14, start_mode=2, p1_depth=1,
                                     p2_depth=0, despawn=2, max_ticks=40), (2, 2), 1024, 71),
+    # separation damage's multiply-shift ceil(k / period) (round 5) over long
+    # separations and at the largest period ORX_SEP_PERIOD_MAX
+    "stairs_sep_period7_long": (dict(width=16, height=16, start_mode=2, p1_depth=0, p2_depth=3,
+                                     max_ticks=0, flags=1, sep_period=7, player_health=40),
+                                (2, 2), 1000, 76),
+    "stairs_sep_period_max": (dict(width=12, height=12, start_mode=2, p1_depth=0, p2_depth=2,
+                                   max_ticks=70, flags=1, sep_period=1 << 24, player_health=3),
+                              (2, 2), 777, 77),
 }
 
 
