@@ -89,6 +89,17 @@ def build(force: bool = False, verbose: bool = False, defines: Iterable[str] = (
     if not force and os.path.exists(out) and built_id(out) == sid:
         return out
     os.makedirs(os.path.dirname(out), exist_ok=True)
+    # one build per output at a time (parallel test workers in a fresh tree):
+    # the others wait on the lock and then find the library built
+    import fcntl
+    with open(out + ".lock", "w") as lock:
+        fcntl.flock(lock, fcntl.LOCK_EX)
+        if not force and os.path.exists(out) and built_id(out) == sid:
+            return out
+        return _build_locked(out, sid, defines, verbose)
+
+
+def _build_locked(out: str, sid: str, defines, verbose: bool) -> str:
     base = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
             f'-DORX_BUILD_ID="{sid}"'] + [f"-D{d}" for d in defines]
     if any(d.split("=")[0] == "ORX_STAMPS" for d in defines):

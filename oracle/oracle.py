@@ -43,8 +43,10 @@ def build(force: bool = False) -> str:
     src = os.path.join(HERE, "orx_oracle.c")
     if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < os.path.getmtime(src):
         import subprocess
+        tmp = f"{LIB_PATH}.{os.getpid()}.tmp"   # (parallel test workers: atomic replace)
         subprocess.check_call(["gcc", "-O2", "-std=c11", "-Wall", "-shared", "-fPIC", "-o",
-                               LIB_PATH, src])
+                               tmp, src])
+        os.replace(tmp, LIB_PATH)
     return LIB_PATH
 
 

@@ -22,6 +22,14 @@ def gpu_available() -> bool:
 
 
 @pytest.fixture(scope="session")
+def engine_lib():
+    """liborx.so, built first if this tree has none (or a stale one)."""
+    from optimax_rogue_amd import _lib, build
+    build.build()
+    return _lib.load()
+
+
+@pytest.fixture(scope="session")
 def oracle_lib():
     from oracle import oracle
     oracle.build()

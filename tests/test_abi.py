@@ -27,11 +27,8 @@ def struct_fields(name):
 
 
 @pytest.fixture(scope="module")
-def lib():
-    from optimax_rogue_amd import _lib
-    from optimax_rogue_amd import build
-    build.build()
-    return _lib.load()
+def lib(engine_lib):
+    return engine_lib
 
 
 def test_library_exports_every_declared_symbol(lib):

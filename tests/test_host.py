@@ -190,13 +190,13 @@ def test_decode_compact_round_trip():
     assert got.dtype == np.int32 and np.array_equal(got, rows.astype(np.int32))
 
 
-def test_compact_rows_refuse_what_does_not_fit():
+def test_compact_rows_refuse_what_does_not_fit(engine_lib):
     """orx_rollout_ex(ORX_OBS_COMPACT) refuses configurations whose values
     the compact fields cannot hold, before any device work."""
     import ctypes
     from optimax_rogue_amd import EnvConfig, _lib
     from optimax_rogue_amd.enums import OBS_COMPACT
-    lib = _lib.load()
+    lib = engine_lib
     st = _lib.OrxState()
 
     def rc(cfg, fmt=OBS_COMPACT):
