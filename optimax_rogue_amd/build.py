@@ -44,6 +44,8 @@ VARIANTS = {
     "sepw0": ("ORX_SEP_WAVES=0",),    # the separation-damage StaircaseBot form uncapped (131 VGPRs)
     "envw5": ("ORX_ENV_WAVES=5",),    # orx_env_step_ex held to 5 waves per SIMD
     "envw6": ("ORX_ENV_WAVES=6",),    # ... to 6
+    "envd1": ("ORX_ENV_DIAG=1",),     # orx_env_step without its tick (outputs of the loaded state)
+    "envd2": ("ORX_ENV_DIAG=2",),     # orx_env_step without its observation rows
 }
 
 

@@ -2224,6 +2224,9 @@ __global__ void __launch_bounds__(256) policy_kernel(orx_state_t st, int32_t pol
 #ifndef ORX_ENV_WAVES
 #define ORX_ENV_WAVES 1
 #endif
+#ifndef ORX_ENV_DIAG  // diagnostic builds: 1 no tick, 2 no observation rows
+#define ORX_ENV_DIAG 0
+#endif
 template <int NCAP, bool GRID, bool EXT>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORX_ENV_WAVES)))
 env_step_kernel(
@@ -2264,7 +2267,9 @@ env_step_kernel(
     auto out = [&](const Player& p1, const Player& p2, int32_t tick, int32_t after) {
       const int32_t row[ORX_OBS_FIELDS] = {p1.x, p1.y, p1.d, p1.hp, p2.x, p2.y, p2.d, p2.hp,
                                            tick, after, p1.sx, p1.sy, p2.sx, p2.sy};
-      if (lds_rows) {  // (uniform)
+      if constexpr ((ORX_ENV_DIAG & 2) != 0) {  // diagnostic: no observation rows
+        if (row[0] == -12345) obs[i] = row[1];   // (keeps the row's values live)
+      } else if (lds_rows) {  // (uniform)
 #pragma unroll
         for (int f = 0; f < ORX_OBS_FIELDS; ++f)
           rows_lds[threadIdx.x * ORX_OBS_FIELDS + f] = row[f];
@@ -2281,10 +2286,18 @@ env_step_kernel(
       bad = before == ORX_IN_PROGRESS && after == ORX_STATUS_BAD_ACTION;
     };
     before = st.status[i];
-    step_game<NCAP, false, GRID, EXT>(hc, st, get_action, B, i, key, off, nullptr, nullptr, out);
+    if constexpr ((ORX_ENV_DIAG & 1) != 0) {  // diagnostic: no tick (the outputs of the loaded state)
+      Player p1, p2;
+      load_players<GRID>(st, B, i, p1, p2);
+      pair = pack_actions(l1, l2);
+      out(p1, p2, st.tick[i], before);
+    } else {
+      step_game<NCAP, false, GRID, EXT>(hc, st, get_action, B, i, key, off, nullptr, nullptr,
+                                        out);
+    }
     reinterpret_cast<uint16_t*>(act)[i] = pair;
   }
-  if (lds_rows) {  // the workgroup's rows as one contiguous run (uniform)
+  if (lds_rows && (ORX_ENV_DIAG & 2) == 0) {  // the workgroup's rows as one run (uniform)
     __syncthreads();
     const uint32_t g0 = blockIdx.x * blockDim.x;
     const uint32_t n = (min(B - g0, (uint32_t)blockDim.x)) * ORX_OBS_FIELDS;

@@ -55,6 +55,33 @@ def child(lib):
         out[f"env_{B}_b2b"] = round(a.elapsed_time(b) * 1e3 / n, 2)
         del eng, la, lo, lr, ld, ls, lb
         torch.cuda.empty_cache()
+    # 65,536 games: 50 launches captured in one HIP graph (the device's time)
+    eng = BatchedEngine(cfg, 65536, seed=3, device=dev)
+    la = torch.randint(1, 6, (65536,), dtype=torch.int64, device=dev)
+    lo = torch.empty((65536, len(OBS_FIELDS)), dtype=torch.int32, device=dev)
+    lr = torch.empty(65536, dtype=torch.float32, device=dev)
+    ld = torch.empty(65536, dtype=torch.bool, device=dev)
+    ls = torch.empty(65536, dtype=torch.int32, device=dev)
+    lb = torch.zeros(1, dtype=torch.int32, device=dev)
+    eng.env_step(la, 1, lo, lr, ld, ls, lb)
+    g = torch.cuda.CUDAGraph()
+    sg = torch.cuda.Stream(device=dev)
+    sg.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(sg):
+        with torch.cuda.graph(g, stream=sg):
+            for _ in range(50):
+                eng.env_step(la, 1, lo, lr, ld, ls, lb)
+    torch.cuda.current_stream().wait_stream(sg)
+    g.replay()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(4):
+        g.replay()
+    b.record()
+    torch.cuda.synchronize()
+    out["env_65536_graph"] = round(a.elapsed_time(b) * 1e3 / 200, 2)
+    del g, eng
     pool = torch.randint(1, 6, (16, 65536), dtype=torch.int64, device=dev)
     env = VecEnv(cfg, 65536, seed=3, device=dev, opponent=1, out_buffers=2)
     for k in range(20):

@@ -38,7 +38,8 @@ for s in $STEPS; do
         --timeout 120 --timeout-method thread > $O/envtests.log 2>&1
       rc=$?; echo "envtests rc=$rc"; tail -5 $O/envtests.log; fatal $rc envtests;;
     abenv)
-      timeout -k 10 600 python3 tools/ab_env.py optimax_rogue_amd/liborx.so --reps=3 \
+      timeout -k 10 600 python3 tools/ab_env.py tools/ab_libs/base.so tools/ab_libs/ptr.so \
+        --reps=3 \
         > $O/ab_env.jsonl 2> $O/ab_env.err
       rc=$?; echo "abenv rc=$rc"; cat $O/ab_env.jsonl; fatal $rc abenv;;
     replaytests)
@@ -67,6 +68,13 @@ for s in $STEPS; do
         --reps=3 > $O/ab_c5.jsonl 2> $O/ab_c5.err
       rc=$?; echo "abc5 rc=$rc"; cat $O/ab_c5.jsonl; fatal $rc abc5;;
     abstep)
+      timeout -k 10 600 python3 tools/ab_step.py tools/ab_libs/base.so tools/ab_libs/ptr.so \
+        --reps=3 > $O/ab_step.jsonl 2> $O/ab_step.err
+      rc=$?; echo "abstep rc=$rc"; cat $O/ab_step.jsonl; fatal $rc abstep;;
+    abenvstep)
+      timeout -k 10 600 python3 tools/ab_env.py tools/ab_libs/base.so tools/ab_libs/ptr.so \
+        --reps=3 > $O/ab_env.jsonl 2> $O/ab_env.err
+      rc=$?; echo "abenv rc=$rc"; cat $O/ab_env.jsonl; fatal $rc abenv
       timeout -k 10 600 python3 tools/ab_step.py tools/ab_libs/base.so tools/ab_libs/ptr.so \
         --reps=3 > $O/ab_step.jsonl 2> $O/ab_step.err
       rc=$?; echo "abstep rc=$rc"; cat $O/ab_step.jsonl; fatal $rc abstep;;
