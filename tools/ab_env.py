@@ -55,9 +55,28 @@ def child(lib):
         out[f"env_{B}_b2b"] = round(a.elapsed_time(b) * 1e3 / n, 2)
         del eng, la, lo, lr, ld, ls, lb
         torch.cuda.empty_cache()
-    # 65,536 games: 50 launches captured in one HIP graph (the device's time)
+    # 65,536 games: 50 launches captured in one HIP graph (the device's time),
+    # for int64 / int32 / int8 learner actions
+    for dt in (torch.int64, torch.int32, torch.int8):
+        out[f"env_65536_graph_{str(dt)[6:]}"] = graph_us(torch, cfg, dev, dt)
+    pool = torch.randint(1, 6, (16, 65536), dtype=torch.int64, device=dev)
+    env = VecEnv(cfg, 65536, seed=3, device=dev, opponent=1, out_buffers=2)
+    for k in range(20):
+        env.step(pool[k % 16])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(400):
+        env.step(pool[k % 16])
+    torch.cuda.synchronize()
+    out["vecenv_ring_us"] = round((time.perf_counter() - t0) / 400 * 1e6, 2)
+    print(json.dumps(out), flush=True)
+
+
+def graph_us(torch, cfg, dev, dt):
+    from optimax_rogue_amd import OBS_FIELDS
+    from optimax_rogue_amd.engine import BatchedEngine
     eng = BatchedEngine(cfg, 65536, seed=3, device=dev)
-    la = torch.randint(1, 6, (65536,), dtype=torch.int64, device=dev)
+    la = torch.randint(1, 6, (65536,), dtype=dt, device=dev)
     lo = torch.empty((65536, len(OBS_FIELDS)), dtype=torch.int32, device=dev)
     lr = torch.empty(65536, dtype=torch.float32, device=dev)
     ld = torch.empty(65536, dtype=torch.bool, device=dev)
@@ -80,19 +99,7 @@ def child(lib):
         g.replay()
     b.record()
     torch.cuda.synchronize()
-    out["env_65536_graph"] = round(a.elapsed_time(b) * 1e3 / 200, 2)
-    del g, eng
-    pool = torch.randint(1, 6, (16, 65536), dtype=torch.int64, device=dev)
-    env = VecEnv(cfg, 65536, seed=3, device=dev, opponent=1, out_buffers=2)
-    for k in range(20):
-        env.step(pool[k % 16])
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(400):
-        env.step(pool[k % 16])
-    torch.cuda.synchronize()
-    out["vecenv_ring_us"] = round((time.perf_counter() - t0) / 400 * 1e6, 2)
-    print(json.dumps(out), flush=True)
+    return round(a.elapsed_time(b) * 1e3 / 200, 2)
 
 
 def main():
