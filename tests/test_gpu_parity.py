@@ -624,6 +624,9 @@ SHARDED_EXTRAS = {
     # paired StaircaseBot form at 32 games per wave), separation damage off / on
     "c5_131072_sep_off": ("c5", 131072, 2, (2, 2), 0),
     "c5_131072_sep_on": ("c5sep", 131072, 2, (2, 2), 0),
+    # round 5: a RandomBot against a StaircaseBot on C3 (the c3_mixed extra,
+    # pair_rollout_kernel<8, 4, ...>: the mixed paired form)
+    "c3_mixed": ("c3", 65536, 2, (1, 2), 0),
 }
 
 
@@ -635,6 +638,8 @@ def _extras_cfg(which):
         return EnvConfig(width=64, height=64, n_npcs=8, layouts=bank.layouts)
     if which == "c3_rpg":
         return EnvConfig(width=64, height=64, n_npcs=8, flags=EXT_RPG)
+    if which == "c3":
+        return EnvConfig.c3()
     cfg = EnvConfig.c5()
     if which == "c5sep":
         cfg.flags, cfg.sep_period = EXT_SEPARATION_DAMAGE, 8
@@ -1142,6 +1147,43 @@ def test_golden_step_n(name):
     for t in range(fx.T):
         assert np.array_equal(o[t], _obs_rows(fx.state(t + 1))), f"{name} obs t={t + 1}"
     compare_state(eng.snapshot(), fx.state(fx.T), fx.K, f"{name} final")
+
+
+def test_replay_bench_shape_fast_equals_generic():
+    """bench.py's replay_step_n extra in the form it is timed (C3, 65,536
+    games, a 128-tick uniform move log, int32 rows: the fast replay_kernel at
+    64 games per wave) equals the generic one-lane form (ORX_STEP_N_GENERIC=1,
+    itself checked tick by tick against orx_step and the reference fixtures):
+    every row and the final state, over two consecutive logs."""
+    import torch
+    from optimax_rogue_amd import EnvConfig
+    from optimax_rogue_amd.engine import BatchedEngine
+    from optimax_rogue_amd.enums import OBS_FIELDS
+    dev = torch.device("cuda", 0)
+    B, T = 65536, 128
+    g = torch.Generator(device="cpu").manual_seed(11)
+    logs = [torch.randint(1, 6, (T, B, 2), generator=g, dtype=torch.int8).to(dev)
+            for _ in range(2)]
+    res = []
+    for generic in ("0", "1"):
+        os.environ["ORX_STEP_N_GENERIC"] = generic
+        try:
+            eng = BatchedEngine(EnvConfig.c3(), B, seed=3, device=dev)
+            rows = []
+            for log in logs:
+                obs = torch.empty((T, len(OBS_FIELDS), B), dtype=torch.int32, device=dev)
+                eng.step_n(log, obs=obs)
+                rows.append(obs.cpu().numpy())
+            torch.cuda.synchronize()
+        finally:
+            del os.environ["ORX_STEP_N_GENERIC"]
+        res.append((rows, eng.snapshot()))
+    (r0, s0), (r1, s1) = res
+    for k in range(2):
+        assert np.array_equal(r0[k], r1[k]), k
+    for k in s0:
+        assert np.array_equal(s0[k], s1[k]), k
+    assert s0["ep_count"].sum() > 0 and s0["counters"][0].sum() > 0
 
 
 STEP_N_CASES = {
