@@ -112,6 +112,20 @@ def _cpu_model() -> str:
     return platform.processor() or platform.machine()
 
 
+def physical_cores() -> int:
+    """Physical cores of the host: unique (core, socket) pairs of `lscpu -p`
+    (os.cpu_count() when lscpu is absent)."""
+    try:
+        out = subprocess.run(["lscpu", "-p=CORE,SOCKET"], capture_output=True, text=True,
+                             timeout=20).stdout
+        pairs = {tuple(l.split(",")[:2]) for l in out.splitlines() if l and l[0] != "#"}
+        if pairs:
+            return len(pairs)
+    except (OSError, subprocess.SubprocessError):
+        pass
+    return os.cpu_count() or 1
+
+
 def cpu_baseline(cfg_dict: dict, seconds: float) -> dict:
     """The C oracle (scalar port of the reference updater) on the host cores
     (the reference's own Python updater, timed in the build container, rides
@@ -194,7 +208,42 @@ def cpu_baseline(cfg_dict: dict, seconds: float) -> dict:
             "value": pyr["value"] / ratio["per_core"], "cores": pyr["cores"],
             "note": "python_restatement / pyref_vs_reference.per_core (both legs measured on "
                     "one host): the reference updater's estimated rate on this box's cores"}
+    # the whole host (every physical core of the box, not the
+    # per-GPU share above): the C port as one thread per physical core this
+    # job may run on, and the Python restatement as one process per such core
+    phys = physical_cores()
+    n_all = max(1, min(phys, avail))
+    res_all = {}
+    th = [threading.Thread(target=leg, args=(k, 2.0, res_all)) for k in range(n_all)]
+    t0 = time.perf_counter()
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    el_all = time.perf_counter() - t0
+    tot_all = sum(B * n for n, _ in res_all.values())
+    pyr_all = None
+    try:
+        r = subprocess.run([sys.executable, "-m", "oracle.pyref", "--bench", "--seconds=2.0",
+                            "--single=0.5", f"--procs={n_all}"],
+                           cwd=ROOT, capture_output=True, text=True, timeout=300)
+        pyr_all = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else \
+            {"error": r.stderr[-500:]}
+        pyr_all.pop("lscpu", None)
+    except (subprocess.SubprocessError, ValueError, IndexError) as e:
+        pyr_all = {"error": repr(e)}
+    whole = {"physical_cores": phys, "cpus_visible": os.cpu_count(), "cpus_in_affinity": avail,
+             "cores_used": n_all, "host": _cpu_model(),
+             "port": {"value": tot_all / el_all, "unit": "env-steps/s", "cores": n_all,
+                      "per_core": tot_all / el_all / n_all,
+                      "sample": f"{n_all} threads x 256 games for {el_all:.1f} s "
+                                f"({tot_all} env-steps)"},
+             "python_restatement": pyr_all,
+             "note": "every physical core of the host this job may run on (lscpu: unique "
+                     "(core, socket) pairs, capped by the process's CPU affinity); the "
+                     "top-level value is the per-GPU share of 16 threads"}
     return {"value": total / el, "unit": "env-steps/s", "cores": cores, "kind": "port",
+            "whole_host": whole,
             "python_restatement": pyr,
             "reference_python": ref,
             "per_core": total / el / cores, "single_core": single,
@@ -307,7 +356,8 @@ def extras(torch, cfg, dev, B_cfg, K, large_rollout=False):
     torch.cuda.empty_cache()
     # (1c) a replay: orx_step_n over a 128-tick move log (int8 [128, B, 2],
     # uniform 1..5) at the config batch, every tick's observation rows
-    # written -- the generic one-lane tick, one launch per 128 ticks
+    # written -- replay_kernel (the rollout's tick in LOG mode, one lane per
+    # game), one launch per 128 ticks
     eng = BatchedEngine(cfg, B_cfg, seed=3, device=dev)
     T = 128
     log = torch.randint(1, 6, (T, B_cfg, 2), dtype=torch.int8, device=dev)
@@ -507,6 +557,75 @@ def extras(torch, cfg, dev, B_cfg, K, large_rollout=False):
     return out
 
 
+C5_GLOBAL = 131072   # BASELINE.json configs[4]: 131,072 games on 128x128 over 8 GPUs
+
+
+def c5_sharded(torch, dist, dev, rank, world, coll_dev, steps, warmup=3, T=128):
+    """BASELINE.json configs[4] (C5) as a multi-GPU job: the 131,072 games
+    strong-sharded over the ranks by parallel.shard (16,384 per rank at 8
+    GPUs), both players StaircaseBots (staircasebot.py:9-21; their descends are
+    updater.py:259-296), separation damage off and on.  Every rank runs its
+    share as two stream shards (the paired form, as the 1-GPU extra), timed
+    like the headline: `warmup` untimed steps, then `steps` 128-tick launches
+    bracketed by barrier + synchronize, the max over ranks; then its own
+    returns all-gather.  Returns rank 0's block (None elsewhere)."""
+    from optimax_rogue_amd import EnvConfig
+    from optimax_rogue_amd.engine import StreamShardedEngine
+    from optimax_rogue_amd.enums import EXT_SEPARATION_DAMAGE
+    from optimax_rogue_amd.parallel import gather_returns, shard
+    off, n = shard(C5_GLOBAL, rank, world)
+    block = {"global_batch": C5_GLOBAL, "ticks_per_step": T, "steps": steps, "warmup": warmup,
+             "policy": "2x StaircaseBot", "grid": "128x128", "scaling": "strong",
+             "note": "configs[4]: 131,072 games strong-sharded over the ranks by global id; "
+                     "value = 131,072 x ticks x steps / max over ranks of the timed span "
+                     "(barrier + synchronize on both sides); separation damage = build "
+                     "extension EXT_SEPARATION_DAMAGE, sep_period 8"}
+    for flag in (0, EXT_SEPARATION_DAMAGE):
+        c = EnvConfig.c5()
+        if flag:
+            c.flags, c.sep_period = flag, 8
+        e = StreamShardedEngine(c, n, seed=5, game_offset=off, device=dev, n_streams=2)
+        o, a = e.trajectory_buffers(T)
+        go = e.rollout_launcher(T, 2, 2, obs=o, act=a)
+        e.fork()
+        for _ in range(warmup):
+            go()
+        e.join()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        e.fork()
+        for _ in range(steps):
+            go()
+        e.join()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        mine = {"rank": rank, "offset": off, "count": n, "elapsed_s": el}
+        el_max = el
+        ranks = [mine]
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64, device=coll_dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el_max = float(t.item())
+            ranks = [None] * world
+            dist.all_gather_object(ranks, mine)
+        rets = gather_returns(e.episode_returns(), C5_GLOBAL)
+        shape = e.rollout_shape(2, 2)
+        key = "separation_damage_on" if flag else "separation_damage_off"
+        block[key] = {"value": C5_GLOBAL * T * steps / el_max, "unit": "env-steps/s",
+                      "ms_per_step": el_max / steps * 1e3,
+                      "episodes_finished": int(rets[1].sum().item()),
+                      "games_per_wave": shape["games_per_wave"],
+                      "lanes_per_game": shape["lanes_per_game"], "ranks": ranks}
+        del e, o, a, go
+        torch.cuda.empty_cache()
+    return block if rank == 0 else None
+
+
 def _free_port() -> int:
     import socket
     s = socket.socket()
@@ -545,13 +664,22 @@ def launch_check(args) -> None:
     init("gloo" if world > 1 else None)
     G = args.global_batch if args.strong else args.batch * world
     offset, count = shard(G, rank, world)
-    mine = {"rank": rank, "local_rank": local, "offset": offset, "count": count}
+    c5_off, c5_count = shard(C5_GLOBAL, rank, world)
+    mine = {"rank": rank, "local_rank": local, "offset": offset, "count": count,
+            "c5": {"offset": c5_off, "count": c5_count}}
     ranks = [mine]
     if world > 1:
         ranks = [None] * world
         dist.all_gather_object(ranks, mine)
     if rank == 0:
-        print(json.dumps({"n_gpus": world, "global_batch": G, "ranks": ranks}), flush=True)
+        line = {"n_gpus": world, "global_batch": G, "ranks": ranks}
+        if world > 1 and not args.no_c5:
+            # the configs[4] block the N > 1 line carries (c5_sharded)
+            line["c5"] = {"global_batch": C5_GLOBAL,
+                          "ranks": [{"rank": x["rank"], **x.pop("c5")} for x in ranks]}
+        for x in ranks:
+            x.pop("c5", None)
+        print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
@@ -583,6 +711,11 @@ def main():
                     help="nccl (= RCCL, default) or gloo (multi-rank rehearsal on one GPU)")
     ap.add_argument("--same-device", action="store_true",
                     help="every rank uses cuda:0 (rehearsing N ranks on a 1-GPU box)")
+    ap.add_argument("--no-c5", action="store_true",
+                    help="with N > 1 ranks, skip the configs[4] block (C5: 131,072 StaircaseBot "
+                         "games strong-sharded over the ranks, c5_sharded)")
+    ap.add_argument("--c5-steps", type=int, default=20,
+                    help="timed steps of each C5 block (N > 1 ranks)")
     ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.steps < 1 or args.chunk < 1 or args.warmup < 0 or args.gpus < 1:
@@ -684,6 +817,13 @@ def main():
     mean_ret = float(allrets[0].sum().item()) / max(1, episodes)
 
     value = G * chunk * args.steps / elapsed
+    # BASELINE.json configs[4] on the same ranks: C5's 131,072 games
+    # strong-sharded over them (every rank takes part: barriers, collectives)
+    c5 = None
+    if world > 1 and not args.no_c5:
+        del obs, act, launch, eng
+        torch.cuda.empty_cache()
+        c5 = c5_sharded(torch, dist, dev, rank, world, coll_dev, args.c5_steps)
     if rank == 0:
         traffic = None
         if os.path.exists(TRAFFIC_FILE):
@@ -769,6 +909,8 @@ def main():
             "ranks": ranks,
             "extras": extra,
         }
+        if world > 1:
+            result["c5"] = c5
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -1982,7 +1982,9 @@ __device__ __forceinline__ Cfg make_cfg(const orx_cfg_t& h, const orx_state_t& s
   c.autoreset = h.autoreset;
   c.ext = h.flags;
   c.sep_period = h.sep_period > 0 ? h.sep_period : 1;
-  {
+  c.sep_sh = 31;           // P = 1 (unused without separation damage)
+  c.sep_m = 0x80000001u;
+  if (h.flags & ORX_EXT_SEPARATION_DAMAGE) {  // (wave-uniform; the division only when used)
     const uint32_t P = (uint32_t)c.sep_period;
     const int32_t l = P > 1u ? 32 - __clz(P - 1u) : 0;
     c.sep_sh = 31 + l;

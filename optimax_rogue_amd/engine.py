@@ -357,12 +357,15 @@ class BatchedEngine:
         pointers as plain integers).  The caller has checked the tensors."""
         fn, check = self.lib.orx_env_step_ex, _lib.check
         pcfg, pst, act = self._pcfg, self._pst, self.actions.data_ptr()
-        B, seed, off, p2 = self.B, self.seed, self.game_offset, int(p2)
+        B, p2 = self.B, int(p2)
         stream = _raw_stream_getter(self.device)
+        eng = self
 
         def launch(a_ptr, nb, cols, obs, rew, done, status, bad):
-            code = fn(pcfg, pst, a_ptr, nb, cols, p2, act, obs, rew, done, status, bad, B, seed,
-                      off, stream())
+            # seed and game_offset read per call: a later change to the
+            # engine's keys reaches this path as it reaches step / rollout
+            code = fn(pcfg, pst, a_ptr, nb, cols, p2, act, obs, rew, done, status, bad, B,
+                      eng.seed, eng.game_offset, stream())
             if code:
                 check("orx_env_step_ex", code)
         return launch

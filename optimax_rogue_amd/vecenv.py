@@ -19,6 +19,7 @@ Player 2 is the learner's opponent: a device policy (``Policy.Random``,
 """
 from __future__ import annotations
 
+import warnings
 from typing import Optional, Union
 
 import torch
@@ -36,16 +37,23 @@ class VecEnv:
     ``check_actions`` -- what happens to actions outside the Move codes (e.g.
     a 0-based argmax); the engine always stops such a game with
     STATUS_BAD_ACTION (done, reward 0: a truncation; it restarts on the next
-    step):
+    step), and the step returns normally:
 
     * ``"deferred"`` (default): the launch also counts refused actions into a
       device counter, and every ``check_every`` steps ``step`` reads it back
       asynchronously (pinned memory and an event, no host sync); once a read
-      shows new refusals, a later ``step`` raises ValueError (before playing
-      its own tick).  Detection lags by at most two check periods;
-      ``bad_actions()`` reads the count now (synchronizing).
+      that has landed shows new refusals, ``step`` issues a RuntimeWarning
+      (and ``warnings_seen`` counts it).  Nothing is raised and every tick is
+      played.  When a read has not landed at its check, the next check waits
+      for it, so the warning comes some check periods after the refusal --
+      how many depends on when the copy completes.  ``bad_actions()`` reads
+      the exact count now (synchronizing).
+    * ``"deferred-raise"``: as ``"deferred"``, but the ``step`` that sees new
+      refusals raises ValueError instead of warning -- before launching, so
+      the actions passed to THAT call are not played (pass them again after
+      handling the error).
     * ``True``: a host check before every launch raises ValueError at once
-      (a device-to-host sync per step).
+      (a device-to-host sync per step; the offending call plays no tick).
     * ``False``: no detection.
 
     ``out_buffers`` -- 0 (default): every step returns fresh tensors; k > 0:
@@ -61,8 +69,13 @@ class VecEnv:
                  check_every: int = 64):
         if not int(cfg.autoreset):
             raise ValueError("VecEnv needs cfg.autoreset = 1 (finished games restart)")
-        if check_actions not in (True, False, "deferred"):
-            raise ValueError('check_actions must be True, False or "deferred"')
+        if isinstance(check_actions, str):
+            if check_actions not in ("deferred", "deferred-raise"):
+                raise ValueError('check_actions must be a bool, "deferred" or "deferred-raise"')
+        elif type(check_actions).__name__ in ("bool", "bool_") or check_actions in (0, 1):
+            check_actions = bool(check_actions)   # (1, np.True_ -> True: the host check)
+        else:
+            raise ValueError('check_actions must be a bool, "deferred" or "deferred-raise"')
         self.engine = BatchedEngine(cfg, n_games, seed=seed, game_offset=game_offset,
                                     device=device)
         self.B = self.engine.B
@@ -83,9 +96,10 @@ class VecEnv:
         self._bad_dev = torch.zeros(1, dtype=torch.int32, device=self.device)
         self._bad_ptr = self._bad_dev.data_ptr()
         self._bad_host = torch.zeros(1, dtype=torch.int32).pin_memory() \
-            if self.check_actions == "deferred" else None
+            if isinstance(self.check_actions, str) else None
         self._bad_event = None
         self._bad_seen = 0
+        self.warnings_seen = 0
         self._steps = 0
         self._ring = [self._alloc_out() for _ in range(self.out_buffers)]
         self._ring_ptrs = [tuple(t.data_ptr() for t in out) for out in self._ring]
@@ -145,7 +159,10 @@ class VecEnv:
             self._bad_event = None
             if n > self._bad_seen:
                 new, self._bad_seen = n - self._bad_seen, n
-                raise ValueError(self._bad_message(new))
+                if self.check_actions == "deferred-raise":
+                    raise ValueError(self._bad_message(new))
+                self.warnings_seen += 1
+                warnings.warn(self._bad_message(new), RuntimeWarning, stacklevel=3)
         # the copy runs on the counter's device's current stream (the stream
         # orx_env_step_ex launches on), and the event is recorded there, not
         # on whichever device happens to be current
@@ -178,8 +195,8 @@ class VecEnv:
         (1..6 with EXT_HEAL), any integer dtype.  A value outside them (e.g. a
         0-based argmax) stops that game with STATUS_BAD_ACTION: it is done
         with reward 0 this step (a truncation) and restarts on the next one;
-        ``check_actions`` decides whether and when ValueError is raised for
-        it (class docstring).  One launch (orx_env_step_ex) and no host sync
+        ``check_actions`` decides whether and when it is reported (a
+        warning by default; class docstring).  One launch (orx_env_step_ex) and no host sync
         (unless check_actions=True).  Returns (observation int32 [n_games,
         14], reward float32, done bool, status int32 [n_games]): separate
         tensors, fresh ones unless ``out_buffers`` > 0."""

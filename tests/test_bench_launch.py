@@ -42,6 +42,26 @@ def test_gpus_n_starts_n_ranks(n):
     assert [x["offset"] for x in out["ranks"]] == [65536 * k for k in range(n)]
 
 
+def test_gpus_n_carries_the_c5_block():
+    """configs[4] (C5: 131,072 StaircaseBot games over 8 GPUs) on the N > 1
+    line: every rank's strong share of the 131,072 games by parallel.shard;
+    a single rank has none (its C5 figures are the 1-GPU extras)."""
+    r = _run(["--gpus", "2", "--same-device", "--launch-check"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = _line(r.stdout)
+    assert out["c5"]["global_batch"] == 131072
+    assert [(x["rank"], x["offset"], x["count"]) for x in out["c5"]["ranks"]] == \
+        [(0, 0, 65536), (1, 65536, 65536)]
+    r = _run(["--gpus", "3", "--same-device", "--launch-check"])
+    out = _line(r.stdout)
+    assert [(x["offset"], x["count"]) for x in out["c5"]["ranks"]] == \
+        [(0, 43691), (43691, 43691), (87382, 43690)]
+    out = _line(_run(["--gpus", "1", "--launch-check"]).stdout)
+    assert "c5" not in out
+    out = _line(_run(["--gpus", "2", "--same-device", "--launch-check", "--no-c5"]).stdout)
+    assert "c5" not in out
+
+
 def test_gpus_n_strong_shards_the_global_batch():
     r = _run(["--gpus", "2", "--same-device", "--launch-check", "--strong",
               "--global-batch", "1001"])

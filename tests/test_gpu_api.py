@@ -442,33 +442,64 @@ def test_vecenv_bad_actions_truncate_on_device():
 
 def test_vecenv_deferred_bad_action_check():
     """The default check_actions="deferred": refused actions are counted on
-    the device by orx_env_step_ex (no host sync) and a later step raises
-    ValueError once the asynchronous read-back shows them (within a few
-    check periods); correct actions never raise, and a caught error is not
-    raised again for the same refusals.  bad_actions() reads the count."""
+    the device by orx_env_step_ex (no host sync) and a later step warns once
+    the asynchronous read-back shows them (every tick is still played);
+    "deferred-raise" raises ValueError instead.  Correct actions never report,
+    a report is not repeated for the same refusals, bad_actions() reads the
+    count."""
+    import warnings
     import torch
     from optimax_rogue_amd import EnvConfig, VecEnv
     dev = torch.device("cuda", 0)
     B = 256
-    env = VecEnv(EnvConfig(width=10, height=10, max_ticks=50), B, seed=5, device=dev,
-                 check_every=4)
-    good = torch.full((B,), 2, dtype=torch.int64, device=dev)
-    for _ in range(40):
-        env.step(good)
-    assert env.bad_actions() == 0
-    bad = good.clone()
-    bad[[1, 7, 200]] = 0                       # a 0-based argmax in three games
-    env.step(bad)
-    raised = 0
-    for _ in range(60):
-        try:
+    for mode in ("deferred", "deferred-raise"):
+        env = VecEnv(EnvConfig(width=10, height=10, max_ticks=50), B, seed=5, device=dev,
+                     check_every=4, **({} if mode == "deferred" else {"check_actions": mode}))
+        good = torch.full((B,), 2, dtype=torch.int64, device=dev)
+        for _ in range(40):
             env.step(good)
-        except ValueError as e:
-            assert "3 game(s)" in str(e) and "0-based" in str(e)
-            raised += 1
-        torch.cuda.synchronize()
-    assert raised == 1
-    assert env.bad_actions() == 3
+        assert env.bad_actions() == 0
+        bad = good.clone()
+        bad[[1, 7, 200]] = 0                       # a 0-based argmax in three games
+        env.step(bad)
+        raised = 0
+        t0 = int(env.engine.tick.sum())
+        with warnings.catch_warnings(record=True) as w:
+            warnings.simplefilter("always")
+            for _ in range(60):
+                try:
+                    env.step(good)
+                except ValueError as e:
+                    assert "3 game(s)" in str(e) and "0-based" in str(e)
+                    raised += 1
+                torch.cuda.synchronize()
+        msgs = [str(x.message) for x in w if issubclass(x.category, RuntimeWarning)]
+        if mode == "deferred":
+            assert raised == 0 and len(msgs) == 1 and "3 game(s)" in msgs[0]
+            assert env.warnings_seen == 1
+        else:
+            assert raised == 1 and not msgs
+        assert env.bad_actions() == 3
+        assert int(env.engine.tick.sum()) > t0
+
+
+def test_vecenv_check_actions_normalized():
+    """check_actions accepts bools (1 / numpy True mean the host check), the
+    two deferred modes, and nothing else."""
+    import numpy as np
+    import torch
+    from optimax_rogue_amd import EnvConfig, VecEnv
+    dev = torch.device("cuda", 0)
+    cfg = EnvConfig(width=10, height=10)
+    for v in (1, np.True_, True):
+        env = VecEnv(cfg, 8, seed=2, device=dev, check_actions=v)
+        assert env.check_actions is True
+        with pytest.raises(ValueError, match="Move values"):
+            env.step(torch.tensor([1, 2, 3, 4, 5, 0, 1, 1], device=dev))
+    assert VecEnv(cfg, 8, device=dev, check_actions=np.False_).check_actions is False
+    for v in ("raise", 2, None):
+        with pytest.raises(ValueError, match="check_actions"):
+            VecEnv(cfg, 8, device=dev, check_actions=v)
 
 
 def test_vecenv_out_buffers_ring():

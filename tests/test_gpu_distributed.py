@@ -91,14 +91,16 @@ def test_bench_gpus_2_runs_two_ranks():
     """`python bench.py --gpus 2` (no torchrun around it) starts two ranks by
     itself: here both on cuda:0 with the gloo gather (--same-device; RCCL takes
     one rank per device), as the driver's SCALE run does with one GPU each.
-    The line reports n_gpus 2, both ranks' shards and the returns gather."""
+    The line reports n_gpus 2, both ranks' shards and the returns gather,
+    and the configs[4] (C5) block timed on the same ranks."""
     root = os.path.dirname(HERE)
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="1")
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
     r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2",
                         "--same-device", "--dist-backend", "gloo", "--batch", "8192",
-                        "--steps", "2", "--warmup", "1", "--no-extras", "--no-cpu-baseline"],
+                        "--steps", "2", "--warmup", "1", "--no-extras", "--no-cpu-baseline",
+                        "--c5-steps", "2"],
                        env=env, capture_output=True, text=True, timeout=110, cwd=root)
     assert r.returncode == 0, r.stderr[-3000:]
     line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
@@ -107,6 +109,16 @@ def test_bench_gpus_2_runs_two_ranks():
         [(0, 0, 8192), (1, 8192, 8192)]
     assert line["returns_gather_ms"] is not None and line["returns_gather_backend"] == "gloo"
     assert line["value"] > 0
+    # configs[4]: C5's 131,072 StaircaseBot games strong-sharded over the two
+    # ranks, separation damage off and on, max over ranks
+    c5 = line["c5"]
+    assert c5["global_batch"] == 131072 and c5["steps"] == 2
+    for key in ("separation_damage_off", "separation_damage_on"):
+        b = c5[key]
+        assert [(x["rank"], x["offset"], x["count"]) for x in b["ranks"]] == \
+            [(0, 0, 65536), (1, 65536, 65536)]
+        assert b["value"] > 0 and b["lanes_per_game"] == 2
+        assert abs(b["ms_per_step"] * 1e-3 * 2 - max(x["elapsed_s"] for x in b["ranks"])) < 1e-6
 
 
 def test_rccl_process_group_on_the_device():
