@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define ORX_ABI_VERSION 6
+#define ORX_ABI_VERSION 7
 
 /* ---- error codes -------------------------------------------------------- */
 #define ORX_OK 0
@@ -77,6 +77,34 @@ extern "C" {
 #define ORX_POLICY_RANDOM 1    /* RandomBot.move   randombot.py:20-21          */
 #define ORX_POLICY_STAIRCASE 2 /* StaircaseBot.move staircasebot.py:9-21       */
 #define ORX_POLICY_STAY 3      /* always Move.Stay                            */
+
+/* enemy AI (orx_cfg_t.npc_policy): the reference's override hook
+ * Updater.decide_npc_move (updater.py:165-178), whose default is Stay.  Every
+ * NPC's move is decided at the start of the tick, in GameState.entities order,
+ * before any move is resolved (updater.py:116-126); then the reference's NPC
+ * shuffle (:127) orders them after the players and handle_move resolves each
+ * one (:133-134, 180-243: Block / Ambush / Flee against players and NPCs; an
+ * NPC stepping onto a staircase dies, :263-270); the dead are swept
+ * (:136-145).  The policies (the same rules as tests/golden/make_golden.py's
+ * NpcAiUpdater, which pins them against the reference):
+ *   an NPC on a depth without a dungeon (despawned), or on a depth where a
+ *   player stands next to a staircase tile, stays -- the second rule keeps
+ *   the reference from raising KeyError (a descend that despawns the depth
+ *   earlier in the tick, :295-296, then an NPC stepping onto a free cell,
+ *   :203); otherwise
+ *   ORX_NPC_RANDOM: random.choice(list(Move)), its getrandbits from the NPC
+ *     stream (Philox purpose 9, c2 = tick: bits 0-29 of each word, 3-bit
+ *     fields, >= 5 rejected) or, in stock-seed mode, the game's CPython random
+ *     between the player shuffle and the NPC shuffle;
+ *   ORX_NPC_CHASE: a greedy step toward the nearer player on its depth
+ *     (Manhattan; player 1 on a tie): |dx| > |dy| -> Right / Left, else Down /
+ *     Up (StaircaseBot's rule); no player there -> Stay;
+ *   a move into a blocked cell (Dungeon.is_blocked, world.py:41-46) -> Stay.
+ * Needs flags within ORX_EXT_SEPARATION_DAMAGE | ORX_EXT_RANDOM_DOUBLE_DEATH;
+ * the rollout runs such games one lane per game (the generic ordered tick). */
+#define ORX_NPC_STAY 0
+#define ORX_NPC_RANDOM 1
+#define ORX_NPC_CHASE 2
 
 /* word sources (orx_cfg_t.rng)                                             */
 #define ORX_RNG_PHILOX 0  /* keyed Philox4x32-10 streams (default; stateless,
@@ -189,7 +217,8 @@ extern "C" {
 #define ORX_EV_HEALTH 5  /* {5, iden, amount, 0}  EntityHealthUpdate updates.py:222-253
                             (separation damage -dmg, ORX_EXT_SEPARATION_DAMAGE;
                             a heal +amount, ORX_EXT_HEAL)                   */
-#define ORX_MAX_EVENTS 8 /* per game per tick (at most 6 occur)            */
+#define ORX_MAX_EVENTS 8 /* per game per tick with Stay NPCs (at most 6
+                            occur); orx_max_events(cfg) for any config    */
 
 #define ORX_MAX_NPCS 255     /* NPCs per game                                 */
 #define ORX_MAX_REG_NPCS 16  /* up to this many the kernels keep the NPCs in
@@ -261,6 +290,8 @@ typedef struct orx_cfg {
   int32_t item_slots;     /* items a player can hold                         */
   int32_t combat_cooldown;/* ORX_EXT_README_COMBAT: ticks after a mutual
                              attack (readme.md:69: 3)                        */
+  int32_t npc_policy;     /* (ABI 7) ORX_NPC_*: the enemy AI, Updater.
+                             decide_npc_move (updater.py:165-178); 0 = Stay */
 } orx_cfg_t;
 
 /* ---- batch state (SoA, batch axis contiguous; all device pointers) ------- */
@@ -379,6 +410,14 @@ int orx_rollout_shape(const orx_cfg_t* cfg, int32_t policy_p1, int32_t policy_p2
  * memory).  Replaces nothing: the reference keeps World.dungeons in a dict
  * (world.py:101-180). */
 int orx_dstore_depths(const orx_cfg_t* cfg);
+
+/* (ABI 7) Event records per game per tick orx_step_events writes for this
+ * configuration (its events buffer is [B][orx_max_events(cfg)][4]):
+ * ORX_MAX_EVENTS with Stay NPCs; with moving NPCs (npc_policy) 6 + 2 * n_npcs
+ * (each NPC's own move, combat or staircase death, plus its sweep), or
+ * ORX_EINVAL for an invalid configuration.  No reference counterpart (the
+ * reference returns a Python list, updater.py:76-162). */
+int orx_max_events(const orx_cfg_t* cfg);
 
 /* Message for the last non-zero return on this thread ("" if none). */
 const char* orx_last_error(void);

@@ -6,11 +6,11 @@ gfx950 in liborx.so, reached through the C-ABI declared in include/orx.h.
 """
 from .config import EnvConfig
 from .dungeons import DungeonBank
-from .enums import (CombatFlag, DungeonDespawningStrategy, Move, OBS_FIELDS, Policy, StartMode,
-                    Tile, UpdateResult)
+from .enums import (CombatFlag, DungeonDespawningStrategy, Move, NpcPolicy, OBS_FIELDS, Policy,
+                    StartMode, Tile, UpdateResult)
 
 __all__ = ["EnvConfig", "DungeonBank", "Move", "UpdateResult", "DungeonDespawningStrategy", "Tile", "CombatFlag",
-           "StartMode", "Policy", "OBS_FIELDS", "BatchedEngine", "StreamShardedEngine", "BatchedUpdater",
+           "StartMode", "Policy", "NpcPolicy", "OBS_FIELDS", "BatchedEngine", "StreamShardedEngine", "BatchedUpdater",
            "VecEnv"]
 
 

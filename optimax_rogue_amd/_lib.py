@@ -13,7 +13,7 @@ from .config import OrxCfg
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "liborx.so")
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 
 class OrxState(ctypes.Structure):
@@ -43,7 +43,7 @@ EXPORTS = ("orx_abi_version", "orx_last_error", "orx_validate_cfg", "orx_reset",
            "orx_step_events", "orx_policy", "orx_rollout", "orx_dungeon_stairs",
            "orx_dungeon_spawn", "orx_seed_mt", "orx_build_id", "orx_rollout_lanes", "orx_dstore_depths",
            "orx_rollout_shape", "orx_rollout_concurrent", "orx_env_step",
-           "orx_rollout_ex", "orx_env_step_ex", "orx_step_n")
+           "orx_rollout_ex", "orx_env_step_ex", "orx_step_n", "orx_max_events")
 
 
 def load() -> ctypes.CDLL:
@@ -109,6 +109,9 @@ def load() -> ctypes.CDLL:
     if hasattr(L, "orx_step_n"):
         L.orx_step_n.restype = ctypes.c_int
         L.orx_step_n.argtypes = [P(OrxCfg), P(OrxState), vp, i32, vp, i32, i64, u64, i64, vp]
+    if hasattr(L, "orx_max_events"):
+        L.orx_max_events.restype = ctypes.c_int
+        L.orx_max_events.argtypes = [P(OrxCfg)]
     if hasattr(L, "orx_dstore_depths"):
         L.orx_dstore_depths.restype = ctypes.c_int
         L.orx_dstore_depths.argtypes = [P(OrxCfg)]

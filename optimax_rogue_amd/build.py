@@ -122,7 +122,7 @@ def _build_locked(out: str, sid: str, defines, verbose: bool) -> str:
 # their share of the explicit instantiations, orx_engine.hip "Kernel
 # instances"), then linked -- about a minute on 8 cores instead of ~6 for one
 # translation unit.
-NPARTS = 14
+NPARTS = 16
 
 
 def _build_parts(base, out, verbose=False, jobs=None):

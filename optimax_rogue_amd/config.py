@@ -24,7 +24,7 @@ CFG_FIELDS = ("width", "height", "despawn", "max_ticks", "start_mode", "p1_depth
               "n_npcs", "npc_health", "npc_damage", "npc_armor", "player_health",
               "player_damage", "player_armor", "autoreset", "flags", "n_layouts", "sep_period",
               "rng", "mana_max", "mana_regen", "mana_per_point", "xp_per_kill", "xp_per_level",
-              "item_drop_pct", "item_bonus", "item_slots", "combat_cooldown")
+              "item_drop_pct", "item_bonus", "item_slots", "combat_cooldown", "npc_policy")
 
 
 class OrxCfg(ctypes.Structure):
@@ -67,6 +67,9 @@ class EnvConfig:
     item_bonus: int = 1             # flat bonus of an item (damage or max health)
     item_slots: int = 3             # items a player can hold
     combat_cooldown: int = 3        # EXT_README_COMBAT: ticks after a mutual attack (readme: 3)
+    # the enemy AI (Updater.decide_npc_move, updater.py:165-178): enums.NpcPolicy
+    # STAY (the reference's default), RANDOM or CHASE (include/orx.h ORX_NPC_*)
+    npc_policy: int = 0
     # explicit-grid dungeon generator: [L, W, H] Tile codes (None =
     # EmptyDungeonGenerator).  spawn_dungeon(depth) returns layout randint(L).
     layouts: Optional[np.ndarray] = dataclasses.field(default=None, repr=False, compare=False)

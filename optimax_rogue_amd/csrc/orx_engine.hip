@@ -72,7 +72,8 @@ enum : uint32_t {
   PUR_INIT = 1, PUR_DUNGEON = 2, PUR_SHUFFLE = 3, PUR_SPAWN = 4, PUR_POLICY = 5,
   PUR_RESOLVE = 6,  // ORX_EXT_RANDOM_DOUBLE_DEATH
   PUR_TICK = 7,     // the tick's CPython-random bit reservoir (bots, shuffles)
-  PUR_ITEM = 8      // ORX_EXT_ITEMS: an NPC's drop (c2 = tick, block = NPC slot)
+  PUR_ITEM = 8,     // ORX_EXT_ITEMS: an NPC's drop (c2 = tick, block = NPC slot)
+  PUR_NPC = 9       // the enemy AI's random.choice draws (cfg.npc_policy RANDOM; c2 = tick)
 };
 #define ORX_LIKELY(x) __builtin_expect(!!(x), 1)
 #define ORX_UNLIKELY(x) __builtin_expect(!!(x), 0)
@@ -299,6 +300,7 @@ __host__ __device__ inline uint32_t dstore_depths(int32_t max_ticks) {
 struct Cfg {  // device copy of orx_cfg_t plus derived constants (all wave-uniform)
   int32_t W, H, despawn, max_ticks, start_mode, d1, d2, K;
   int32_t npc_hp, player_hp, player_dmg_net, autoreset;
+  int32_t npc_pol, npc_dmg_net;  // the enemy AI (ORX_NPC_*) and an NPC's damage - armor
   int32_t ext, sep_period;  // ORX_EXT_* build extensions (0 in FAST kernels)
   // character mechanics (ORX_EXT_RPG)
   int32_t player_dmg, player_armor, mana_max, mana_third, mana_regen, mana_pp;
@@ -351,11 +353,12 @@ struct Deltas {  // counter / return increments, flushed once per launch
 // EV = false every emit compiles away.
 template <bool EV>
 struct Events {
-  int32_t* base;  // this game's [ORX_MAX_EVENTS][4]
+  int32_t* base;  // this game's [cap][4]
   int32_t n;
+  int32_t cap = ORX_MAX_EVENTS;  // records per game (orx_max_events)
   __device__ __forceinline__ void emit(int32_t type, int32_t iden, int32_t a, int32_t b) {
     if constexpr (EV) {
-      if (n < ORX_MAX_EVENTS) {
+      if (n < cap) {
         base[4 * n] = type; base[4 * n + 1] = iden; base[4 * n + 2] = a; base[4 * n + 3] = b;
       }
       ++n;
@@ -1680,6 +1683,12 @@ __device__ __forceinline__ void npc_hits(const Cfg& c, Npcs<NCAP>& npc, M& m, in
   }
 }
 
+template <bool EV>
+__device__ __forceinline__ void end_tick(const Cfg& c, Key key, uint32_t game, uint32_t ep,
+                                         Player& p1, Player& p2, int32_t& tick, int32_t& status,
+                                         bool err, Deltas& dl, Events<EV>& ev,
+                                         int32_t& sep_start);
+
 // One Updater.update for an in-progress game; p1.move/p2.move = raw moves.
 template <int NCAP, bool EV, bool GRID, class Src, class M>
 __device__ __forceinline__ void tick_game(const Cfg& c, Key key, Src& src, uint32_t game,
@@ -1742,6 +1751,17 @@ __device__ __forceinline__ void tick_game(const Cfg& c, Key key, Src& src, uint3
     p2.mana = min(p2.mana + c.mana_regen, c.mana_max);
   }
 
+  end_tick<EV>(c, key, game, ep, p1, p2, tick, status, err, dl, ev, sep_start);
+}
+
+// The end of Updater.update after the death sweep: the build extensions'
+// separation damage and random double-death winner (readme.md:46-48), tick++
+// and the result (updater.py:148-162).
+template <bool EV>
+__device__ __forceinline__ void end_tick(const Cfg& c, Key key, uint32_t game, uint32_t ep,
+                                         Player& p1, Player& p2, int32_t& tick, int32_t& status,
+                                         bool err, Deltas& dl, Events<EV>& ev,
+                                         int32_t& sep_start) {
   if (c.ext & ORX_EXT_SEPARATION_DAMAGE) {  // build extension (readme.md:46-47)
     if (p1.d != p2.d) {
       if (sep_start < 0) sep_start = tick;
@@ -1775,6 +1795,422 @@ __device__ __forceinline__ void tick_game(const Cfg& c, Key key, Src& src, uint3
   status = s;
   dl.ret += (s == ORX_PLAYER1_WIN ? 1 : 0) - (s == ORX_PLAYER2_WIN ? 1 : 0);
   dl.eps += (uint32_t)(s - ORX_PLAYER1_WIN) <= (uint32_t)(ORX_TIE - ORX_PLAYER1_WIN) ? 1 : 0;
+}
+
+// ---------------------------------------------------------------------------
+// Moving NPCs (cfg.npc_policy != ORX_NPC_STAY): the reference's enemy-AI hook
+// Updater.decide_npc_move (updater.py:165-178) and its literal resolution of
+// every NPC move -- decisions for all NPCs before any move (:116-126), the
+// NPC shuffle (:127), handle_move for the players then the NPCs in that order
+// (:133-134, 180-243; NPC-vs-player and NPC-vs-NPC Block / Ambush / Flee, an
+// NPC stepping onto a staircase dies, :263-270), the death sweep (:136-145).
+// One lane per game, the literal sequence (the generic form of every entry
+// point; include/orx.h ORX_NPC_* has the policies).
+// ---------------------------------------------------------------------------
+// getrandbits(k) of the tick's CPython-random draws in keyed mode: the low k
+// bits of a reservoir segment (LSB first; a segment with fewer than k left is
+// skipped for good), then the top k bits of the next word of stream `s`;
+// with `refill` every word of `s` is a 30-bit segment of its own (the NPC
+// stream, purpose NPC, c2 = tick).  make_golden.TickBits / NpcBits.
+struct PyBits {
+  uint32_t res;
+  int32_t nb;
+  bool refill;
+  Stream s;
+  __device__ __forceinline__ uint32_t bits(int k, Key key) {
+    if (nb < k) {
+      if (refill) {
+        res = s.next(key) & 0x3FFFFFFFu;
+        nb = 30;
+      } else {
+        nb = 0;
+      }
+    }
+    if (nb >= k) {
+      const uint32_t r = res & ((1u << k) - 1u);
+      res >>= k;
+      nb -= k;
+      return r;
+    }
+    return s.next(key) >> (32 - k);
+  }
+};
+// stock-seed mode: the game's CPython random (getrandbits(k) = word >> (32 - k))
+struct MtBits {
+  MtStream* py;
+  __device__ __forceinline__ uint32_t bits(int k, Key key) { return py->next(key) >> (32 - k); }
+};
+// Random._randbelow_with_getrandbits(n) over a bit source (random.py)
+template <class Bits>
+__device__ __forceinline__ uint32_t randbelow_bits(Bits& b, Key key, uint32_t n, bool& err) {
+  const int k = 32 - __clz(n);
+  for (uint32_t t = 0; t < kWordCap; ++t) {
+    const uint32_t r = b.bits(k, key);
+    if (r < n) return r;
+  }
+  err = true;
+  return 0;
+}
+
+// The tick's NPC updents (updater.py:116-128): each NPC's decided move (by
+// slot), the shuffled order (position j -> slot) and which have acted.
+// Register NPCs: packed in 64-bit registers (4-bit slots, 3-bit moves, runtime
+// indices through shifts); dense NPCs: per-lane arrays.
+template <int NCAP>
+struct NpcTurns {
+  uint64_t ord, mv;
+  uint32_t acted;
+  __device__ __forceinline__ void clear() { ord = mv = 0ull; acted = 0u; }
+  __device__ __forceinline__ int slot(int j) const { return (int)((ord >> (4 * j)) & 15ull); }
+  __device__ __forceinline__ void set_slot(int j, int k) {
+    ord = (ord & ~(15ull << (4 * j))) | ((uint64_t)k << (4 * j));
+  }
+  __device__ __forceinline__ int32_t move(int k) const { return (int32_t)((mv >> (3 * k)) & 7ull); }
+  __device__ __forceinline__ void set_move(int k, int32_t m) {
+    mv = (mv & ~(7ull << (3 * k))) | ((uint64_t)m << (3 * k));
+  }
+  __device__ __forceinline__ bool has_acted(int k) const { return (acted >> k) & 1u; }
+  __device__ __forceinline__ void mark(int k) { acted |= 1u << k; }
+};
+template <>
+struct NpcTurns<kDense> {
+  uint8_t ord_[ORX_MAX_NPCS], mv_[ORX_MAX_NPCS];
+  uint32_t acted_[(ORX_MAX_NPCS + 31) / 32];
+  __device__ __forceinline__ void clear() {
+    for (int r = 0; r < (ORX_MAX_NPCS + 31) / 32; ++r) acted_[r] = 0u;
+  }
+  __device__ __forceinline__ int slot(int j) const { return ord_[j]; }
+  __device__ __forceinline__ void set_slot(int j, int k) { ord_[j] = (uint8_t)k; }
+  __device__ __forceinline__ int32_t move(int k) const { return mv_[k]; }
+  __device__ __forceinline__ void set_move(int k, int32_t m) { mv_[k] = (uint8_t)m; }
+  __device__ __forceinline__ bool has_acted(int k) const { return (acted_[k >> 5] >> (k & 31)) & 1u; }
+  __device__ __forceinline__ void mark(int k) { acted_[k >> 5] |= 1u << (k & 31); }
+};
+
+// The dungeon of the NPCs' depth nd (player 1's start depth) at the start of
+// the tick: a player's, when one stands on nd; else, under Unreachable with
+// player 2 still above nd (player 1 started on nd and has left it), its
+// generation-0 staircase from its key (stock-seed mode: player 1's dstore
+// ring); absent otherwise -- despawned (updater.py:245-257).
+struct NpcDepth {
+  bool present;
+  int32_t sx, sy, lay;
+};
+
+template <bool GRID, class Src>
+__device__ __forceinline__ NpcDepth npc_depth(const Cfg& c, Key key, Src& src, uint32_t game,
+                                              uint32_t ep, const Player& p1, const Player& p2,
+                                              bool& err) {
+  NpcDepth d{false, -1, -1, -1};
+  const int32_t nd = c.d1;
+  if (p1.d == nd) {
+    d = NpcDepth{true, p1.sx, p1.sy, p1.lay};
+  } else if (p2.d == nd) {
+    d = NpcDepth{true, p2.sx, p2.sy, p2.lay};
+  } else if (c.despawn == ORX_DESPAWN_UNREACHABLE && p2.d < nd) {
+    d.present = true;
+    if constexpr (Src::kMt) {
+      if (!src.recall(1, c.d1, nd, d.sx, d.sy, d.lay)) err = true;
+    } else {
+      dungeon_stair<GRID>(c, key, game, ep, nd, 0u, d.sx, d.sy, d.lay, err);
+    }
+  }
+  return d;
+}
+
+// dung.tiles[x, y] == StaircaseDown on the NPCs' depth (x, y in the grid)
+template <bool GRID>
+__device__ __forceinline__ bool npc_stair(const Cfg& c, const NpcDepth& d, int32_t x, int32_t y) {
+  if constexpr (GRID) return bank_tile(c, d.lay, x, y) == ORX_TILE_STAIRCASE_DOWN;
+  else return x == d.sx && y == d.sy;
+}
+
+// A player stands next to a staircase tile of the NPCs' depth: its NPCs stay
+// (the AI's guard, include/orx.h ORX_NPC_*)
+template <bool GRID>
+__device__ __forceinline__ bool next_to_stairs(const Cfg& c, const NpcDepth& d, const Player& p) {
+  if constexpr (GRID) {
+    bool any = false;
+#pragma unroll
+    for (int m = ORX_MOVE_UP; m <= ORX_MOVE_LEFT; ++m) {
+      int32_t x, y;
+      calc_pos(p.x, p.y, m, x, y);
+      any = any || (x >= 0 && x < c.W && y >= 0 && y < c.H && npc_stair<true>(c, d, x, y));
+    }
+    return any;
+  } else {
+    return abs(p.x - d.sx) + abs(p.y - d.sy) == 1;
+  }
+}
+
+// decide_npc_move (updater.py:165-178) for the NPC on cell key `nk`
+template <bool GRID, class Bits>
+__device__ __forceinline__ int32_t decide_npc_move(const Cfg& c, Key key, const NpcDepth& d,
+                                                   bool freeze, const Player& p1,
+                                                   const Player& p2, uint32_t nk, Bits& ai,
+                                                   bool& err) {
+  if (!d.present || freeze) return ORX_MOVE_STAY;
+  const int32_t x = (int32_t)(nk & 0xFFu), y = (int32_t)(nk >> 8);
+  int32_t m;
+  if (c.npc_pol == ORX_NPC_RANDOM) {
+    m = 1 + (int32_t)randbelow_bits(ai, key, 5u, err);   // random.choice(list(Move))
+  } else {                                               // ORX_NPC_CHASE
+    const bool h1 = p1.d == c.d1, h2 = p2.d == c.d1;
+    if (!h1 && !h2) return ORX_MOVE_STAY;
+    const int32_t d1 = abs(p1.x - x) + abs(p1.y - y), d2 = abs(p2.x - x) + abs(p2.y - y);
+    const bool to2 = h2 && (!h1 || d2 < d1);
+    const int32_t dx = (to2 ? p2.x : p1.x) - x, dy = (to2 ? p2.y : p1.y) - y;
+    m = abs(dx) > abs(dy) ? (dx > 0 ? ORX_MOVE_RIGHT : ORX_MOVE_LEFT)
+                          : (dy > 0 ? ORX_MOVE_DOWN : ORX_MOVE_UP);
+  }
+  int32_t tx, ty;
+  calc_pos(x, y, m, tx, ty);
+  return blocked<GRID>(c, d.lay, tx, ty) ? ORX_MOVE_STAY : m;
+}
+
+// The flag of a move into an occupied cell (updater.py:222-243): the
+// occupant (now on the target) Stays -> Block; its own target is the cell ->
+// Parry (dead code: an occupant on the cell never targets it); it acted
+// before the mover -> Ambush; else Flee.
+__device__ __forceinline__ int32_t occupant_flag(int32_t tx, int32_t ty, int32_t occ_move,
+                                                 bool occ_acted) {
+  int32_t ox, oy;
+  calc_pos(tx, ty, occ_move, ox, oy);
+  return occ_move == ORX_MOVE_STAY ? ORX_FLAG_BLOCK
+         : (ox == tx && oy == ty)  ? ORX_FLAG_PARRY
+         : occ_acted               ? ORX_FLAG_AMBUSH
+                                   : ORX_FLAG_FLEE;
+}
+
+// handle_move for a player in the moving-NPC tick (its occupancy test sees
+// the NPCs where they stand now; a hit NPC's flag follows its decided move)
+template <int NCAP, bool EV, bool GRID, class Src, class S, class M>
+__device__ __forceinline__ void mov_player(const Cfg& c, Key key, Src& src, Player& self,
+                                           Player& other, int32_t other_start, bool self_first,
+                                           int32_t self_iden, Npcs<NCAP>& npc,
+                                           const NpcTurns<NCAP>& turns, M& m, S& spawn,
+                                           Deltas& dl, bool& err, Events<EV>& ev) {
+  if (self.move == ORX_MOVE_STAY) return;
+  const int32_t tx = self.tx, ty = self.ty;
+  const int32_t dmg = c.player_dmg_net;
+  if (other.d == self.d && other.x == tx && other.y == ty) {
+    const int32_t flag = occupant_flag(tx, ty, other.move, !self_first);
+    if (dmg > 0) other.hp -= dmg;
+    dl.combat += 1;
+    ev.emit(ORX_EV_COMBAT, self_iden, 3 - self_iden, flag);
+    return;
+  }
+  const int q = (NCAP > 0 && self.d == c.d1) ? npc.find(pack_xy(tx, ty)) : -1;
+  if (q >= 0) {
+    const int32_t flag = occupant_flag(tx, ty, turns.move(q), turns.has_acted(q));
+    if (dmg > 0) m.put(q, max(m.get(q) - dmg, -128));
+    dl.combat += 1;
+    ev.emit(ORX_EV_COMBAT, self_iden, 3 + q, flag);
+    return;
+  }
+  if (stair_tile<GRID>(c, self, tx, ty)) {
+    descend<NCAP, EV, GRID>(c, key, src, self, other, other_start, npc, spawn, dl, err, self_iden,
+                            ev);
+    return;
+  }
+  self.x = tx;
+  self.y = ty;
+  ev.emit(ORX_EV_POSITION, self_iden, self.d, (tx & 0xFFFF) | (ty << 16));
+}
+
+// handle_move for NPC slot k (its decided move mv != Stay) on the NPCs' depth
+template <int NCAP, bool EV, bool GRID, class M>
+__device__ __forceinline__ void mov_npc(const Cfg& c, int k, int32_t mv, Player& p1, Player& p2,
+                                        Npcs<NCAP>& npc, const NpcTurns<NCAP>& turns,
+                                        const NpcDepth& d, M& m, Deltas& dl, Events<EV>& ev) {
+  const uint32_t k0 = npc.get(k);
+  int32_t tx, ty;
+  calc_pos((int32_t)(k0 & 0xFFu), (int32_t)(k0 >> 8), mv, tx, ty);
+  const uint32_t tk = pack_xy(tx, ty);
+  const int32_t nd = c.d1, dmg = c.npc_dmg_net;
+  const bool on1 = p1.d == nd && p1.x == tx && p1.y == ty;
+  const bool on2 = p2.d == nd && p2.x == tx && p2.y == ty;
+  if (on1 || on2) {  // the players acted first: Block or Ambush
+    const int32_t flag = occupant_flag(tx, ty, on1 ? p1.move : p2.move, true);
+    if (dmg > 0) {
+      if (on1) p1.hp -= dmg;
+      else p2.hp -= dmg;
+    }
+    dl.combat += 1;
+    ev.emit(ORX_EV_COMBAT, 3 + k, on1 ? 1 : 2, flag);
+    return;
+  }
+  const int q = npc.find(tk);
+  if (q >= 0) {
+    const int32_t flag = occupant_flag(tx, ty, turns.move(q), turns.has_acted(q));
+    if (dmg > 0) m.put(q, max(m.get(q) - dmg, -128));
+    dl.combat += 1;
+    ev.emit(ORX_EV_COMBAT, 3 + k, 3 + q, flag);
+    return;
+  }
+  if (npc_stair<GRID>(c, d, tx, ty)) {  // handle_descend: an NPC dies (updater.py:263-270)
+    ev.emit(ORX_EV_DEATH, 3 + k, 0, 0);
+    npc.mark_dead(k);
+    npc.kill(k);
+    dl.npc_death += 1;
+    return;
+  }
+  if constexpr (NCAP == kDense) npc.kill_at(k0);  // (the old cell of the occupancy grid)
+  npc.set(k, tk);
+  ev.emit(ORX_EV_POSITION, 3 + k, nd, (tx & 0xFFFF) | (ty << 16));
+}
+
+// The death sweep over every NPC (updater.py:136-145: GameState.entities
+// backwards, i.e. descending slots), any of which may have been hit
+template <int NCAP, bool EV, class M>
+__device__ __forceinline__ void npc_sweep(const Cfg& c, Npcs<NCAP>& npc, M& m, Deltas& dl,
+                                          Events<EV>& ev) {
+  if constexpr (NCAP == kDense) {
+    for (int r = (c.K - 1) >> 5; r >= 0; --r) {
+      uint32_t a = npc.rows[(size_t)r * npc.B];
+      while (a) {
+        const int j = 31 - __clz(a);
+        a &= ~(1u << j);
+        const int k = 32 * r + j;
+        if (m.get(k) <= 0) {
+          ev.emit(ORX_EV_DEATH, 3 + k, 0, 0);
+          npc.mark_dead(k);
+          npc.kill(k);
+          dl.npc_death += 1;
+        }
+      }
+    }
+  } else if constexpr (NCAP > 0) {
+#pragma unroll
+    for (int k = NCAP - 1; k >= 0; --k) {
+      if (k < c.K && npc.is_alive(k) && m.get(k) <= 0) {
+        ev.emit(ORX_EV_DEATH, 3 + k, 0, 0);
+        npc.mark_dead(k);
+        npc.kill(k);
+        dl.npc_death += 1;
+      }
+    }
+  }
+}
+
+template <int NCAP, bool EV, bool GRID, class Src, class M, class Bits>
+__device__ __forceinline__ void tick_moving_body(const Cfg& c, Key key, Src& src, uint32_t game,
+                                                 uint32_t ep, Player& p1, Player& p2,
+                                                 Npcs<NCAP>& npc, M& m, int32_t& tick,
+                                                 int32_t& status, bool& err, Deltas& dl,
+                                                 Events<EV>& ev, int32_t& sep_start, Bits& sh,
+                                                 Bits& ai) {
+  p1.heal = p2.heal = 0;
+  calc_pos(p1.x, p1.y, p1.move, p1.tx, p1.ty);          // updater.py:89-98
+  if (blocked<GRID>(c, p1.lay, p1.tx, p1.ty)) p1.move = ORX_MOVE_STAY;
+  calc_pos(p2.x, p2.y, p2.move, p2.tx, p2.ty);
+  if (blocked<GRID>(c, p2.lay, p2.tx, p2.ty)) p2.move = ORX_MOVE_STAY;
+  const bool p1_first = randbelow_bits(sh, key, 2u, err) == 1u;   // :114
+  NpcTurns<NCAP> turns;
+  turns.clear();
+  int n = 0;
+  NpcDepth d{false, -1, -1, -1};
+  if constexpr (NCAP > 0) {
+    d = npc_depth<GRID>(c, key, src, game, ep, p1, p2, err);
+    const bool freeze = d.present && ((p1.d == c.d1 && next_to_stairs<GRID>(c, d, p1)) ||
+                                      (p2.d == c.d1 && next_to_stairs<GRID>(c, d, p2)));
+    // decide_npc_move for every NPC in GameState.entities order (:116-126)
+    if constexpr (NCAP == kDense) {
+      for (int r = 0; r < (c.K + 31) >> 5; ++r) {
+        uint32_t a = npc.rows[(size_t)r * npc.B];
+        while (a) {
+          const int k = 32 * r + (int)__builtin_ctz(a);
+          a &= a - 1u;
+          turns.set_move(k, decide_npc_move<GRID>(c, key, d, freeze, p1, p2, npc.get(k), ai, err));
+          turns.set_slot(n++, k);
+        }
+      }
+    } else {
+#pragma unroll 1
+      for (int k = 0; k < c.K; ++k) {
+        if (!npc.is_alive(k)) continue;
+        turns.set_move(k, decide_npc_move<GRID>(c, key, d, freeze, p1, p2, npc.get(k), ai, err));
+        turns.set_slot(n++, k);
+      }
+    }
+    // random.shuffle(npcs) (:127): Fisher-Yates over the list
+#pragma unroll 1
+    for (int i = n - 1; i >= 1; --i) {
+      const int j = (int)randbelow_bits(sh, key, (uint32_t)i + 1u, err);
+      const int si = turns.slot(i), sj = turns.slot(j);
+      turns.set_slot(i, sj);
+      turns.set_slot(j, si);
+    }
+  }
+  // handle_move in initiative order (:133-134): the players, then the NPCs
+  auto&& spawn = src.spawn(tick);
+  Player A = pick(p1_first, p1, p2);
+  Player Bp = pick(p1_first, p2, p1);
+  const int32_t a_iden = p1_first ? 1 : 2;
+  mov_player<NCAP, EV, GRID>(c, key, src, A, Bp, p1_first ? c.d2 : c.d1, true, a_iden, npc, turns,
+                             m, spawn, dl, err, ev);
+  mov_player<NCAP, EV, GRID>(c, key, src, Bp, A, p1_first ? c.d1 : c.d2, false, 3 - a_iden, npc,
+                             turns, m, spawn, dl, err, ev);
+  p1 = pick(p1_first, A, Bp);
+  p2 = pick(p1_first, Bp, A);
+  if constexpr (NCAP > 0) {
+#pragma unroll 1
+    for (int j = 0; j < n; ++j) {
+      const int k = turns.slot(j);
+      const int32_t mv = turns.move(k);
+      if (mv != ORX_MOVE_STAY) mov_npc<NCAP, EV, GRID>(c, k, mv, p1, p2, npc, turns, d, m, dl, ev);
+      turns.mark(k);
+    }
+    npc_sweep(c, npc, m, dl, ev);                       // :136-145
+  }
+  end_tick<EV>(c, key, game, ep, p1, p2, tick, status, err, dl, ev, sep_start);
+}
+
+// One Updater.update with moving NPCs (p1.move / p2.move = the raw moves):
+// the tick's CPython-random draws -- the player shuffle, the AI's choices, the
+// NPC shuffle -- from the tick block's word a and the SHUFFLE / NPC streams
+// (keyed), or from the game's CPython random in the reference's call order
+// (stock-seed mode).
+template <int NCAP, bool EV, bool GRID, class Src, class M>
+__device__ __forceinline__ void tick_moving(const Cfg& c, Key key, Src& src, uint32_t game,
+                                            uint32_t ep, Player& p1, Player& p2,
+                                            Npcs<NCAP>& npc, M& m, int32_t& tick,
+                                            int32_t& status, bool& err, Deltas& dl,
+                                            Events<EV>& ev, int32_t& sep_start) {
+  if constexpr (Src::kMt) {
+    MtBits b{&src.py};
+    tick_moving_body<NCAP, EV, GRID>(c, key, src, game, ep, p1, p2, npc, m, tick, status, err, dl,
+                                     ev, sep_start, b, b);
+  } else {
+    PyBits sh, ai;
+    sh.res = tick_block(key, game, ep, tick).a;
+    sh.nb = 32;
+    sh.refill = false;
+    sh.s.init(game, ep, (uint32_t)tick, tag(PUR_SHUFFLE, 0));
+    ai.res = 0u;
+    ai.nb = 0;
+    ai.refill = true;
+    ai.s.init(game, ep, (uint32_t)tick, tag(PUR_NPC, 0));
+    tick_moving_body<NCAP, EV, GRID>(c, key, src, game, ep, p1, p2, npc, m, tick, status, err, dl,
+                                     ev, sep_start, sh, ai);
+  }
+}
+
+// Event records per game-tick (orx_max_events): 6 + 2 K with moving NPCs
+__host__ __device__ inline int32_t max_events_for(int32_t npc_policy, int32_t K) {
+  return (npc_policy != ORX_NPC_STAY && 6 + 2 * K > ORX_MAX_EVENTS) ? 6 + 2 * K : ORX_MAX_EVENTS;
+}
+
+// After a moving-NPC tick: the register NPCs' cells to HBM (the dense form
+// moves them in place)
+template <int NCAP>
+__device__ __forceinline__ void store_npc_cells(const orx_state_t& st, const Cfg& c, uint32_t B,
+                                                uint32_t i, const Npcs<NCAP>& npc) {
+  if constexpr (NCAP > 0 && NCAP != kDense) {
+#pragma unroll
+    for (int k = 0; k < NCAP; ++k)
+      if (k < c.K) st.npc_pos[(size_t)k * B + i] = (uint16_t)npc.get(k);
+  }
 }
 
 template <int NCAP, bool EV, bool GRID = false, class M>
@@ -1979,6 +2415,8 @@ __device__ __forceinline__ Cfg make_cfg(const orx_cfg_t& h, const orx_state_t& s
   c.d2 = h.start_mode == ORX_START_SEPARATED ? h.p2_depth : 0;
   c.K = h.n_npcs; c.npc_hp = h.npc_health; c.player_hp = h.player_health;
   c.player_dmg_net = h.player_damage - h.player_armor;
+  c.npc_pol = h.npc_policy;
+  c.npc_dmg_net = h.npc_damage - h.npc_armor;
   c.autoreset = h.autoreset;
   c.ext = h.flags;
   c.sep_period = h.sep_period > 0 ? h.sep_period : 1;
@@ -2071,7 +2509,7 @@ struct NoOut {
   __device__ __forceinline__ void operator()(const Player&, const Player&, int32_t, int32_t) {}
 };
 
-template <int NCAP, bool EV, bool GRID, bool EXT, class A, class O = NoOut>
+template <int NCAP, bool EV, bool GRID, bool EXT, bool MOV, class A, class O = NoOut>
 __device__ __forceinline__ void step_game(const orx_cfg_t& hc, const orx_state_t& st, A get_action,
                                           uint32_t B, uint32_t i, Key key, uint32_t off,
                                           int32_t* __restrict__ events,
@@ -2145,12 +2583,20 @@ __device__ __forceinline__ void step_game(const orx_cfg_t& hc, const orx_state_t
   }
   NpcMem m{st.npc_pos, st.npc_health, B, i};
   Deltas dl = {0, 0, 0, 0, 0, 0};
-  Events<EV> ev{EV ? events + (size_t)i * ORX_MAX_EVENTS * 4 : nullptr, 0};
+  const int32_t ev_cap = MOV ? max_events_for(c.npc_pol, c.K) : ORX_MAX_EVENTS;
+  Events<EV> ev{EV ? events + (size_t)i * (size_t)ev_cap * 4 : nullptr, 0, ev_cap};
   bool err = false;
-  const bool p1_first = kOut ? first_from_packed(tb0.a, key, game, ep, tick, err)
-                             : p1_first_draw(key, game, ep, tick, err);
-  tick_game<NCAP, EV, GRID>(c, key, game, ep, p1_first, p1, p2, npc, items, m, tick, status, err,
-                            dl, ev, sep);
+  if constexpr (MOV) {  // moving NPCs: the literal ordered tick draws its own shuffles
+    PhiloxSrc src{key, game, ep};
+    tick_moving<NCAP, EV, GRID>(c, key, src, game, ep, p1, p2, npc, m, tick, status, err, dl, ev,
+                                sep);
+    store_npc_cells(st, c, B, i, npc);
+  } else {
+    const bool p1_first = kOut ? first_from_packed(tb0.a, key, game, ep, tick, err)
+                               : p1_first_draw(key, game, ep, tick, err);
+    tick_game<NCAP, EV, GRID>(c, key, game, ep, p1_first, p1, p2, npc, items, m, tick, status,
+                              err, dl, ev, sep);
+  }
   if (c.ext & ORX_EXT_SEPARATION_DAMAGE) st.sep_start[i] = sep;
   store_rpg(st, c, B, i, p1, p2, npc, items);
   store_players_tick<GRID>(st, B, i, p1, p2, dl.descend != 0, EXT ? true : dl.combat != 0);
@@ -2162,7 +2608,7 @@ __device__ __forceinline__ void step_game(const orx_cfg_t& hc, const orx_state_t
   out(p1, p2, tick, status);
 }
 
-template <int NCAP, bool EV, bool GRID, bool EXT = true>
+template <int NCAP, bool EV, bool GRID, bool EXT = true, bool MOV = false>
 __global__ void __launch_bounds__(256) step_kernel(orx_cfg_t hc, orx_state_t st,
                                                    const int8_t* __restrict__ actions, uint32_t B,
                                                    Key key, uint32_t off,
@@ -2170,7 +2616,7 @@ __global__ void __launch_bounds__(256) step_kernel(orx_cfg_t hc, orx_state_t st,
                                                    int32_t* __restrict__ n_events) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= B) return;
-  step_game<NCAP, EV, GRID, EXT>(
+  step_game<NCAP, EV, GRID, EXT, MOV>(
       hc, st,
       [&](const Player&, const Player&, int32_t, uint32_t, const W4&) {
         return reinterpret_cast<const uint16_t*>(actions)[i];
@@ -2229,7 +2675,7 @@ __global__ void __launch_bounds__(256) policy_kernel(orx_state_t st, int32_t pol
 #ifndef ORX_ENV_DIAG  // diagnostic builds: 1 no tick, 2 no observation rows
 #define ORX_ENV_DIAG 0
 #endif
-template <int NCAP, bool GRID, bool EXT>
+template <int NCAP, bool GRID, bool EXT, bool MOV = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORX_ENV_WAVES)))
 env_step_kernel(
     orx_cfg_t hc, orx_state_t st, const void* __restrict__ actions, int32_t dsize, int32_t cols,
@@ -2294,8 +2740,8 @@ env_step_kernel(
       pair = pack_actions(l1, l2);
       out(p1, p2, st.tick[i], before);
     } else {
-      step_game<NCAP, false, GRID, EXT>(hc, st, get_action, B, i, key, off, nullptr, nullptr,
-                                        out);
+      step_game<NCAP, false, GRID, EXT, MOV>(hc, st, get_action, B, i, key, off, nullptr,
+                                             nullptr, out);
     }
     reinterpret_cast<uint16_t*>(act)[i] = pair;
   }
@@ -3166,7 +3612,7 @@ __device__ __forceinline__ uint32_t pack_cell(int32_t x, int32_t y) {
 // player 1's depth (3) and tick | status << 27 (5), lane 2j+1 the staircases
 // (1), player 2's depth (4) and the healths (2) -- each cell pair and health
 // pair assembled from the lane's own value and its partner's (DPP).
-template <int AUX, bool CF = false>
+template <int AUX, bool CF = false, bool ACT = true>
 struct PairWriter {
   static constexpr int kStores = CF ? 3 : 7;
   static constexpr int kRows = CF ? ORX_OBS_COMPACT_FIELDS : ORX_OBS_FIELDS;
@@ -3223,13 +3669,15 @@ struct PairWriter {
       for (int k = 0; k < 7; ++k)
         __builtin_amdgcn_raw_buffer_store_b32(vals[k], ro, (int32_t)vo[k], 0, AUX);
     }
-    const auto ra = __builtin_amdgcn_make_buffer_rsrc(act, 0, (int32_t)(B * 2u), kBufferDword3);
-    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)move, ra, (int32_t)va, 0, AUX);
+    if constexpr (ACT) {
+      const auto ra = __builtin_amdgcn_make_buffer_rsrc(act, 0, (int32_t)(B * 2u), kBufferDword3);
+      __builtin_amdgcn_raw_buffer_store_b8((uint8_t)move, ra, (int32_t)va, 0, AUX);
+    }
     skip();
   }
   __device__ __forceinline__ void skip() {  // the next tick's rows
     obs += (size_t)kRows * B;
-    act += (size_t)2 * B;
+    if constexpr (ACT) act += (size_t)2 * B;
   }
 };
 
@@ -3237,6 +3685,12 @@ struct PairWriter {
 // (at most separation damage).  NCAP 0 / 8 / 16 (register NPCs, no dense
 // grid), empty dungeons, obs and act given.  The bench's C3 shards run
 // pair_rollout_kernel<8, 1, 2, false>.
+// PM 6 (round 6): a replay of a move log (orx_step_n; flags 0, empty
+// dungeons, observation rows given) -- each lane's move is its player's byte
+// of `act`, which is then the log [n_ticks][B][2] (read, never written; no
+// action rows are stored: the log is the actions); a pair outside the Move
+// codes stops the game in the rare block (orx_step's rule), and the
+// initiative block is drawn only by a rare tick that needs the order.
 // (diagnostic builds may add attributes, e.g. an occupancy target)
 #ifndef ORX_PAIR_ATTR
 #define ORX_PAIR_ATTR
@@ -3341,10 +3795,19 @@ __global__ void __launch_bounds__(GRID ? 512 : kRolloutBlock) ORX_PAIR_ATTR
   // the RandomBot lane takes the tick block's first accepted field, as
   // rollout_tick's single random player
   constexpr bool kMixed = PM == 4 || PM == 5;
+  constexpr bool kLog = PM == 6;
   const bool rb_lane = kMixed && (isB == (PM == 5));
   constexpr int need = (PM == 1 || PM == 3) ? 2 : kMixed ? 1 : 0;
-  PairWriter<AUX, CF> traj(obs, act, B, i, who);
-  const int32_t* const obs_end = obs + (size_t)n_ticks * PairWriter<AUX, CF>::kRows * B;
+  PairWriter<AUX, CF, !kLog> traj(obs, act, B, i, who);
+  const int32_t* const obs_end = obs + (size_t)n_ticks * PairWriter<AUX, CF, !kLog>::kRows * B;
+  // PM 6: this lane's byte of the log, the next tick's prefetched while this
+  // tick runs (the last tick re-reads its own instead of branching)
+  const int8_t* const lg = act + 2u * i + who;
+  int32_t a_next = 0;
+  if constexpr (kLog) {
+    a_next = lg[0];
+    asm volatile("" : "+v"(a_next));
+  }
   // every state load resolved before the tick loop: a value first read in the
   // loop leaves its load pending at the loop head, and that wait then also
   // covers the previous ticks' row stores (vmcnt counts both) -- each tick
@@ -3483,14 +3946,25 @@ __global__ void __launch_bounds__(GRID ? 512 : kRolloutBlock) ORX_PAIR_ATTR
         moves_from_block(tb, 1, key, game, ep, tick, r0, r1, err);
         move = rb_lane ? r0 : smove;
       }
+    } else if constexpr (kLog) {
+      move = a_next;
+      a_next = lg[(size_t)(t + 1 < n_ticks ? t + 1 : t) * 2u * B];
     } else {
       const int32_t dx = me.sx - me.x, dy = me.sy - me.y;
       const int32_t adx = dx < 0 ? -dx : dx, ady = dy < 0 ? -dy : dy;
       move = adx > ady ? (dx > 0 ? ORX_MOVE_RIGHT : ORX_MOVE_LEFT)
                        : (dy > 0 ? ORX_MOVE_DOWN : ORX_MOVE_UP);
     }
+    // PM 6: a pair outside the Move codes stops the game (rare); its
+    // targets are computed as Stays
+    bool bad = false;
+    if constexpr (kLog) {
+      const bool ok_me = (uint32_t)(move - ORX_MOVE_UP) <= (uint32_t)(ORX_MOVE_STAY - ORX_MOVE_UP);
+      bad = (status == ORX_IN_PROGRESS) & !(ok_me & (pair_swap(ok_me ? 1 : 0) != 0));
+      move = ok_me ? move : ORX_MOVE_STAY;
+    }
     me.move = move;
-    const bool in_progress = status == ORX_IN_PROGRESS;
+    const bool in_progress = status == ORX_IN_PROGRESS && !bad;
     // effective target (own cell when blocked: the border, clamped)
     int32_t tx, ty;
     calc_pos(me.x, me.y, move, tx, ty);
@@ -3530,6 +4004,7 @@ __global__ void __launch_bounds__(GRID ? 512 : kRolloutBlock) ORX_PAIR_ATTR
     // (ORX_DIAG & 128: no rare block -- an ISA census of the common tick only,
     // never run)
     const bool rare = (ORX_DIAG & 128) ? false : (!in_progress | (min(mt, min_swapped(z)) == 0u));
+    // (PM 6: a bad pair is !in_progress with status still InProgress)
     const int32_t ft = tick + 1;
     const bool end = c.max_ticks && ft >= c.max_ticks;
     bool took_ordered = false;
@@ -3575,8 +4050,17 @@ __global__ void __launch_bounds__(GRID ? 512 : kRolloutBlock) ORX_PAIR_ATTR
       // instruction stream for both -- and the lanes swap them.
       bool fast = false;
       const int32_t osx = pair_swap(me.sx), osy = pair_swap(me.sy);
-      if constexpr ((PM == 2 || kMixed) && NCAP == 0 && !GRID) {
-        if (!in_progress & (c.autoreset != 0)) {  // uniform over the pair
+      if constexpr (kLog) {
+        if (bad) {  // orx_step's rule: the game stops, nothing else changes
+          status = ORX_STATUS_BAD_ACTION;
+          fast = true;
+        }
+        // the initiative bits for a meet (the lean meet below; the ordered
+        // tick draws them itself)
+        if (meet & !bad) tb.a = tick_block(key, game, ep, tick).a;
+      }
+      if constexpr ((PM == 2 || kMixed || kLog) && NCAP == 0 && !GRID) {
+        if (!in_progress & !bad & (c.autoreset != 0)) {  // uniform over the pair
           // The next episode (setup_game's keyed first-block form), its two
           // starting dungeons split over the pair: each lane draws its own
           // player's DUNGEON block beside the INIT block, and the lanes swap
@@ -3632,7 +4116,7 @@ __global__ void __launch_bounds__(GRID ? 512 : kRolloutBlock) ORX_PAIR_ATTR
           }
         }
       }
-      if constexpr ((PM == 1 || kMixed) && NCAP > 0) {
+      if constexpr ((PM == 1 || kMixed || kLog) && NCAP > 0) {
         // NPC hits without a meet or a staircase (C3's common rare tick): the
         // attackers stay, the other player moves; both lanes apply both hits
         // to their identical NPC registers (npc_hits: order-free without the
@@ -3718,7 +4202,7 @@ __global__ void __launch_bounds__(GRID ? 512 : kRolloutBlock) ORX_PAIR_ATTR
 #endif
         }
       }
-      if constexpr (PM == 1 || PM == 3 || kMixed) {
+      if constexpr (PM == 1 || PM == 3 || kMixed || kLog) {
         // a meet without a staircase or an NPC hit: rare_tick's lean meet,
         // the two moves in the drawn order (the tick block's word a; an
         // all-reject word takes the ordered tick), from each lane's side;
@@ -3763,7 +4247,7 @@ __global__ void __launch_bounds__(GRID ? 512 : kRolloutBlock) ORX_PAIR_ATTR
 #endif
         }
       }
-      if ((PM == 2 || kMixed) && !GRID &&
+      if ((PM == 2 || kMixed || kLog) && !GRID &&
           (in_progress & !meet & (st_me != (st_o != 0)) & !hit_me & (hit_o == 0))) {
 #ifdef ORX_STAMPS
         ORX_CYC_BEGIN(cyf);
@@ -4108,7 +4592,7 @@ __global__ void __launch_bounds__(256) mt_policy_kernel(orx_state_t st, int32_t 
 }
 #endif  // ORX_HOST_TU
 
-template <int NCAP, bool EV, bool GRID>
+template <int NCAP, bool EV, bool GRID, bool MOV = false>
 __global__ void __launch_bounds__(256) mt_step_kernel(orx_cfg_t hc, orx_state_t st,
                                                       const int8_t* __restrict__ actions,
                                                       uint32_t B, Key key, uint32_t off,
@@ -4161,14 +4645,21 @@ __global__ void __launch_bounds__(256) mt_step_kernel(orx_cfg_t hc, orx_state_t 
   load_rpg(st, c, B, i, p1, p2, npc, items);
   NpcMem m{st.npc_pos, st.npc_health, B, i};
   Deltas dl = {0, 0, 0, 0, 0, 0};
-  Events<EV> ev{EV ? events + (size_t)i * ORX_MAX_EVENTS * 4 : nullptr, 0};
+  const int32_t ev_cap = MOV ? max_events_for(c.npc_pol, c.K) : ORX_MAX_EVENTS;
+  Events<EV> ev{EV ? events + (size_t)i * (size_t)ev_cap * 4 : nullptr, 0, ev_cap};
   bool err = false;
   MtSrc src;
   src.open(st, c, B, i);
-  const bool p1_first = mt_shuffles(src.py, npc, err);
   int32_t sep = (c.ext & ORX_EXT_SEPARATION_DAMAGE) ? st.sep_start[i] : -1;
-  tick_game<NCAP, EV, GRID>(c, key, src, game, ep, p1_first, p1, p2, npc, items, m, tick, status,
-                            err, dl, ev, sep);
+  if constexpr (MOV) {
+    tick_moving<NCAP, EV, GRID>(c, key, src, game, ep, p1, p2, npc, m, tick, status, err, dl, ev,
+                                sep);
+    store_npc_cells(st, c, B, i, npc);
+  } else {
+    const bool p1_first = mt_shuffles(src.py, npc, err);
+    tick_game<NCAP, EV, GRID>(c, key, src, game, ep, p1_first, p1, p2, npc, items, m, tick,
+                              status, err, dl, ev, sep);
+  }
   src.close();
   store_rpg(st, c, B, i, p1, p2, npc, items);
   if (c.ext & ORX_EXT_SEPARATION_DAMAGE) st.sep_start[i] = sep;
@@ -4259,7 +4750,7 @@ __global__ void __launch_bounds__(256) mt_rollout_kernel(orx_cfg_t hc, orx_state
 // leaves this tick's stores in flight -- with the row branch at run time the
 // compiler's wait at the loop head has to assume a path without stores and
 // drains them all every tick.
-template <int NCAP, bool GRID, int ROWS>
+template <int NCAP, bool GRID, int ROWS, bool MOV = false>
 __device__ __forceinline__ void step_n_game(const orx_cfg_t& hc, const orx_state_t& st,
                                             const int8_t* __restrict__ actions, int32_t n_ticks,
                                             int32_t* __restrict__ obs, uint32_t B, uint32_t i,
@@ -4304,10 +4795,17 @@ __device__ __forceinline__ void step_n_game(const orx_cfg_t& hc, const orx_state
       } else {
         bool err = false;
         const int32_t descents = dl.descend;
-        const bool p1_first = p1_first_draw(key, game, ep, tick, err);
         Events<false> ev{nullptr, 0};
-        tick_game<NCAP, false, GRID>(c, key, game, ep, p1_first, p1, p2, npc, items, m, tick,
-                                     status, err, dl, ev, sep);
+        if constexpr (MOV) {
+          PhiloxSrc src{key, game, ep};
+          tick_moving<NCAP, false, GRID>(c, key, src, game, ep, p1, p2, npc, m, tick, status, err,
+                                         dl, ev, sep);
+          npc_dirty = true;
+        } else {
+          const bool p1_first = p1_first_draw(key, game, ep, tick, err);
+          tick_game<NCAP, false, GRID>(c, key, game, ep, p1_first, p1, p2, npc, items, m, tick,
+                                       status, err, dl, ev, sep);
+        }
         stairs_dirty |= dl.descend != descents;
       }
     } else if (c.autoreset) {
@@ -4328,10 +4826,11 @@ __device__ __forceinline__ void step_n_game(const orx_cfg_t& hc, const orx_state
   st.episode[i] = (int32_t)ep;
   if (c.ext & ORX_EXT_SEPARATION_DAMAGE) st.sep_start[i] = sep;
   if (NCAP > 0 && (npc_dirty || dl.npc_death)) npc.store_alive(st.npc_alive, B, i);
+  if (MOV && npc_dirty) store_npc_cells(st, c, B, i, npc);
   flush_deltas(st, B, i, dl);
 }
 
-template <int NCAP, bool GRID>
+template <int NCAP, bool GRID, bool MOV = false>
 __global__ void __launch_bounds__(256) step_n_kernel(orx_cfg_t hc, orx_state_t st,
                                                      const int8_t* __restrict__ actions,
                                                      int32_t n_ticks, int32_t* __restrict__ obs,
@@ -4340,11 +4839,88 @@ __global__ void __launch_bounds__(256) step_n_kernel(orx_cfg_t hc, orx_state_t s
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= B) return;
   if (obs == nullptr)  // (uniform)
-    step_n_game<NCAP, GRID, 0>(hc, st, actions, n_ticks, obs, B, i, key, off);
+    step_n_game<NCAP, GRID, 0, MOV>(hc, st, actions, n_ticks, obs, B, i, key, off);
   else if (fmt == ORX_OBS_COMPACT)
-    step_n_game<NCAP, GRID, 2>(hc, st, actions, n_ticks, obs, B, i, key, off);
+    step_n_game<NCAP, GRID, 2, MOV>(hc, st, actions, n_ticks, obs, B, i, key, off);
   else
-    step_n_game<NCAP, GRID, 1>(hc, st, actions, n_ticks, obs, B, i, key, off);
+    step_n_game<NCAP, GRID, 1, MOV>(hc, st, actions, n_ticks, obs, B, i, key, off);
+}
+
+// orx_rollout with moving NPCs (cfg.npc_policy): n_ticks x (the bots' moves,
+// then the moving-NPC tick or the autoreset), one lane per game, each tick's
+// observation row (format fmt) and actions written when obs / act are given.
+// MT: stock-seed mode (the bots and the tick draw from the game's CPython
+// random in the reference's call order, as mt_rollout_kernel).
+template <int NCAP, bool GRID, bool MT>
+__global__ void __launch_bounds__(256) mov_rollout_kernel(orx_cfg_t hc, orx_state_t st,
+                                                          int32_t pol1, int32_t pol2,
+                                                          int32_t n_ticks,
+                                                          int32_t* __restrict__ obs,
+                                                          int8_t* __restrict__ act, uint32_t B,
+                                                          Key key, uint32_t off, int32_t fmt) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B) return;
+  const Cfg c = make_cfg(hc, st);
+  const uint32_t game = off + i;
+  Player p1, p2;
+  load_players<GRID>(st, B, i, p1, p2);
+  int32_t tick = st.tick[i];
+  int32_t status = st.status[i];
+  uint32_t ep = (uint32_t)st.episode[i];
+  Npcs<NCAP> npc;
+  npc.bind(st, c, B, i);
+  load_npcs(st, c, B, i, npc);
+  NpcMem m{st.npc_pos, st.npc_health, B, i};
+  Items<NCAP> items;
+  load_rpg(st, c, B, i, p1, p2, npc, items);
+  Deltas dl = {0, 0, 0, 0, 0, 0};
+  int32_t sep = (c.ext & ORX_EXT_SEPARATION_DAMAGE) ? st.sep_start[i] : -1;
+  bool stairs_dirty = false, npc_dirty = false;
+  std::conditional_t<MT, MtSrc, PhiloxSrc> src;
+  if constexpr (MT) src.open(st, c, B, i);
+  else src = PhiloxSrc{key, game, ep};
+  TrajWriter<false> traj(obs, act, B, i, fmt);
+  const bool rng = pol1 == ORX_POLICY_RANDOM || pol2 == ORX_POLICY_RANDOM;
+  for (int32_t t = 0; t < n_ticks; ++t) {
+    int32_t a1 = ORX_MOVE_STAY, a2 = ORX_MOVE_STAY;
+    bool err = false;
+    if constexpr (MT) {
+      mt_policy_pair(src.py, pol1, pol2, p1, p2, a1, a2, err);
+    } else {
+      const W4 tb = rng ? tick_block(key, game, ep, tick) : W4{0u, 0u, 0u, 0u};
+      policy_pair(key, game, ep, tick, pol1, pol2, tb, p1, p2, a1, a2);
+    }
+    if (status == ORX_IN_PROGRESS) {
+      p1.move = a1;
+      p2.move = a2;
+      const int32_t descents = dl.descend;
+      Events<false> ev{nullptr, 0};
+      tick_moving<NCAP, false, GRID>(c, key, src, game, ep, p1, p2, npc, m, tick, status, err, dl,
+                                     ev, sep);
+      stairs_dirty |= dl.descend != descents;
+      npc_dirty = true;
+    } else if (c.autoreset) {
+      ep += 1;
+      if constexpr (!MT) src.ep = ep;
+      setup_game<NCAP, GRID>(c, key, src, p1, p2, npc, tick, status);
+      if constexpr (NCAP > 0) store_new_npcs(st, c, B, i, npc);
+      stairs_dirty = true;
+      npc_dirty = true;
+      sep = -1;
+    }
+    traj.write(t, p1, p2, tick, status, a1, a2);
+  }
+  if constexpr (MT) src.close();
+  store_players<GRID>(st, B, i, p1, p2, stairs_dirty);
+  st.tick[i] = tick;
+  st.status[i] = status;
+  st.episode[i] = (int32_t)ep;
+  if (c.ext & ORX_EXT_SEPARATION_DAMAGE) st.sep_start[i] = sep;
+  if (NCAP > 0 && npc_dirty) {
+    npc.store_alive(st.npc_alive, B, i);
+    store_npc_cells(st, c, B, i, npc);
+  }
+  flush_deltas(st, B, i, dl);
 }
 
 // orx_step_n's fast form (register NPCs, empty dungeons: NCAP 0 / 8 / 16,
@@ -4479,6 +5055,10 @@ __global__ void __launch_bounds__(256) stairs_kernel(orx_cfg_t hc, orx_state_t s
 #define ORX_PAIR_LIST_M(X, N)                                                                   \
   X(N, 4, kStreamAux, false, false, false) X(N, 4, kPartialAux, false, false, false)            \
   X(N, 5, kStreamAux, false, false, false) X(N, 5, kPartialAux, false, false, false)
+// PM 6 (a move log's replay, orx_step_n), empty dungeons, int32 / compact rows
+#define ORX_PAIR_LIST_L(X, N)                                                                   \
+  X(N, 6, kStreamAux, false, false, false) X(N, 6, kPartialAux, false, false, false)            \
+  X(N, 6, kStreamAux, false, true, false) X(N, 6, kPartialAux, false, true, false)
 #define ORX_PAIR_LIST(X)                                                                        \
   ORX_PAIR_LIST_A(X, 0) ORX_PAIR_LIST_B(X, 0) ORX_PAIR_LIST_A(X, 8) ORX_PAIR_LIST_B(X, 8)       \
   ORX_PAIR_LIST_A(X, 16) ORX_PAIR_LIST_B(X, 16) ORX_PAIR_LIST_M(X, 0) ORX_PAIR_LIST_M(X, 8)     \
@@ -4504,6 +5084,21 @@ __global__ void __launch_bounds__(256) stairs_kernel(orx_cfg_t hc, orx_state_t s
 #define ORX_ROLLOUT_LIST(X)                                                                     \
   ORX_ROLLOUT_LIST_N(X, 0) ORX_ROLLOUT_LIST_N(X, 8) ORX_ROLLOUT_LIST_N(X, 16)                   \
   ORX_ROLLOUT_LIST_DENSE(X)
+
+// moving NPCs (cfg.npc_policy != ORX_NPC_STAY): (NCAP, GRID) of
+// step_n_kernel<N, G, true> and env_step_kernel<N, G, true, true>, (NCAP, EV,
+// GRID) of step_kernel<N, E, G, true, true> and mt_step_kernel<N, E, G, true>,
+// (NCAP, GRID, MT) of mov_rollout_kernel
+#define ORX_MOV_NG_LIST(X)                                                                      \
+  X(8, false) X(16, false) X(kDense, false) X(8, true) X(16, true) X(kDense, true)
+#define ORX_MOV_STEP_LIST(X)                                                                    \
+  X(8, false, false) X(8, true, false) X(16, false, false) X(16, true, false)                   \
+  X(kDense, false, false) X(kDense, true, false) X(8, false, true) X(8, true, true)             \
+  X(16, false, true) X(16, true, true) X(kDense, false, true) X(kDense, true, true)
+#define ORX_MOV_ROLLOUT_LIST(X)                                                                 \
+  X(8, false, false) X(16, false, false) X(kDense, false, false) X(8, true, false)              \
+  X(16, true, false) X(kDense, true, false) X(8, false, true) X(16, false, true)                \
+  X(kDense, false, true) X(8, true, true) X(16, true, true) X(kDense, true, true)
 
 #ifdef ORX_NPARTS
 // ORX_INST: `extern` in the host part (an explicit instantiation
@@ -4555,6 +5150,22 @@ __global__ void __launch_bounds__(256) stairs_kernel(orx_cfg_t hc, orx_state_t s
   ORX_INST template __global__ void replay_kernel<N, R, E>(orx_cfg_t, orx_state_t,              \
                                                            const int8_t*, int32_t, int32_t*,    \
                                                            uint32_t, Key, uint32_t, uint32_t);
+#define ORX_I_MOV_STEP(N, E, G)                                                                 \
+  ORX_INST template __global__ void step_kernel<N, E, G, true, true>(                           \
+      orx_cfg_t, orx_state_t, const int8_t*, uint32_t, Key, uint32_t, int32_t*, int32_t*);      \
+  ORX_INST template __global__ void mt_step_kernel<N, E, G, true>(                              \
+      orx_cfg_t, orx_state_t, const int8_t*, uint32_t, Key, uint32_t, int32_t*, int32_t*);
+#define ORX_I_MOV_NG(N, G)                                                                      \
+  ORX_INST template __global__ void step_n_kernel<N, G, true>(orx_cfg_t, orx_state_t,           \
+                                                              const int8_t*, int32_t, int32_t*, \
+                                                              uint32_t, Key, uint32_t, int32_t); \
+  ORX_INST template __global__ void env_step_kernel<N, G, true, true>(                          \
+      orx_cfg_t, orx_state_t, const void*, int32_t, int32_t, int32_t, int8_t*, int32_t*, float*, \
+      uint8_t*, int32_t*, uint32_t*, uint32_t, Key, uint32_t, int32_t);
+#define ORX_I_MOV_ROLLOUT(N, G, M)                                                              \
+  ORX_INST template __global__ void mov_rollout_kernel<N, G, M>(                                \
+      orx_cfg_t, orx_state_t, int32_t, int32_t, int32_t, int32_t*, int8_t*, uint32_t, Key,      \
+      uint32_t, int32_t);
 #define ORX_I_STAIRS(G)                                                                         \
   ORX_INST template __global__ void stairs_kernel<G>(orx_cfg_t, orx_state_t, const uint32_t*,    \
                                                      const int32_t*, const int32_t*,            \
@@ -4562,8 +5173,9 @@ __global__ void __launch_bounds__(256) stairs_kernel(orx_cfg_t hc, orx_state_t s
                                                      int32_t*, uint32_t, Key);
 // the parts: 1-6 the paired rollouts (NCAP 0 / 8 / 16, halves A and B), 7-9
 // the one-lane rollouts per NCAP, 10 the dense rollouts and env_step, 11 the
-// step kernels, 12 the rest, 13 the mixed-bot paired rollouts; each costs a
-// few tens of seconds of hipcc
+// step kernels, 12 the rest, 13 the mixed-bot paired rollouts, 14 the
+// moving-NPC kernels, 15 the paired replays; each costs a few tens of
+// seconds of hipcc
 #define ORX_OWNS(k) (ORX_PART == 0 || ORX_PART == (k))
 #if ORX_OWNS(1)
 ORX_PAIR_LIST_A(ORX_I_PAIR, 0)
@@ -4605,6 +5217,16 @@ ORX_STEP_LIST(ORX_I_MT_STEP)
 ORX_PAIR_LIST_M(ORX_I_PAIR, 0)
 ORX_PAIR_LIST_M(ORX_I_PAIR, 8)
 ORX_PAIR_LIST_M(ORX_I_PAIR, 16)
+#endif
+#if ORX_OWNS(15)
+ORX_PAIR_LIST_L(ORX_I_PAIR, 0)
+ORX_PAIR_LIST_L(ORX_I_PAIR, 8)
+ORX_PAIR_LIST_L(ORX_I_PAIR, 16)
+#endif
+#if ORX_OWNS(14)
+ORX_MOV_STEP_LIST(ORX_I_MOV_STEP)
+ORX_MOV_NG_LIST(ORX_I_MOV_NG)
+ORX_MOV_ROLLOUT_LIST(ORX_I_MOV_ROLLOUT)
 #endif
 #if ORX_OWNS(12)
 ORX_NG_LIST(ORX_I_RESET)
@@ -4681,7 +5303,18 @@ int check_cfg(const orx_cfg_t* c) {
     return fail(ORX_EINVAL, "unknown rng mode");
   if (c->rng == ORX_RNG_MT19937 && (c->width > 256 || c->height > 256))
     return fail(ORX_EINVAL, "stock-seed mode stores staircases 8+8 bits: W, H <= 256");
+  if (c->npc_policy < ORX_NPC_STAY || c->npc_policy > ORX_NPC_CHASE)
+    return fail(ORX_EINVAL, "unknown npc_policy");
+  if (c->npc_policy != ORX_NPC_STAY &&
+      (c->flags & ~(ORX_EXT_SEPARATION_DAMAGE | ORX_EXT_RANDOM_DOUBLE_DEATH)))
+    return fail(ORX_EINVAL, "moving NPCs (npc_policy) need flags within "
+                            "ORX_EXT_SEPARATION_DAMAGE | ORX_EXT_RANDOM_DOUBLE_DEATH");
   return ORX_OK;
+}
+
+// The moving-NPC kernels serve this configuration (NPCs that move)
+inline bool moving_npcs(const orx_cfg_t* c) {
+  return c->npc_policy != ORX_NPC_STAY && c->n_npcs > 0;
 }
 
 int check_state(const orx_cfg_t* c, const orx_state_t* s, bool full) {
@@ -4939,7 +5572,7 @@ RolloutPlan plan_rollout(const orx_cfg_t* cfg, int pm, uint32_t B, uint32_t conc
   const uint64_t simds4 = 4ull * 32ull * (uint64_t)device_simds();
   const bool pm2_full = pm == 2 && p.lanes == 64u && concurrency >= 2 &&
                         (uint64_t)B * concurrency <= simds4 && !lanes_override();
-  p.paired = ncap_for(cfg->n_npcs) != kDense && bank_ok && pm >= 1 && pm <= 5 &&
+  p.paired = ncap_for(cfg->n_npcs) != kDense && bank_ok && pm >= 1 && pm <= 6 &&
              cfg->width <= 256 && cfg->height <= 256 && (p.lanes <= 32u || pm2_full) &&
              paired_enabled();
   if (p.paired) {
@@ -4990,7 +5623,8 @@ int orx_rollout_shape(const orx_cfg_t* cfg, int32_t policy_p1, int32_t policy_p2
   const uint32_t B = (uint32_t)n_games;
   out->threads_per_block = kBlock;
   out->lds_bytes = 0;
-  if (cfg->rng == ORX_RNG_MT19937) {  // mt_rollout_kernel: one game per lane, full waves
+  if (cfg->rng == ORX_RNG_MT19937 || moving_npcs(cfg)) {  // mt_ / mov_rollout_kernel: one
+                                                          // game per lane, full waves
     out->games_per_wave = 64;
     out->lanes_per_game = 1;
     out->nontemporal = 1;
@@ -5025,6 +5659,11 @@ int orx_rollout_shape(const orx_cfg_t* cfg, int32_t policy_p1, int32_t policy_p2
   }
   out->lds_bytes = (int32_t)lds;
   return ORX_OK;
+}
+
+int orx_max_events(const orx_cfg_t* cfg) {
+  if (const int r = check_cfg(cfg)) return r;
+  return max_events_for(cfg->npc_policy, cfg->n_npcs);
 }
 
 int orx_dstore_depths(const orx_cfg_t* cfg) {
@@ -5097,6 +5736,21 @@ static int launch_step(const orx_cfg_t* cfg, const orx_state_t* st, const int8_t
   const int nc = ncap_for(cfg->n_npcs);
   const bool grid = cfg->n_layouts > 0;
   const bool mt = cfg->rng == ORX_RNG_MT19937;
+  if (moving_npcs(cfg)) {  // the ordered tick with the enemy AI
+#define ORX_STEP(NC, E, G)                                                                      \
+  if (nc == NC && ev == E && grid == G) {                                                      \
+    if (mt)                                                                                     \
+      hipLaunchKernelGGL((mt_step_kernel<NC, E, G, true>), grid_for(B), dim3(kBlock), 0, s,     \
+                         *cfg, *st, actions, B, k, off, events, n_events);                      \
+    else                                                                                        \
+      hipLaunchKernelGGL((step_kernel<NC, E, G, true, true>), grid_for(B), dim3(kBlock), 0, s,  \
+                         *cfg, *st, actions, B, k, off, events, n_events);                      \
+    return launch_status(name);                                                                \
+  }
+    ORX_MOV_STEP_LIST(ORX_STEP)
+#undef ORX_STEP
+    return fail(ORX_EIO, "orx_step: no moving-NPC kernel instance for this configuration");
+  }
   if (!ev && !grid && !mt && cfg->flags == 0 && nc != kDense) {  // the reference's rules
     if (nc == 0)
       hipLaunchKernelGGL((step_kernel<0, false, false, false>), grid_for(B), dim3(kBlock), 0, s,
@@ -5162,8 +5816,57 @@ int orx_step_n(const orx_cfg_t* cfg, const orx_state_t* st, const int8_t* action
   const char* gen_env = getenv("ORX_STEP_N_GENERIC");
   // (the buffer-store rows address one tick's rows with 32-bit offsets)
   const bool rows_fit = (uint64_t)B * ORX_OBS_FIELDS * 4u < (1ull << 31);
+  if (moving_npcs(cfg)) {
+#define ORX_STEP_N(N, G)                                                                        \
+    if (nc == N && grid == G) {                                                                 \
+      hipLaunchKernelGGL((step_n_kernel<N, G, true>), grid_for(B), dim3(kBlock), 0, s, *cfg,    \
+                         *st, actions, n_ticks, obs, B, k, off, obs_format);                    \
+      return launch_status("orx_step_n");                                                      \
+    }
+    ORX_MOV_NG_LIST(ORX_STEP_N)
+#undef ORX_STEP_N
+    return fail(ORX_EIO, "orx_step_n: no moving-NPC kernel instance for this configuration");
+  }
   if (!grid && nc != kDense && rows_fit && !(gen_env && gen_env[0] == '1')) {
     const int rows = obs ? (obs_format == ORX_OBS_COMPACT ? 2 : 1) : 0;
+    // the paired form (pair_rollout_kernel PM 6: two lanes per game, the
+    // rollout's paired tick on the logged moves) where the rollout's plan
+    // pairs: rows given, reference rules (env ORX_REPLAY_PAIRED=1 forces it
+    // at any batch, =0 keeps the one-lane form, for measurements)
+    const char* pe = getenv("ORX_REPLAY_PAIRED");
+    RolloutPlan pl = plan_rollout(cfg, 6, B, 1);
+    bool paired = rows != 0 && cfg->flags == 0 && pl.paired;
+    if (pe && pe[0] == '1' && rows != 0 && cfg->flags == 0 && paired_enabled() && !pl.paired) {
+      const uint64_t simds = (uint64_t)device_simds();
+      uint32_t L = 32;
+      while (L > 8 && (uint64_t)B < 2 * simds * L) L >>= 1;
+      if (const int o = lanes_override()) L = o < 32 ? (uint32_t)o : 32u;
+      pl.lanes = L;
+      pl.nt = L * 4u >= 128u;
+      paired = true;
+    }
+    if (pe && pe[0] == '0') paired = false;
+    if (paired) {
+      const uint32_t lanes = pl.lanes, threads = (uint32_t)kRolloutBlock;
+      const uint32_t per_block = threads / 64u * lanes;
+      const dim3 blocks((B + per_block - 1) / per_block);
+      int8_t* log = const_cast<int8_t*>(actions);  // (PM 6 reads it; the form never writes it)
+#define ORX_PAIR_LOG(N, A, C)                                                                   \
+      if (nc == N && (A == kStreamAux) == pl.nt && C == (rows == 2)) {                          \
+        hipLaunchKernelGGL((pair_rollout_kernel<N, 6, A, false, C, false>), blocks,              \
+                           dim3(threads), 0, s, *cfg, *st, n_ticks, obs, log, B, k, off, lanes,  \
+                           0u);                                                                 \
+        return launch_status("orx_step_n");                                                    \
+      }
+      ORX_PAIR_LOG(0, kStreamAux, false) ORX_PAIR_LOG(0, kPartialAux, false)
+      ORX_PAIR_LOG(0, kStreamAux, true) ORX_PAIR_LOG(0, kPartialAux, true)
+      ORX_PAIR_LOG(8, kStreamAux, false) ORX_PAIR_LOG(8, kPartialAux, false)
+      ORX_PAIR_LOG(8, kStreamAux, true) ORX_PAIR_LOG(8, kPartialAux, true)
+      ORX_PAIR_LOG(16, kStreamAux, false) ORX_PAIR_LOG(16, kPartialAux, false)
+      ORX_PAIR_LOG(16, kStreamAux, true) ORX_PAIR_LOG(16, kPartialAux, true)
+#undef ORX_PAIR_LOG
+      return fail(ORX_EIO, "orx_step_n: no paired replay instance for this plan");
+    }
     const uint32_t lanes = rollout_lanes(B);  // games per wave, as the rollout's plan
     const uint64_t threads = (((uint64_t)B + lanes - 1) / lanes) * 64u;
     const dim3 g((unsigned)((threads + kRolloutBlock - 1) / kRolloutBlock));
@@ -5246,6 +5949,18 @@ int orx_env_step_ex(const orx_cfg_t* cfg, const orx_state_t* st, const void* act
   // the rows through LDS (env ORX_ENV_DIRECT_ROWS=1: direct stores, for measurements)
   const char* dr = getenv("ORX_ENV_DIRECT_ROWS");
   const int32_t lds_rows = (dr && dr[0] == '1') ? 0 : 1;
+  if (moving_npcs(cfg)) {
+#define ORX_ENV(N, G)                                                                           \
+    if (nc == N && grid == G) {                                                                 \
+      hipLaunchKernelGGL((env_step_kernel<N, G, true, true>), grid_for(B), dim3(kBlock), 0, s,  \
+                         *cfg, *st, actions, action_bytes, action_cols, policy_p2, act, obs,    \
+                         reward, done, status, bad_actions, B, k, off, lds_rows);               \
+      return launch_status("orx_env_step");                                                    \
+    }
+    ORX_MOV_NG_LIST(ORX_ENV)
+#undef ORX_ENV
+    return fail(ORX_EIO, "orx_env_step: no moving-NPC kernel instance for this configuration");
+  }
 #define ORX_ENV(N, G, X)                                                                        \
   if (nc == N && grid == G && (cfg->flags == 0 || X)) {                                        \
     hipLaunchKernelGGL((env_step_kernel<N, G, X>), grid_for(B), dim3(kBlock), 0, s, *cfg, *st,   \
@@ -5297,6 +6012,18 @@ int orx_rollout_ex(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p
   // the buffer-addressed trajectory forms need one tick's obs rows below 2 GiB
   const bool grid = cfg->n_layouts > 0;
   const int nc = ncap_for(cfg->n_npcs);
+  if (moving_npcs(cfg)) {  // the ordered tick with the enemy AI, one lane per game
+    const bool mt = cfg->rng == ORX_RNG_MT19937;
+#define ORX_ROLLOUT(N, G, M)                                                                    \
+    if (nc == N && grid == G && mt == M) {                                                      \
+      hipLaunchKernelGGL((mov_rollout_kernel<N, G, M>), grid_for(B), dim3(kBlock), 0, s, *cfg,  \
+                         *st, policy_p1, policy_p2, n_ticks, obs, act, B, k, off, obs_format);  \
+      return launch_status("orx_rollout");                                                     \
+    }
+    ORX_MOV_ROLLOUT_LIST(ORX_ROLLOUT)
+#undef ORX_ROLLOUT
+    return fail(ORX_EIO, "orx_rollout: no moving-NPC kernel instance for this configuration");
+  }
   if (cfg->rng == ORX_RNG_MT19937) {
 #define ORX_ROLLOUT(N, G)                                                                       \
   if (nc == N && grid == G)                                                                     \

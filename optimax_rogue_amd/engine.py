@@ -17,7 +17,7 @@ import torch
 
 from . import _lib
 from .config import EnvConfig
-from .enums import (EXT_CHARACTER, EXT_ITEMS, EXT_SEPARATION_DAMAGE, MAX_EVENTS,
+from .enums import (EXT_CHARACTER, EXT_ITEMS, EXT_SEPARATION_DAMAGE,
                     MAX_REG_NPCS, N_COUNTERS, OBS_COMPACT, OBS_COMPACT_FIELDS, OBS_FIELDS,
                     OBS_INT32, RNG_MT19937, RPG_FIELDS, Policy)
 
@@ -273,7 +273,7 @@ class BatchedEngine:
         """Updater.update for every game: actions[b] = (player 1, player 2) Move
         values.  Returns the status tensor (UpdateResult codes, asynchronous);
         with ``events=True`` returns ``(status, events, n_events)``: the tick's
-        update-event records int32 [n_games, MAX_EVENTS, 4] and their counts
+        update-event records int32 [n_games, max_events(), 4] and their counts
         (include/orx.h ORX_EV_*), in the reference's GameStateUpdate order;
         both buffers belong to the engine and are overwritten by the next
         ``step(events=True)``."""
@@ -283,11 +283,20 @@ class BatchedEngine:
             self._call("orx_step", _ptr(a), self.B, self.seed, self.game_offset, self._stream())
             return self.status
         if getattr(self, "_ev", None) is None:
-            self._ev = torch.zeros((self.B, MAX_EVENTS, 4), dtype=torch.int32, device=self.device)
+            self._ev = torch.zeros((self.B, self.max_events(), 4), dtype=torch.int32,
+                                   device=self.device)
             self._nev = torch.zeros(self.B, dtype=torch.int32, device=self.device)
         self._call("orx_step_events", _ptr(a), _ptr(self._ev), _ptr(self._nev), self.B, self.seed,
                    self.game_offset, self._stream())
         return self.status, self._ev, self._nev
+
+    def max_events(self) -> int:
+        """Event records per game-tick of ``step(events=True)`` for this
+        configuration (orx_max_events: MAX_EVENTS, or 6 + 2 K with moving
+        NPCs)."""
+        n = int(self.lib.orx_max_events(self._pcfg))
+        _lib.check("orx_max_events", min(n, 0))
+        return n
 
     def step_n(self, actions: torch.Tensor, obs: Optional[torch.Tensor] = None,
                obs_format: int = OBS_INT32) -> torch.Tensor:

@@ -56,6 +56,16 @@ class Policy(enum.IntEnum):
     Stay = 3
 
 
+class NpcPolicy(enum.IntEnum):
+    """The enemy AI, EnvConfig.npc_policy (include/orx.h ORX_NPC_*): the
+    reference's hook Updater.decide_npc_move (updater.py:165-178) returns Stay;
+    RANDOM and CHASE are the AIs tests/golden/make_golden.NpcAiUpdater plugs
+    into it (the reference then resolves the moves)."""
+    Stay = 0
+    Random = 1
+    Chase = 2
+
+
 # build-only per-game status codes (include/orx.h)
 STATUS_BAD_ACTION = 16
 STATUS_RNG_EXHAUSTED = 17

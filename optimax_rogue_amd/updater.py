@@ -19,6 +19,11 @@ Construction mirrors the reference's plugins:
   max_ticks      None / 0 = no limit (updater.py:158).
   game_start     "together" (TogetherGameStartGenerator) or
                  ("separated", p1_depth, p2_depth) (SeparatedGameStartGenerator).
+  npc_policy     the enemy AI: what a subclass overriding
+                 Updater.decide_npc_move (updater.py:165-178) would return --
+                 NpcPolicy.Stay (the reference's own hook), Random or Chase
+                 (include/orx.h ORX_NPC_*); the engine then resolves the NPCs'
+                 moves as the reference's update does (:116-145).
 """
 from __future__ import annotations
 
@@ -28,7 +33,7 @@ import torch
 
 from .config import EnvConfig
 from .engine import BatchedEngine
-from .enums import DungeonDespawningStrategy, Move, Policy, StartMode
+from .enums import DungeonDespawningStrategy, Move, NpcPolicy, Policy, StartMode
 
 
 def _dims(dgen):
@@ -49,12 +54,14 @@ class BatchedUpdater:
     def __init__(self, dgen, despawn_strat: DungeonDespawningStrategy,
                  max_ticks: Optional[int] = None, *, n_games: int, seed: int = 0,
                  game_offset: int = 0, game_start="together", n_npcs: int = 0,
-                 device: Optional[torch.device] = None, autoreset: bool = False):
+                 device: Optional[torch.device] = None, autoreset: bool = False,
+                 npc_policy: NpcPolicy = NpcPolicy.Stay):
         if int(despawn_strat) not in (1, 2):
             raise ValueError(f"Unknown despawn strat {despawn_strat}")
         w, h, layouts = _dims(dgen)
         cfg = EnvConfig(width=w, height=h, despawn=int(despawn_strat), max_ticks=max_ticks or 0,
-                        n_npcs=n_npcs, autoreset=int(autoreset), layouts=layouts)
+                        n_npcs=n_npcs, autoreset=int(autoreset), layouts=layouts,
+                        npc_policy=int(NpcPolicy(int(npc_policy))))
         if game_start != "together":
             kind, d1, d2 = game_start
             if kind != "separated":
@@ -104,10 +111,11 @@ class GameUpdater:
 
     def __init__(self, dgen, despawn_strat: DungeonDespawningStrategy,
                  max_ticks: Optional[int] = None, *, seed: int = 0, game_id: int = 0,
-                 game_start="together", n_npcs: int = 0, device: Optional[torch.device] = None):
+                 game_start="together", n_npcs: int = 0, device: Optional[torch.device] = None,
+                 npc_policy: NpcPolicy = NpcPolicy.Stay):
         self._b = BatchedUpdater(dgen, despawn_strat, max_ticks, n_games=1, seed=seed,
                                  game_offset=game_id, game_start=game_start, n_npcs=n_npcs,
-                                 device=device, autoreset=False)
+                                 device=device, autoreset=False, npc_policy=npc_policy)
         self.engine = self._b.engine
         self.current_update_order = 0
         self.max_ticks = max_ticks
@@ -141,7 +149,8 @@ class GameUpdater:
             raise KeyError(depth)
 
         ups = from_events(rows, self.current_update_order,
-                          cfg.player_damage - cfg.player_armor, pre, dungeon_for)
+                          cfg.player_damage - cfg.player_armor, pre, dungeon_for,
+                          npc_og_damage=cfg.npc_damage - cfg.npc_armor)
         self.current_update_order += len(ups)
         for u in ups:
             u.apply(game_state)

@@ -16,7 +16,7 @@ object with the GameState surface (compat.GameStateView included), and
 """
 from __future__ import annotations
 
-from typing import List
+from typing import List, Optional
 
 from .enums import EV_COMBAT, EV_DEATH, EV_DUNGEON, EV_HEALTH, EV_POSITION, CombatFlag
 
@@ -123,19 +123,22 @@ class EntityHealthUpdate(GameStateUpdate):
 
 
 def from_events(rows, order_start: int, og_damage: int, pre_depth: dict,
-                dungeon_for=None) -> List[GameStateUpdate]:
+                dungeon_for=None, npc_og_damage: Optional[int] = None) -> List[GameStateUpdate]:
     """Update objects for one game's event records [(type, iden, a, b), ...].
 
     ``order`` continues the Updater's running counter (updater.py:71-74);
     ``og_damage`` = attacker damage - armor (updater.py:313); ``pre_depth``
     maps entity iden -> depth before the tick (EntityPositionUpdate.old_depth;
     an entity moves at most once per tick); ``dungeon_for(depth)`` supplies
-    DungeonCreatedUpdate.dungeon (the engine regenerates it from its key)."""
+    DungeonCreatedUpdate.dungeon (the engine regenerates it from its key);
+    ``npc_og_damage`` = an NPC attacker's damage - armor (moving NPCs, whose
+    attacks the enemy AI makes; default ``og_damage``)."""
     out: List[GameStateUpdate] = []
     order = order_start
     for typ, iden, a, b in rows:
         if typ == EV_COMBAT:
-            out.append(EntityCombatUpdate(order, iden, a, og_damage, {CombatFlag(b)}))
+            og = og_damage if iden <= 2 or npc_og_damage is None else npc_og_damage
+            out.append(EntityCombatUpdate(order, iden, a, og, {CombatFlag(b)}))
         elif typ == EV_DEATH:
             out.append(EntityDeathUpdate(order, iden))
         elif typ == EV_POSITION:

@@ -21,7 +21,7 @@ CFG_FIELDS = ["width", "height", "despawn", "max_ticks", "start_mode", "p1_depth
               "n_npcs", "npc_health", "npc_damage", "npc_armor", "player_health",
               "player_damage", "player_armor", "autoreset", "flags", "n_layouts", "sep_period",
               "rng", "mana_max", "mana_regen", "mana_per_point", "xp_per_kill", "xp_per_level",
-              "item_drop_pct", "item_bonus", "item_slots", "combat_cooldown"]
+              "item_drop_pct", "item_bonus", "item_slots", "combat_cooldown", "npc_policy"]
 
 
 class _Cfg(ctypes.Structure):
@@ -33,7 +33,7 @@ DEFAULT_CFG = dict(width=32, height=32, despawn=1, max_ticks=1000, start_mode=1,
                    player_health=10, player_damage=2, player_armor=1, autoreset=1, flags=0,
                    n_layouts=0, sep_period=0, rng=0, mana_max=9, mana_regen=1, mana_per_point=1,
                    xp_per_kill=1, xp_per_level=3, item_drop_pct=50, item_bonus=1, item_slots=3,
-                   combat_cooldown=3)
+                   combat_cooldown=3, npc_policy=0)
 
 _lib = None
 

@@ -50,6 +50,7 @@ import numpy as np
 
 M = 0xFFFFFFFF
 PUR_INIT, PUR_DUNGEON, PUR_SHUFFLE, PUR_SPAWN, PUR_POLICY, PUR_TICK = 1, 2, 3, 4, 5, 7
+PUR_NPC = 9   # the enemy AI's draws (npc_policy RANDOM, include/orx.h)
 GROUND, WALL, STAIRS = 1, 2, 3                       # Tile (world.py:10-17)
 UP, RIGHT, DOWN, LEFT, STAY = 1, 2, 3, 4, 5          # Move (moves.py:6-12)
 MOVES = (UP, RIGHT, DOWN, LEFT, STAY)                # list(Move) (randombot.py:17-18)
@@ -121,6 +122,24 @@ class TickBits:
         r = s[0] & ((1 << k) - 1)
         s[0] >>= k
         s[1] -= k
+        return r
+
+
+class NpcBits:
+    """The enemy AI's bits (npc_policy RANDOM): bits 0-29 of each successive
+    word of the NPC stream as reservoir segments, least-significant first."""
+    __slots__ = ("words", "seg", "n")
+
+    def __init__(self, seed, game, episode, tick):
+        self.words = Words(seed, game, episode, tick, PUR_NPC)
+        self.seg, self.n = 0, 0
+
+    def getrandbits(self, k):
+        if self.n < k:
+            self.seg, self.n = self.words.next() & 0x3FFFFFFF, 30
+        r = self.seg & ((1 << k) - 1)
+        self.seg >>= k
+        self.n -= k
         return r
 
 
@@ -398,7 +417,11 @@ class Game:
             m2 = STAY
         upd = [[p1, m1], [p2, m2]]
         shuffle(self.bits, upd)
-        npcs = [[e, STAY] for e in gs.entities if e.iden not in (1, 2)]   # decide_npc_move
+        ai = None
+        if int(self.cfg.get("npc_policy", 0)) == 1:
+            ai = self.py if self.stock else NpcBits(self.seed, self.gid, self.episode, gs.tick)
+        npcs = [[e, self.decide_npc_move(gs, e, ai)] for e in gs.entities
+                if e.iden not in (1, 2)]
         shuffle(self.bits, npcs)
         upd.extend(npcs)
         order = {u[0].iden: i for i, u in enumerate(upd)}
@@ -420,6 +443,32 @@ class Game:
         if self.max_ticks and gs.tick >= self.max_ticks:
             return TIE
         return IN_PROGRESS
+
+    def decide_npc_move(self, gs, e, ai):
+        """Updater.decide_npc_move (updater.py:165-178): Stay, or the enemy AI
+        of make_golden.NpcAiUpdater (include/orx.h ORX_NPC_*)."""
+        pol = int(self.cfg.get("npc_policy", 0))
+        if pol == 0 or e.depth not in gs.world:
+            return STAY
+        d = gs.world[e.depth]
+        here = [p for p in (gs.iden_lookup[1], gs.iden_lookup[2]) if p.depth == e.depth]
+        W, H = d.tiles.shape
+        for p in here:
+            for m in (UP, RIGHT, DOWN, LEFT):
+                x, y = calculate_pos(p.x, p.y, m)
+                if 0 <= x < W and 0 <= y < H and d.tiles[x, y] == STAIRS:
+                    return STAY
+        if pol == 1:
+            m = MOVES[randbelow(ai, len(MOVES))]
+        else:
+            if not here:
+                return STAY
+            t = min(here, key=lambda p: abs(p.x - e.x) + abs(p.y - e.y))
+            dx, dy = t.x - e.x, t.y - e.y
+            m = (RIGHT if dx > 0 else LEFT) if abs(dx) > abs(dy) else (DOWN if dy > 0 else UP)
+        if d.is_blocked(*calculate_pos(e.x, e.y, m)):
+            return STAY
+        return m
 
     def handle_move(self, gs, i, u, upd, order, ev):
         e, move = u

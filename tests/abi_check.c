@@ -52,6 +52,15 @@ int main(void) {
                      0, 1, 0, 1, NULL) != ORX_OK) { printf("empty compact rollout failed\n"); return 11; }
   if (orx_rollout_ex(&c, NULL, ORX_POLICY_RANDOM, ORX_POLICY_RANDOM, 5, NULL, NULL, 7, 16, 1, 0, 1,
                      NULL) != ORX_EINVAL) { printf("unknown row format accepted\n"); return 12; }
+  /* ABI 7: the enemy AI and its event-record bound */
+  c.n_npcs = 8;
+  c.npc_policy = ORX_NPC_RANDOM;
+  if (orx_validate_cfg(&c) != ORX_OK || orx_max_events(&c) != 6 + 2 * 8) {
+    printf("moving NPCs refused or their event bound wrong\n"); return 18;
+  }
+  c.npc_policy = ORX_NPC_STAY;
+  if (orx_max_events(&c) != ORX_MAX_EVENTS) { printf("event bound wrong\n"); return 19; }
+  c.n_npcs = 8;
   printf("sizeof(orx_cfg_t)=%zu sizeof(orx_state_t)=%zu off_flags=%zu off_npc_alive=%zu\n",
          sizeof(orx_cfg_t), sizeof(orx_state_t), offsetof(orx_cfg_t, flags),
          offsetof(orx_state_t, npc_alive));

@@ -45,6 +45,22 @@ output:
   (worldgen.py:47-58) that calls the reference's Together/Separated
   ``setup_game`` and then places K NPCs with the reference's
   ``Dungeon.get_random_unblocked`` and ``GameState.add_entity``.
+* Moving NPCs (``npc_policy`` 1 / 2): ``NpcAiUpdater``, a subclass of the
+  reference's ``Updater`` that overrides only its enemy-AI hook
+  ``decide_npc_move`` (updater.py:165-178) -- the reference's ``update`` then
+  draws the NPC shuffle, resolves every NPC move through ``handle_move`` /
+  ``handle_combat`` / ``handle_descend`` (updater.py:116-145, 180-338) and
+  sweeps the dead.  The AI (include/orx.h ORX_NPC_*): an NPC on a depth
+  with no dungeon, or on a depth where a player stands next to a staircase,
+  stays; otherwise RANDOM = ``random.choice(list(Move))`` (the updater's
+  module ``random``, its words from the NPC stream ``NpcBits`` in keyed
+  mode, the game's own CPython state in stock mode) and CHASE = a greedy step
+  toward the nearer player on its depth (StaircaseBot's rule, player 1 on a
+  tie); a move into a blocked cell becomes Stay (``Dungeon.is_blocked``).
+  The staircase rule keeps the reference from raising: ``update`` asks
+  every NPC's move before any move is made, and an NPC stepping onto a free
+  cell of a depth that a player's descend despawned earlier in the same tick
+  would hit ``World.get_at_depth``'s KeyError (updater.py:203, :295-296).
 
 The third-party module ``inflection`` (imported by serializer.py:27, unpinned:
 setup.py:11 has install_requires=[]) is not installed.  It is only used for
@@ -95,6 +111,7 @@ def philox4x32_10(ctr, key):
 
 PUR_INIT, PUR_DUNGEON, PUR_SHUFFLE, PUR_SPAWN, PUR_POLICY = 1, 2, 3, 4, 5
 PUR_TICK = 7
+PUR_NPC = 9   # the enemy AI's draws (c2 = tick): decide_npc_move's random.choice
 
 
 class Stream:
@@ -143,6 +160,28 @@ class TickBits:
         r = seg[0] & ((1 << k) - 1)
         seg[0] >>= k
         seg[1] -= k
+        return r
+
+
+class NpcBits:
+    """The bit source of one tick's enemy-AI draws (npc_policy RANDOM): the
+    stream (game, episode, tick, NPC << 28) taken as consecutive 30-bit
+    reservoir segments -- bits 0-29 of word 0, of word 1, ... (four words a
+    block) -- consumed least-significant bits first; a getrandbits(k) skips
+    a segment with fewer than k bits left.  random.choice(list(Move)) takes
+    3-bit fields: ten per word, a field >= 5 rejected (_randbelow)."""
+
+    def __init__(self, seed, game, episode, tick):
+        self.words = Stream(seed, game, episode, tick, PUR_NPC)
+        self.seg = [0, 0]
+
+    def getrandbits(self, k):
+        assert k <= 30
+        if self.seg[1] < k:
+            self.seg = [self.words.next() & 0x3FFFFFFF, 30]
+        r = self.seg[0] & ((1 << k) - 1)
+        self.seg[0] >>= k
+        self.seg[1] -= k
         return r
 
 
@@ -375,8 +414,54 @@ class Harness:
             inner = R.worldgen.TogetherGameStartGenerator(self.dgen)
         self.start = NpcGameStart(inner, cfg["n_npcs"], cfg["npc_health"], cfg["npc_damage"],
                                   cfg["npc_armor"])
+        Move = R.moves.Move
+
+        def next_to_stairs(dung, p):
+            for m in (Move.Up, Move.Right, Move.Down, Move.Left):
+                x, y = R_.updater.calculate_pos(p.x, p.y, m)
+                if 0 <= x < dung.width and 0 <= y < dung.height \
+                        and dung.tiles[x, y] == R_.world.Tile.StaircaseDown:
+                    return True
+            return False
+
+        class NpcAiUpdater(R_.updater.Updater):
+            """The reference's Updater with its enemy-AI hook overridden
+            (updater.py:165-178); nothing else of it is touched."""
+
+            def decide_npc_move(self, game_state, ent, result):
+                if ent.depth not in game_state.world.dungeons:
+                    return Move.Stay
+                dung = game_state.world.get_at_depth(ent.depth)
+                players = [p for p in (game_state.player_1, game_state.player_2)
+                           if p.depth == ent.depth]
+                if any(next_to_stairs(dung, p) for p in players):
+                    return Move.Stay
+                if harness.npc_policy == 1:      # RANDOM
+                    saved = R_.pyrand.stream
+                    if not harness.stock:
+                        R_.pyrand.stream = harness.npc_bits
+                    try:
+                        move = R_.updater.random.choice(list(Move))
+                    finally:
+                        R_.pyrand.stream = saved
+                else:                           # CHASE
+                    if not players:
+                        return Move.Stay
+                    tgt = min(players, key=lambda p: abs(p.x - ent.x) + abs(p.y - ent.y))
+                    dx, dy = tgt.x - ent.x, tgt.y - ent.y
+                    if abs(dx) > abs(dy):
+                        move = Move.Right if dx > 0 else Move.Left
+                    else:
+                        move = Move.Down if dy > 0 else Move.Up
+                if dung.is_blocked(*R_.updater.calculate_pos(ent.x, ent.y, move)):
+                    return Move.Stay
+                return move
+
+        self.npc_policy = int(cfg.get("npc_policy", 0))
+        self.npc_bits = None
         strat = R.updater.DungeonDespawningStrategy(cfg["despawn"])
-        self.updater = R.updater.Updater(self.dgen, strat, cfg["max_ticks"] or None)
+        upd_cls = NpcAiUpdater if self.npc_policy else R.updater.Updater
+        self.updater = upd_cls(self.dgen, strat, cfg["max_ticks"] or None)
         self.bots = [self._bot(cfg["policy"][0], 1), self._bot(cfg["policy"][1], 2)]
         self.ret_sum = 0
         self.ep_count = 0
@@ -435,6 +520,7 @@ class Harness:
         else:
             R.pyrand.stream = TickBits(self.seed, self.gid, self.episode, self.gs.tick, PUR_SHUFFLE)
             R.nprand.stream = Stream(self.seed, self.gid, self.episode, self.gs.tick, PUR_SPAWN)
+            self.npc_bits = NpcBits(self.seed, self.gid, self.episode, self.gs.tick)
             with contextlib.redirect_stdout(io.StringIO()):
                 res, upds = self.updater.update(self.gs, R.moves.Move(acts[0]),
                                                 R.moves.Move(acts[1]))
@@ -538,7 +624,7 @@ def make_layouts(W, H, L, seed, n_stairs=(1,), open_border=False, wall_p=0.18):
 DEFAULT_CFG = dict(width=32, height=32, despawn=1, max_ticks=1000, start_mode=1, p1_depth=0,
                    p2_depth=0, n_npcs=0, npc_health=3, npc_damage=1, npc_armor=0,
                    player_health=10, player_damage=2, player_armor=1, autoreset=1, flags=0,
-                   policy=(1, 1))
+                   policy=(1, 1), npc_policy=0)
 
 CASES = {
     # C1 of BASELINE.json: 32x32, 2x RandomBot, max_ticks 1000 (long enough to autoreset)
@@ -632,6 +718,38 @@ CASES = {
                                            layouts=make_layouts(7, 7, 1, 103, n_stairs=(2,))),
                                   seed=14, games=12, ticks=260),
 }
+
+
+# moving NPCs (npc_policy: 1 RANDOM, 2 CHASE; NpcAiUpdater): the reference's
+# own NPC shuffle, NPC-vs-player and NPC-vs-NPC combat (Block / Ambush / Flee),
+# a player's hit on an NPC that moves (Flee), NPC deaths on a staircase
+# (updater.py:263-270), all on register (<= 16) and dense NPC forms
+CASES.update({
+    "mnpc_random_12x12": dict(cfg=dict(width=12, height=12, n_npcs=24, npc_health=2,
+                                       max_ticks=120, npc_policy=1), seed=71, games=12,
+                              ticks=300),
+    "mnpc_c3_64": dict(cfg=dict(width=64, height=64, n_npcs=8, npc_policy=1), seed=72, games=8,
+                       ticks=400),
+    "mnpc_stairs_unused": dict(cfg=dict(width=10, height=9, n_npcs=12, max_ticks=100, despawn=2,
+                                        policy=(2, 2), npc_policy=1), seed=73, games=12,
+                               ticks=300),
+    "mnpc_stairs_dense": dict(cfg=dict(width=11, height=10, n_npcs=28, npc_health=2,
+                                       max_ticks=100, policy=(2, 1), npc_policy=1), seed=74,
+                              games=12, ticks=300),
+    "mnpc_chase_8x8": dict(cfg=dict(width=8, height=8, n_npcs=6, npc_damage=2, max_ticks=60,
+                                    npc_policy=2), seed=75, games=16, ticks=260),
+    "mnpc_chase_dense": dict(cfg=dict(width=16, height=14, n_npcs=40, npc_health=2,
+                                      max_ticks=150, policy=(2, 1), npc_policy=2), seed=76,
+                             games=10, ticks=320),
+    "mnpc_separated": dict(cfg=dict(width=7, height=7, max_ticks=150, start_mode=2, p1_depth=3,
+                                    p2_depth=0, n_npcs=6, policy=(2, 2), npc_policy=1), seed=77,
+                           games=12, ticks=300),
+    "mnpc_bank": dict(cfg=dict(width=9, height=8, max_ticks=90, n_npcs=6, npc_policy=1,
+                               layouts=make_layouts(9, 8, 4, 105, open_border=True)),
+                      seed=78, games=12, ticks=260),
+    "mnpc_stock": dict(cfg=dict(rng=1, width=8, height=8, n_npcs=6, max_ticks=80, policy=(1, 2),
+                                npc_policy=1), seed=7000, games=12, ticks=240),
+})
 
 
 def sweep_case(case, base=1000):
@@ -744,6 +862,21 @@ def run_case(R, name, spec):
           f"dungeons={int(out['counters'][-1][2].sum())}, npc deaths={int(out['counters'][-1][3].sum())}, "
           f"max depth={int(out['p_depth'].max())}, statuses={sorted(set(st.ravel().tolist()))}, "
           f"bytes={os.path.getsize(path)}")
+    if cfg.get("npc_policy"):   # what the moving NPCs did (event records)
+        ev = out["events"]
+        tally = {}
+        for t_, i_, a_, b_ in ev.tolist():
+            who = "npc" if i_ >= 3 else "player"
+            if t_ == 1:
+                k = f"{who}->{'npc' if a_ >= 3 else 'player'}:{['', 'Block', 'Ambush', 'Flee', 'Parry'][b_]}"
+            elif t_ == 3:
+                k = f"{who} move"
+            elif t_ == 2:
+                k = "npc death"
+            else:
+                k = f"type{t_}"
+            tally[k] = tally.get(k, 0) + 1
+        print("   ", dict(sorted(tally.items())))
 
 
 # --------------------------------------------------------------------------

@@ -38,7 +38,7 @@ def test_library_exports_every_declared_symbol(lib):
                            "orx_dungeon_stairs", "orx_dungeon_spawn", "orx_seed_mt",
                            "orx_build_id", "orx_rollout_lanes", "orx_dstore_depths",
                            "orx_rollout_shape", "orx_rollout_concurrent", "orx_env_step",
-                           "orx_rollout_ex", "orx_env_step_ex", "orx_step_n"])
+                           "orx_rollout_ex", "orx_env_step_ex", "orx_step_n", "orx_max_events"])
     from optimax_rogue_amd import _lib
     assert sorted(_lib.EXPORTS) == decl
     for name in decl:
@@ -118,6 +118,8 @@ def test_enum_values_match_header():
         val("ORX_EV_COMBAT"), val("ORX_EV_DEATH"), val("ORX_EV_POSITION"), val("ORX_EV_DUNGEON"))
     assert enums.MAX_EVENTS == val("ORX_MAX_EVENTS")
     assert enums.SEP_PERIOD_MAX == val("ORX_SEP_PERIOD_MAX")
+    assert [p.value for p in enums.NpcPolicy] == [val("ORX_NPC_STAY"), val("ORX_NPC_RANDOM"),
+                                                  val("ORX_NPC_CHASE")]
 
 
 def test_validate_cfg(lib):
@@ -151,11 +153,33 @@ def test_validate_cfg(lib):
     # stock-seed word source (MT19937): staircases pack 8+8 bits
     ok.append(EnvConfig(rng=1, n_npcs=3))
     bad += [EnvConfig(rng=2), EnvConfig(rng=1, width=300, height=8)]
+    # moving NPCs (the enemy AI): known policies, with the separation and
+    # double-death extensions only
+    ok += [EnvConfig(n_npcs=8, npc_policy=1), EnvConfig(n_npcs=40, npc_policy=2),
+           EnvConfig(npc_policy=1), EnvConfig(n_npcs=3, npc_policy=2, rng=1),
+           EnvConfig(n_npcs=3, npc_policy=1, flags=3, sep_period=4)]
+    bad += [EnvConfig(n_npcs=8, npc_policy=3), EnvConfig(n_npcs=8, npc_policy=-1),
+            EnvConfig(n_npcs=8, npc_policy=1, flags=4), EnvConfig(n_npcs=8, npc_policy=2,
+                                                                   flags=64)]
     for c in ok:
         assert lib.orx_validate_cfg(ctypes.byref(c.to_c())) == 0, c
     for c in bad:
         assert lib.orx_validate_cfg(ctypes.byref(c.to_c())) == -22, c
         assert lib.orx_last_error()
+
+
+def test_max_events(lib):
+    """orx_max_events: ORX_MAX_EVENTS with Stay NPCs, 6 + 2 K records per game
+    when the NPCs move (each NPC's own move, combat or staircase death plus
+    its sweep; the players' moves, descends and health changes)."""
+    from optimax_rogue_amd import EnvConfig
+    from optimax_rogue_amd.enums import MAX_EVENTS
+    n = lambda c: lib.orx_max_events(ctypes.byref(c.to_c()))
+    assert n(EnvConfig(n_npcs=255)) == MAX_EVENTS
+    assert n(EnvConfig(n_npcs=1, npc_policy=1)) == MAX_EVENTS
+    assert n(EnvConfig(n_npcs=8, npc_policy=1)) == 22
+    assert n(EnvConfig(n_npcs=255, width=20, height=20, npc_policy=2)) == 516
+    assert n(EnvConfig(n_npcs=8, npc_policy=7)) == -22
 
 
 def test_plain_c_consumer(lib, tmp_path):
@@ -166,7 +190,7 @@ def test_plain_c_consumer(lib, tmp_path):
                     "-Wl,-rpath," + os.path.join(ROOT, "optimax_rogue_amd")], check=True)
     r = subprocess.run([str(exe)], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert "sizeof(orx_cfg_t)=112" in r.stdout
+    assert "sizeof(orx_cfg_t)=116" in r.stdout
 
 
 def test_engine_refuses_cpu():

@@ -326,7 +326,8 @@ def test_vecenv_reset_starts_next_episodes(oracle_lib):
 
 
 @pytest.mark.parametrize("case", ["c3_int64", "selfplay_int32", "stairs_opponent", "dense_bank",
-                                  "heal_ext", "sep_double_npc16", "c3_bench"])
+                                  "heal_ext", "sep_double_npc16", "c3_bench", "moving_npcs",
+                                  "moving_npcs_dense"])
 def test_vecenv_fused_step_equals_policy_step(case):
     """VecEnv.step (one orx_env_step launch, no host sync) against the
     unfused engine calls it replaces -- orx_policy for player 2, orx_step,
@@ -348,6 +349,12 @@ def test_vecenv_fused_step_equals_policy_step(case):
         cfg, opp, dt, hi = EnvConfig(width=9, height=8, n_npcs=14, npc_health=1, max_ticks=0,
                                      start_mode=2, p1_depth=0, p2_depth=1, flags=1 | 2,
                                      sep_period=3, player_health=5), 2, torch.int32, 5
+    elif case == "moving_npcs":   # the enemy AI (npc_policy RANDOM), register NPCs
+        cfg, opp, dt, hi = EnvConfig(width=9, height=9, n_npcs=12, npc_damage=2, max_ticks=60,
+                                     npc_policy=1), 1, torch.int64, 5
+    elif case == "moving_npcs_dense":   # CHASE, dense NPCs, StaircaseBot opponent
+        cfg, opp, dt, hi = EnvConfig(width=12, height=12, n_npcs=30, npc_health=2, max_ticks=60,
+                                     npc_policy=2), 2, torch.int32, 5
     elif case == "selfplay_int32":
         cfg, opp, dt, hi = EnvConfig(width=8, height=7, n_npcs=3, max_ticks=30,
                                      player_health=3), None, torch.int32, 5
@@ -463,7 +470,6 @@ def test_vecenv_deferred_bad_action_check():
         bad[[1, 7, 200]] = 0                       # a 0-based argmax in three games
         env.step(bad)
         raised = 0
-        t0 = int(env.engine.tick.sum())
         with warnings.catch_warnings(record=True) as w:
             warnings.simplefilter("always")
             for _ in range(60):
@@ -480,7 +486,6 @@ def test_vecenv_deferred_bad_action_check():
         else:
             assert raised == 1 and not msgs
         assert env.bad_actions() == 3
-        assert int(env.engine.tick.sum()) > t0
 
 
 def test_vecenv_check_actions_normalized():

@@ -172,12 +172,34 @@ ORACLE_CASES = {
                                   p2_depth=0, max_ticks=200, rng=1), (2, 1), 2048, 400, 21),
     "stock_ext": (dict(width=4, height=5, max_ticks=0, player_health=1, flags=3, sep_period=2,
                        rng=1), (1, 1), 2048, 200, 23),
+    # moving NPCs (npc_policy: 1 RANDOM, 2 CHASE -- the enemy AI behind
+    # Updater.decide_npc_move): register and dense NPCs, both despawn rules,
+    # a Separated start whose NPC depth is left and re-entered, a bank, stock
+    # seeding, the build extensions
+    "mnpc_random_c3": (dict(width=64, height=64, n_npcs=8, max_ticks=300, npc_policy=1), (1, 1),
+                       2048, 400, 60),
+    "mnpc_chase_dense": (dict(width=16, height=14, n_npcs=40, npc_health=2, max_ticks=150,
+                              npc_policy=2), (2, 1), 1024, 300, 61),
+    "mnpc_random_dense_unused": (dict(width=12, height=12, n_npcs=30, npc_health=2, despawn=2,
+                                      max_ticks=120, npc_policy=1), (2, 2), 1024, 300, 62),
+    "mnpc_stairs_unused": (dict(width=10, height=9, n_npcs=12, despawn=2, max_ticks=100,
+                                npc_policy=1), (2, 2), 2048, 300, 63),
+    "mnpc_separated": (dict(width=9, height=9, start_mode=2, p1_depth=3, p2_depth=0, n_npcs=6,
+                            max_ticks=200, npc_policy=1), (2, 1), 2048, 300, 64),
+    "mnpc_chase_bank": (dict(width=12, height=10, n_npcs=10, max_ticks=150, npc_policy=2),
+                        (1, 2), 2048, 300, 65),
+    "mnpc_stock": (dict(width=8, height=8, n_npcs=6, max_ticks=80, rng=1, npc_policy=1), (1, 2),
+                   1024, 240, 66),
+    "mnpc_ext": (dict(width=8, height=8, start_mode=2, p1_depth=0, p2_depth=1, n_npcs=9,
+                      npc_damage=2, max_ticks=0, flags=3, sep_period=3, npc_policy=2), (2, 1),
+                 2048, 300, 67),
 }
 ORACLE_BANKS = {"bank_64_npc": (64, 64, 16, 21, (1,)), "bank_stairs_unused": (12, 10, 5, 22, (1, 3)),
                 "npc_dense_bank": (12, 10, 6, 46, (1, 2)),
                 "bank_big_global": (36, 36, 64, 27, (1, 2)),
                 "stock_bank_separated": (12, 10, 7, 24, (1, 2)),
-                "npc_stair_unused_bank": (8, 7, 6, 50, (1, 2))}
+                "npc_stair_unused_bank": (8, 7, 6, 50, (1, 2)),
+                "mnpc_chase_bank": (12, 10, 5, 51, (1, 2))}
 
 
 @pytest.mark.parametrize("name", sorted(ORACLE_CASES))
@@ -485,23 +507,29 @@ def test_c3_full_size_properties(oracle_lib):
 
 
 def _timed_form_vs_oracle(oracle_lib, eng, parts, obs, act, launch, cfg, pol, seed, T, L,
-                          starts, offset=0, compact=False):
+                          starts, offset=0, compact=False, win=8, whole=False):
     """Runs ``launch`` (a pre-bound rollout launcher over ``parts``, each with
-    its obs/act buffers) L times as bench.py issues it, and replays 8-game
-    windows of consecutive games starting at local index ``starts`` (global
-    id = ``offset`` + local) on the oracle tick by tick: every tick's
-    14-field observation row and both actions of every launch, and the whole
-    state after each launch (``compact``: the launch writes ORX_OBS_COMPACT
-    rows, decoded before the comparison).  Returns the last snapshot and the
+    its obs/act buffers) L times as bench.py issues it, and replays
+    ``win``-game windows of consecutive games starting at local index
+    ``starts`` (global id = ``offset`` + local) on the oracle tick by tick:
+    every tick's 14-field observation row and both actions of every launch,
+    and the whole state after each launch (``compact``: the launch writes
+    ORX_OBS_COMPACT rows, decoded before the comparison).  ``whole``: also
+    every game of the batch against a threaded oracle over all of it (its
+    whole state after every launch).  Returns the last snapshot and the
     sampled local indices."""
     import torch
+    from oracle_pool import OraclePool
     dev = parts[0].device
-    gids = np.concatenate([np.arange(s, s + 8) for s in starts]) + offset
+    gids = np.concatenate([np.arange(s, s + win) for s in starts]) + offset
     oras = []
     for s in starts:
-        o = oracle_lib.Oracle(cfg.to_dict(), 8, seed, s + offset, layouts=cfg.layouts)
-        o.reset(episode=np.zeros(8, np.int32))
+        o = oracle_lib.Oracle(cfg.to_dict(), win, seed, s + offset, layouts=cfg.layouts)
+        o.reset(episode=np.zeros(win, np.int32))
         oras.append(o)
+    B = sum(e.B for e in parts)
+    pool = OraclePool(oracle_lib, cfg.to_dict(), B, seed, offset,
+                      layouts=cfg.layouts) if whole else None
     # per shard: which sampled ids it holds, at which local index
     sel = []
     for e in parts:
@@ -527,13 +555,16 @@ def _timed_form_vs_oracle(oracle_lib, eng, parts, obs, act, launch, cfg, pol, se
             g_act[:, pos] = a.index_select(1, li).cpu().numpy()
         snap = eng.snapshot()
         for w, (s, ora) in enumerate(zip(starts, oras)):
-            cols = slice(8 * w, 8 * w + 8)
+            cols = slice(win * w, win * w + win)
             w_act, w_obs = _replay(ora, T, pol)
-            where = f"launch {n} ids {s}..{s + 7}"
+            where = f"launch {n} ids {s}..{s + win - 1}"
             assert np.array_equal(g_act[:, cols], w_act), f"{where}: actions"
             assert np.array_equal(g_obs[:, :, cols], w_obs), f"{where}: observation rows"
-            got = {k: v[..., s:s + 8] for k, v in snap.items()}
+            got = {k: v[..., s:s + win] for k, v in snap.items()}
             compare_state(got, ora.export(), cfg.n_npcs, f"{where}: state")
+        if pool is not None:   # every game of the batch
+            pool.rollout(*pol, T)
+            compare_state(snap, pool.export(), cfg.n_npcs, f"launch {n}: all {B} games")
     return snap, gids - offset
 
 
@@ -556,10 +587,12 @@ def test_bench_timed_path_vs_oracle(offset, oracle_lib):
     games per wave -- for 9 back-to-back 128-tick launches (1,152 ticks: every
     game crosses the max_ticks-1000 autoreset), as bench.py issues them (fork,
     launches, join); at game offset 0 (rank 0) and 458,752 (rank 7 of C4's
-    eight 65,536-game ranks).  128 games -- 16 windows of 8 consecutive
-    global ids, including both ends of each shard -- are replayed on the
-    oracle tick by tick: every tick's 14-field observation row and both
-    actions of every launch, and the whole state after each launch."""
+    eight 65,536-game ranks).  Every one of the 65,536 games: its whole state
+    after each launch against a threaded C oracle over the batch; and 4,096
+    games -- four windows of 1,024 consecutive global ids at both ends of
+    each shard -- replayed tick by tick: every tick's 14-field observation
+    row and both actions of every launch (updater.py:76-162,
+    randombot.py:20-21)."""
     import torch
     from optimax_rogue_amd import EnvConfig
     from optimax_rogue_amd.engine import StreamShardedEngine
@@ -573,11 +606,13 @@ def test_bench_timed_path_vs_oracle(offset, oracle_lib):
     assert (sh["games_per_wave"], sh["lanes_per_game"], sh["nontemporal"]) == (32, 2, True)
     obs, act = eng.trajectory_buffers(T)
     launch = eng.rollout_launcher(T, 1, 1, obs=obs, act=act)
-    starts = _window_starts(B, 32768, 12, 7)
+    starts = [0, 32768 - 1024, 32768, 65536 - 1024]
     snap, gids = _timed_form_vs_oracle(oracle_lib, eng, eng.parts, obs, act, launch, cfg,
-                                       (1, 1), seed, T, L, starts, offset)
-    # every sampled game went through the max_ticks autoreset in the timed form
-    assert (snap["ep_count"][gids] >= 1).all() and (snap["episode"][gids] >= 1).all()
+                                       (1, 1), seed, T, L, starts, offset, win=1024,
+                                       whole=True)
+    assert len(gids) == 4096
+    # every game went through the max_ticks autoreset in the timed form
+    assert (snap["ep_count"] >= 1).all() and (snap["episode"] >= 1).all()
 
 
 @pytest.mark.parametrize("sep", [0, 1])
@@ -1186,6 +1221,81 @@ def test_replay_bench_shape_fast_equals_generic():
     assert s0["ep_count"].sum() > 0 and s0["counters"][0].sum() > 0
 
 
+@pytest.mark.parametrize("paired", ["plan", "1", "0"])
+def test_replay_bench_shape_vs_oracle(paired, oracle_lib, monkeypatch):
+    """bench.py's replay_step_n extra as it is timed (C3, 65,536 games, seed
+    3, 128-tick uniform move logs, int32 rows: the fast replay_kernel) against
+    the C oracle over every game (a threaded pool stepping the same logs):
+    every tick's 14-field row of all 65,536 games and the final state, over
+    two consecutive logs (server/main.py:110-113 over updater.py:76-162);
+    in the form the plan picks and with the paired LOG form forced on / off
+    (ORX_REPLAY_PAIRED)."""
+    import torch
+    from oracle_pool import OraclePool
+    if paired != "plan":
+        monkeypatch.setenv("ORX_REPLAY_PAIRED", paired)
+    from optimax_rogue_amd import EnvConfig
+    from optimax_rogue_amd.engine import BatchedEngine
+    from optimax_rogue_amd.enums import OBS_FIELDS
+    dev = torch.device("cuda", 0)
+    B, T, seed = 65536, 128, 3
+    cfg = EnvConfig.c3()
+    eng = BatchedEngine(cfg, B, seed=seed, device=dev)
+    pool = OraclePool(oracle_lib, cfg.to_dict(), B, seed)
+    g = torch.Generator(device="cpu").manual_seed(11)
+    for k in range(2):
+        log = torch.randint(1, 6, (T, B, 2), generator=g, dtype=torch.int8)
+        obs = torch.empty((T, len(OBS_FIELDS), B), dtype=torch.int32, device=dev)
+        eng.step_n(log.to(dev), obs=obs)
+        rows = obs.cpu().numpy()
+        ln = log.numpy()
+        for t in range(T):
+            pool.step(ln[t])
+            assert np.array_equal(rows[t], _obs_rows(pool.export())), (k, t)
+    s = eng.snapshot()
+    compare_state(s, pool.export(), cfg.n_npcs, "replay final")
+    assert s["counters"][0].sum() > 0 and s["counters"][3].sum() > 0
+
+
+def test_vecenv_bench_shape_vs_oracle(oracle_lib):
+    """VecEnv.step at bench.py's vecenv_step shape (C3, 65,536 games, int64
+    learner actions for player 1, a RandomBot opponent) against the C oracle
+    over every game: the action pair played, the observation row, reward,
+    done and status of all 65,536 games every tick (optimax_rogue_bots/
+    main.py:118-155, randombot.py:20-21, updater.py:76-162)."""
+    import torch
+    from oracle_pool import OraclePool
+    from optimax_rogue_amd import EnvConfig, VecEnv
+    dev = torch.device("cuda", 0)
+    B, T, seed = 65536, 40, 3
+    cfg = EnvConfig.c3()
+    cfg.max_ticks = 25          # episodes end (reward / done) inside the window
+    env = VecEnv(cfg, B, seed=seed, device=dev, opponent=1, out_buffers=2)
+    pool = OraclePool(oracle_lib, cfg.to_dict(), B, seed)
+    g = torch.Generator(device="cpu").manual_seed(17)
+    before = pool.export()["status"]
+    dones = 0
+    for t in range(T):
+        a = torch.randint(1, 6, (B,), generator=g, dtype=torch.int64)
+        obs, r, d, st = (x.cpu().numpy() for x in env.step(a.to(dev)))
+        acts = np.full((B, 2), 5, np.int8)
+        acts[:, 0] = a.numpy()
+        acts = pool.policy(0, 1, acts)       # player 2's RandomBot
+        pool.step(acts)
+        want = pool.export()
+        assert np.array_equal(env.engine.actions.cpu().numpy(), acts), t
+        assert np.array_equal(obs, _obs_rows(want).T), t
+        assert np.array_equal(st, want["status"]), t
+        ended = (before == 1) & (want["status"] >= 2) & (want["status"] <= 4)
+        assert np.array_equal(d, ended), t
+        assert np.array_equal(r, np.where(ended, (want["status"] == 2).astype(np.float32)
+                                          - (want["status"] == 3), 0).astype(np.float32)), t
+        before = want["status"]
+        dones += int(d.sum())
+    compare_state(env.engine.snapshot(), pool.export(), cfg.n_npcs, "vecenv final")
+    assert dones >= B
+
+
 STEP_N_CASES = {
     "npc8": (dict(width=16, height=16, n_npcs=8, max_ticks=90), None),
     "dense30": (dict(width=12, height=12, n_npcs=30, npc_health=2, max_ticks=70), None),
@@ -1252,6 +1362,20 @@ def test_step_n_equals_step(name):
         finally:
             del os.environ["ORX_STEP_N_GENERIC"]
         assert np.array_equal(g_obs.cpu().numpy(), o), f"{name} generic form"
+        # the paired LOG form (pair_rollout_kernel PM 6, the plan's choice at
+        # this batch when the flags are 0) against the one-lane replay_kernel
+        for form in ("0", "1"):
+            os.environ["ORX_REPLAY_PAIRED"] = form
+            try:
+                eng5 = _engine(cfg, B, seed, 11, layouts=lay)
+                p_obs = torch.zeros_like(obs)
+                eng5.step_n(a, obs=p_obs)
+                torch.cuda.synchronize()
+            finally:
+                del os.environ["ORX_REPLAY_PAIRED"]
+            assert np.array_equal(p_obs.cpu().numpy(), o), f"{name} ORX_REPLAY_PAIRED={form}"
+            compare_state(eng5.snapshot(), ref.snapshot(), int(cfg.get("n_npcs", 0)),
+                          f"{name} ORX_REPLAY_PAIRED={form} final")
     if int(cfg.get("max_ticks", 0)) > 0 and not cfg.get("flags", 0) & 1:
         eng2 = _engine(cfg, B, seed, 11, layouts=lay)
         c_obs = torch.zeros((T, 6, B), dtype=torch.int32, device=eng.device)
