@@ -356,8 +356,9 @@ def extras(torch, cfg, dev, B_cfg, K, large_rollout=False):
     torch.cuda.empty_cache()
     # (1c) a replay: orx_step_n over a 128-tick move log (int8 [128, B, 2],
     # uniform 1..5) at the config batch, every tick's observation rows
-    # written -- replay_kernel (the rollout's tick in LOG mode, one lane per
-    # game), one launch per 128 ticks
+    # written -- the paired LOG form (pair_rollout_kernel PM 6, two lanes per
+    # game, round 6; the one-lane replay_kernel timed beside it), one launch
+    # per 128 ticks
     eng = BatchedEngine(cfg, B_cfg, seed=3, device=dev)
     T = 128
     log = torch.randint(1, 6, (T, B_cfg, 2), dtype=torch.int8, device=dev)
@@ -365,14 +366,26 @@ def extras(torch, cfg, dev, B_cfg, K, large_rollout=False):
     eng.step_n(log, obs=robs)
     rs = timed_launches(torch, lambda: eng.step_n(log, obs=robs), 10)
     rmed = sorted(rs)[len(rs) // 2]
-    rb = (bytes_per_game("rollout", K, T) + T * ACT_BYTES) * B_cfg   # + the log read
+    os.environ["ORX_REPLAY_PAIRED"] = "0"   # the one-lane replay_kernel, for the record
+    try:
+        r1 = timed_launches(torch, lambda: eng.step_n(log, obs=robs), 10)
+    finally:
+        del os.environ["ORX_REPLAY_PAIRED"]
+    one_lane = sorted(r1)[len(r1) // 2]
+    # the rows (56 B a tick) and the log read (2 B a tick, in place of the
+    # rollout's action rows: a replay writes none) + the state once
+    rb = bytes_per_game("rollout", K, T) * B_cfg
     out["replay_step_n"] = {"games": B_cfg, "ticks_per_launch": T, "us_per_launch": rmed * 1e6,
                             "env_steps_per_s": B_cfg * T / rmed,
                             "achieved_GBps": rb / rmed / 1e9,
                             "frac": rb / rmed / 1e9 / HBM_PEAK_GBS,
+                            "one_lane_us_per_launch": one_lane * 1e6,
                             "note": "orx_step_n: a 128-tick move log of both players replayed in "
-                                    "one launch with every tick's observation rows (one lane per "
-                                    "game, the generic tick); median of 10 launches"}
+                                    "one launch with every tick's observation rows: the paired "
+                                    "LOG form (pair_rollout_kernel PM 6, 32 games per wave); "
+                                    "one_lane_us_per_launch = the one-lane replay_kernel "
+                                    "(ORX_REPLAY_PAIRED=0); medians of 10 launches; bytes: rows "
+                                    "56 + log 2 per env-step + the state once"}
     del eng, log, robs
     torch.cuda.empty_cache()
     # (2) large batch: the chip full (2^21 games)
@@ -535,6 +548,20 @@ def extras(torch, cfg, dev, B_cfg, K, large_rollout=False):
                            policy="RandomBot vs StaircaseBot", grid="64x64, 8 NPCs",
                            note="two stream shards timed as the headline step (the paired "
                                 "PM 4 form); us_per_launch = one step")
+    # moving NPCs (round 6): C3 with the enemy AI plugged into
+    # Updater.decide_npc_move (npc_policy RANDOM / CHASE, reference-pinned):
+    # the literal ordered tick, one lane per game (mov_rollout_kernel)
+    from optimax_rogue_amd.enums import NpcPolicy
+    for pol_name, npol in (("c3_moving_npcs", NpcPolicy.Random), ("c3_chasing_npcs",
+                                                                  NpcPolicy.Chase)):
+        r = rollout_rate(EnvConfig(width=64, height=64, n_npcs=8, npc_policy=int(npol)), 65536, 1)
+        mb = bytes_per_game("rollout", 8, 128) * 65536
+        r.update(achieved_GBps=mb / r["us_per_launch"] / 1e3,
+                 frac=mb / r["us_per_launch"] / 1e3 / HBM_PEAK_GBS)
+        out[pol_name] = dict(r, policy="2x RandomBot", grid="64x64, 8 NPCs",
+                             note=f"npc_policy {npol.name}: every NPC's move decided, shuffled "
+                                  "and resolved per tick (updater.py:116-145) in the generic "
+                                  "one-lane form; frac by the rollout's own bytes")
     c5 = {}
     for flag in (0, EXT_SEPARATION_DAMAGE):
         c = EnvConfig.c5()

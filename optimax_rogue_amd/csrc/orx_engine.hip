@@ -2681,10 +2681,16 @@ env_step_kernel(
     orx_cfg_t hc, orx_state_t st, const void* __restrict__ actions, int32_t dsize, int32_t cols,
     int32_t pol2, int8_t* __restrict__ act, int32_t* __restrict__ obs, float* __restrict__ reward,
     uint8_t* __restrict__ done, int32_t* __restrict__ status_out, uint32_t* __restrict__ bad_count,
-    uint32_t B, Key key, uint32_t off, int32_t lds_rows) {
+    uint32_t B, Key key, uint32_t off, int32_t lds_rows, uint32_t lanes) {
   __shared__ int32_t rows_lds[256 * ORX_OBS_FIELDS];
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  const bool live = i < B;
+  // `lanes` games per wave (64, or 32: two half-full waves per SIMD at the
+  // config batch, whose state loads then overlap the other wave's tick); a
+  // workgroup's games are contiguous, its row in LDS is the game's index in it
+  const uint32_t wl = threadIdx.x & 63u;
+  const uint32_t gi = (threadIdx.x >> 6) * lanes + wl;   // the game's index in the workgroup
+  const uint32_t per_block = (blockDim.x >> 6) * lanes;
+  const uint32_t i = blockIdx.x * per_block + gi;
+  const bool live = wl < lanes && i < B;
   bool bad = false;
   if (live) {
     const int64_t hi = (EXT && (hc.flags & ORX_EXT_HEAL)) ? ORX_MOVE_HEAL : ORX_MOVE_STAY;
@@ -2720,7 +2726,7 @@ env_step_kernel(
       } else if (lds_rows) {  // (uniform)
 #pragma unroll
         for (int f = 0; f < ORX_OBS_FIELDS; ++f)
-          rows_lds[threadIdx.x * ORX_OBS_FIELDS + f] = row[f];
+          rows_lds[gi * ORX_OBS_FIELDS + f] = row[f];
       } else {
 #pragma unroll
         for (int f = 0; f < ORX_OBS_FIELDS; ++f) obs[(size_t)i * ORX_OBS_FIELDS + f] = row[f];
@@ -2747,8 +2753,8 @@ env_step_kernel(
   }
   if (lds_rows && (ORX_ENV_DIAG & 2) == 0) {  // the workgroup's rows as one run (uniform)
     __syncthreads();
-    const uint32_t g0 = blockIdx.x * blockDim.x;
-    const uint32_t n = (min(B - g0, (uint32_t)blockDim.x)) * ORX_OBS_FIELDS;
+    const uint32_t g0 = blockIdx.x * per_block;
+    const uint32_t n = (g0 < B ? min(B - g0, per_block) : 0u) * ORX_OBS_FIELDS;
     int32_t* base = obs + (size_t)g0 * ORX_OBS_FIELDS;
 #pragma unroll
     for (int k = 0; k < ORX_OBS_FIELDS; ++k) {
@@ -2756,7 +2762,7 @@ env_step_kernel(
       if (j < n) base[j] = rows_lds[j];
     }
   }
-  if (bad_count) {  // uniform
+  if (bad_count) {  // uniform (idle lanes: bad false)
     const uint64_t m = __builtin_amdgcn_ballot_w64(bad);
     if (m != 0ull && __lane_id() == (uint32_t)__builtin_ctzll(m))
       __hip_atomic_fetch_add(bad_count, (uint32_t)__builtin_popcountll(m), __ATOMIC_RELAXED,
@@ -5133,7 +5139,7 @@ __global__ void __launch_bounds__(256) stairs_kernel(orx_cfg_t hc, orx_state_t s
 #define ORX_I_ENV(N, G, X)                                                                      \
   ORX_INST template __global__ void env_step_kernel<N, G, X>(                                   \
       orx_cfg_t, orx_state_t, const void*, int32_t, int32_t, int32_t, int8_t*, int32_t*, float*, \
-      uint8_t*, int32_t*, uint32_t*, uint32_t, Key, uint32_t, int32_t);
+      uint8_t*, int32_t*, uint32_t*, uint32_t, Key, uint32_t, int32_t, uint32_t);
 #define ORX_I_PAIR(N, P, A, S, C, G)                                                            \
   ORX_INST template __global__ void pair_rollout_kernel<N, P, A, S, C, G>(                      \
       orx_cfg_t, orx_state_t, int32_t, int32_t*, int8_t*, uint32_t, Key, uint32_t, uint32_t,     \
@@ -5161,7 +5167,7 @@ __global__ void __launch_bounds__(256) stairs_kernel(orx_cfg_t hc, orx_state_t s
                                                               uint32_t, Key, uint32_t, int32_t); \
   ORX_INST template __global__ void env_step_kernel<N, G, true, true>(                          \
       orx_cfg_t, orx_state_t, const void*, int32_t, int32_t, int32_t, int8_t*, int32_t*, float*, \
-      uint8_t*, int32_t*, uint32_t*, uint32_t, Key, uint32_t, int32_t);
+      uint8_t*, int32_t*, uint32_t*, uint32_t, Key, uint32_t, int32_t, uint32_t);
 #define ORX_I_MOV_ROLLOUT(N, G, M)                                                              \
   ORX_INST template __global__ void mov_rollout_kernel<N, G, M>(                                \
       orx_cfg_t, orx_state_t, int32_t, int32_t, int32_t, int32_t*, int8_t*, uint32_t, Key,      \
@@ -5830,22 +5836,25 @@ int orx_step_n(const orx_cfg_t* cfg, const orx_state_t* st, const int8_t* action
   if (!grid && nc != kDense && rows_fit && !(gen_env && gen_env[0] == '1')) {
     const int rows = obs ? (obs_format == ORX_OBS_COMPACT ? 2 : 1) : 0;
     // the paired form (pair_rollout_kernel PM 6: two lanes per game, the
-    // rollout's paired tick on the logged moves) where the rollout's plan
-    // pairs: rows given, reference rules (env ORX_REPLAY_PAIRED=1 forces it
-    // at any batch, =0 keeps the one-lane form, for measurements)
+    // rollout's paired tick on the logged moves) for rows given under the
+    // reference's rules, at any batch: two waves per SIMD until the wave holds
+    // 32 games (C3, 65,536 games x 128 ticks, int32 rows: 103-104 us against
+    // 114-116 for the one-lane replay_kernel, profiles/r06_v3/
+    // ab_replay_paired.jsonl).  Env ORX_REPLAY_PAIRED=0 keeps the one-lane
+    // form, for measurements.
     const char* pe = getenv("ORX_REPLAY_PAIRED");
-    RolloutPlan pl = plan_rollout(cfg, 6, B, 1);
-    bool paired = rows != 0 && cfg->flags == 0 && pl.paired;
-    if (pe && pe[0] == '1' && rows != 0 && cfg->flags == 0 && paired_enabled() && !pl.paired) {
+    RolloutPlan pl;
+    bool paired = rows != 0 && cfg->flags == 0 && cfg->n_layouts == 0 && paired_enabled() &&
+                  cfg->width <= 256 && cfg->height <= 256 && !(pe && pe[0] == '0');
+    if (paired) {
       const uint64_t simds = (uint64_t)device_simds();
       uint32_t L = 32;
       while (L > 8 && (uint64_t)B < 2 * simds * L) L >>= 1;
       if (const int o = lanes_override()) L = o < 32 ? (uint32_t)o : 32u;
       pl.lanes = L;
       pl.nt = L * 4u >= 128u;
-      paired = true;
+      pl.paired = true;
     }
-    if (pe && pe[0] == '0') paired = false;
     if (paired) {
       const uint32_t lanes = pl.lanes, threads = (uint32_t)kRolloutBlock;
       const uint32_t per_block = threads / 64u * lanes;
@@ -5949,12 +5958,19 @@ int orx_env_step_ex(const orx_cfg_t* cfg, const orx_state_t* st, const void* act
   // the rows through LDS (env ORX_ENV_DIRECT_ROWS=1: direct stores, for measurements)
   const char* dr = getenv("ORX_ENV_DIRECT_ROWS");
   const int32_t lds_rows = (dr && dr[0] == '1') ? 0 : 1;
+  // games per wave: 64, or 32 where that still leaves at most two waves per
+  // SIMD (env ORX_ENV_LANES = 64 / 32 overrides, for measurements)
+  const char* le = getenv("ORX_ENV_LANES");
+  const int lo = le ? atoi(le) : 0;
+  const uint32_t env_lanes = (lo == 32 || lo == 64) ? (uint32_t)lo : 64u;
+  const uint32_t per_blk = (uint32_t)kBlock / 64u * env_lanes;
+  const dim3 env_grid((unsigned)((B + per_blk - 1) / per_blk));
   if (moving_npcs(cfg)) {
 #define ORX_ENV(N, G)                                                                           \
     if (nc == N && grid == G) {                                                                 \
-      hipLaunchKernelGGL((env_step_kernel<N, G, true, true>), grid_for(B), dim3(kBlock), 0, s,  \
+      hipLaunchKernelGGL((env_step_kernel<N, G, true, true>), env_grid, dim3(kBlock), 0, s,     \
                          *cfg, *st, actions, action_bytes, action_cols, policy_p2, act, obs,    \
-                         reward, done, status, bad_actions, B, k, off, lds_rows);               \
+                         reward, done, status, bad_actions, B, k, off, lds_rows, env_lanes);    \
       return launch_status("orx_env_step");                                                    \
     }
     ORX_MOV_NG_LIST(ORX_ENV)
@@ -5963,9 +5979,9 @@ int orx_env_step_ex(const orx_cfg_t* cfg, const orx_state_t* st, const void* act
   }
 #define ORX_ENV(N, G, X)                                                                        \
   if (nc == N && grid == G && (cfg->flags == 0 || X)) {                                        \
-    hipLaunchKernelGGL((env_step_kernel<N, G, X>), grid_for(B), dim3(kBlock), 0, s, *cfg, *st,   \
+    hipLaunchKernelGGL((env_step_kernel<N, G, X>), env_grid, dim3(kBlock), 0, s, *cfg, *st,      \
                        actions, action_bytes, action_cols, policy_p2, act, obs, reward, done,   \
-                       status, bad_actions, B, k, off, lds_rows);                               \
+                       status, bad_actions, B, k, off, lds_rows, env_lanes);                    \
     return launch_status("orx_env_step");                                                      \
   }
   ORX_ENV_LIST(ORX_ENV)

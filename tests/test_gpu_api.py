@@ -402,6 +402,36 @@ def test_vecenv_fused_step_equals_policy_step(case):
         assert np.array_equal(a[k], b[k]), (case, k)
 
 
+@pytest.mark.parametrize("cfgname,B", [("c3", 65536), ("npc_small", 1537), ("dense", 999),
+                                       ("moving", 777)])
+def test_env_step_games_per_wave_invariance(cfgname, B, monkeypatch):
+    """orx_env_step at 64 and at 32 games per wave (ORX_ENV_LANES: two
+    half-full waves per SIMD) gives identical outputs and state, batch sizes
+    that leave a partial workgroup included (its LDS row run)."""
+    import torch
+    from optimax_rogue_amd import EnvConfig, VecEnv
+    cfg = {"c3": EnvConfig.c3(), "npc_small": EnvConfig(width=9, height=8, n_npcs=5, max_ticks=30),
+           "dense": EnvConfig(width=12, height=12, n_npcs=20, max_ticks=40),
+           "moving": EnvConfig(width=9, height=9, n_npcs=6, max_ticks=40, npc_policy=1)}[cfgname]
+    dev = torch.device("cuda", 0)
+    res = []
+    for lanes in ("64", "32"):
+        monkeypatch.setenv("ORX_ENV_LANES", lanes)
+        env = VecEnv(cfg, B, seed=21, device=dev, opponent=1)
+        g = torch.Generator(device="cpu").manual_seed(2)
+        outs = []
+        for t in range(30):
+            a = torch.randint(1, 6, (B,), generator=g, dtype=torch.int64).to(dev)
+            outs.append([x.cpu() for x in env.step(a)])
+        res.append((outs, env.engine.snapshot()))
+    (o64, s64), (o32, s32) = res
+    for t, (a, b) in enumerate(zip(o64, o32)):
+        for x, y in zip(a, b):
+            assert torch.equal(x, y), (cfgname, t)
+    for k in s64:
+        assert np.array_equal(s64[k], s32[k]), (cfgname, k)
+
+
 def test_vecenv_bad_actions_truncate_on_device():
     """Values outside the Move codes (0, -1, 6 without EXT_HEAL, 257 as
     int64 -- which an int8 cast would wrap to the legal 1 -- and 128..255 as

@@ -24,13 +24,13 @@ def child(lib):
     import torch
     from bench import timed_launches
     from optimax_rogue_amd import _lib, EnvConfig
-    _lib.LIB_PATH = os.path.abspath(lib)
+    _lib.LIB_PATH = os.path.abspath(lib.partition("@")[0])
     _lib.ABI_VERSION = ctypes.CDLL(_lib.LIB_PATH).orx_abi_version()
     from optimax_rogue_amd import VecEnv, OBS_FIELDS
     from optimax_rogue_amd.engine import BatchedEngine
     dev = torch.device("cuda", 0)
     cfg = EnvConfig.c3()
-    out = {"lib": lib}
+    out = {"lib": lib, "env_lanes": os.environ.get("ORX_ENV_LANES")}
     for B in (65536, 1 << 21):
         eng = BatchedEngine(cfg, B, seed=3, device=dev)
         for _ in range(2):
@@ -106,10 +106,17 @@ def main():
     opts = dict(a[2:].split("=") for a in sys.argv[1:] if a.startswith("--") and "=" in a)
     if "--child" in sys.argv:
         return child(sys.argv[sys.argv.index("--child") + 1])
+    # a library, or lib@VAR=value (the child runs with that environment
+    # variable: one build, two launch settings, e.g. ORX_ENV_LANES=32)
     libs = [a for a in sys.argv[1:] if not a.startswith("--")]
     for _ in range(int(opts.get("reps", 3))):
-        for lib in libs:
-            r = subprocess.run([sys.executable, __file__, "--child", lib], timeout=300)
+        for spec in libs:
+            lib, _, var = spec.partition("@")
+            env = dict(os.environ)
+            if var:
+                k, v = var.split("=", 1)
+                env[k] = v
+            r = subprocess.run([sys.executable, __file__, "--child", spec], timeout=300, env=env)
             if r.returncode:
                 sys.exit(r.returncode)
 
