@@ -470,6 +470,45 @@ struct Npcs {
     const int k = find(key);
     return k >= 0 && is_alive(k);
   }
+  // slot k's cell / slot k := v for a runtime k (the moving-NPC tick's
+  // initiative order): a select of the 64-bit register pair k >> 2, then
+  // shifts -- get(k) / set(k) through rd / wr would demote q0..q7 to scratch
+  __device__ __forceinline__ uint32_t get_rt(int k) const {
+    if constexpr (NCAP == 0) {
+      return 0xFFFFu;
+    } else {
+      const int j = k >> 2;
+      uint64_t p = (uint64_t)q0 | ((uint64_t)q1 << 32);
+      if constexpr (NCAP > 4) p = j == 1 ? ((uint64_t)q2 | ((uint64_t)q3 << 32)) : p;
+      if constexpr (NCAP > 8) {
+        p = j == 2 ? ((uint64_t)q4 | ((uint64_t)q5 << 32)) : p;
+        p = j == 3 ? ((uint64_t)q6 | ((uint64_t)q7 << 32)) : p;
+      }
+      return (uint32_t)(p >> (16 * (k & 3))) & 0xFFFFu;
+    }
+  }
+  __device__ __forceinline__ void set_rt(int k, uint32_t v) {
+    if constexpr (NCAP > 0) {
+      const int sh = 16 * (k & 3), j = k >> 2;
+      const uint64_t m = 0xFFFFull << sh, b = (uint64_t)(v & 0xFFFFu) << sh;
+      uint64_t p = (uint64_t)q0 | ((uint64_t)q1 << 32);
+      p = j == 0 ? ((p & ~m) | b) : p;
+      q0 = (uint32_t)p; q1 = (uint32_t)(p >> 32);
+      if constexpr (NCAP > 4) {
+        p = (uint64_t)q2 | ((uint64_t)q3 << 32);
+        p = j == 1 ? ((p & ~m) | b) : p;
+        q2 = (uint32_t)p; q3 = (uint32_t)(p >> 32);
+      }
+      if constexpr (NCAP > 8) {
+        p = (uint64_t)q4 | ((uint64_t)q5 << 32);
+        p = j == 2 ? ((p & ~m) | b) : p;
+        q4 = (uint32_t)p; q5 = (uint32_t)(p >> 32);
+        p = (uint64_t)q6 | ((uint64_t)q7 << 32);
+        p = j == 3 ? ((p & ~m) | b) : p;
+        q6 = (uint32_t)p; q7 = (uint32_t)(p >> 32);
+      }
+    }
+  }
   // slot k := dead for a runtime k: 64-bit shifts over register pairs (a
   // switch on k lowers to a branch ladder)
   __device__ __forceinline__ void kill(int k) {
@@ -579,6 +618,8 @@ struct Npcs<kDense> {
   }
   __device__ __forceinline__ void store_alive(uint32_t*, uint32_t, uint32_t) const {}  // in place
   __device__ __forceinline__ uint32_t get(int k) const { return pos[(size_t)k * B]; }
+  __device__ __forceinline__ uint32_t get_rt(int k) const { return get(k); }
+  __device__ __forceinline__ void set_rt(int k, uint32_t key) { set(k, key); }
   __device__ __forceinline__ void set(int k, uint32_t key) {
     const int cl = cell(key);
     grid[cl] = (uint8_t)(k + 1);
@@ -2023,7 +2064,7 @@ template <int NCAP, bool EV, bool GRID, class M>
 __device__ __forceinline__ void mov_npc(const Cfg& c, int k, int32_t mv, Player& p1, Player& p2,
                                         Npcs<NCAP>& npc, const NpcTurns<NCAP>& turns,
                                         const NpcDepth& d, M& m, Deltas& dl, Events<EV>& ev) {
-  const uint32_t k0 = npc.get(k);
+  const uint32_t k0 = npc.get_rt(k);
   int32_t tx, ty;
   calc_pos((int32_t)(k0 & 0xFFu), (int32_t)(k0 >> 8), mv, tx, ty);
   const uint32_t tk = pack_xy(tx, ty);
@@ -2056,7 +2097,7 @@ __device__ __forceinline__ void mov_npc(const Cfg& c, int k, int32_t mv, Player&
     return;
   }
   if constexpr (NCAP == kDense) npc.kill_at(k0);  // (the old cell of the occupancy grid)
-  npc.set(k, tk);
+  npc.set_rt(k, tk);
   ev.emit(ORX_EV_POSITION, 3 + k, nd, (tx & 0xFFFF) | (ty << 16));
 }
 
@@ -2129,7 +2170,8 @@ __device__ __forceinline__ void tick_moving_body(const Cfg& c, Key key, Src& src
 #pragma unroll 1
       for (int k = 0; k < c.K; ++k) {
         if (!npc.is_alive(k)) continue;
-        turns.set_move(k, decide_npc_move<GRID>(c, key, d, freeze, p1, p2, npc.get(k), ai, err));
+        turns.set_move(k, decide_npc_move<GRID>(c, key, d, freeze, p1, p2, npc.get_rt(k), ai,
+                                                err));
         turns.set_slot(n++, k);
       }
     }
@@ -4863,8 +4905,13 @@ __global__ void __launch_bounds__(256) mov_rollout_kernel(orx_cfg_t hc, orx_stat
                                                           int32_t n_ticks,
                                                           int32_t* __restrict__ obs,
                                                           int8_t* __restrict__ act, uint32_t B,
-                                                          Key key, uint32_t off, int32_t fmt) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+                                                          Key key, uint32_t off, int32_t fmt,
+                                                          uint32_t lanes) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (lanes < 64u) {  // uniform: lanes >= `lanes` of every wave idle (as rollout_kernel)
+    if ((threadIdx.x & 63u) >= lanes) return;
+    i = (i >> 6) * lanes + (threadIdx.x & 63u);
+  }
   if (i >= B) return;
   const Cfg c = make_cfg(hc, st);
   const uint32_t game = off + i;
@@ -4876,7 +4923,12 @@ __global__ void __launch_bounds__(256) mov_rollout_kernel(orx_cfg_t hc, orx_stat
   Npcs<NCAP> npc;
   npc.bind(st, c, B, i);
   load_npcs(st, c, B, i, npc);
-  NpcMem m{st.npc_pos, st.npc_health, B, i};
+  // register NPCs keep their health in registers for the launch (as the
+  // rollout's NpcHpRegs), stored once at the end; dense NPCs' stays in HBM
+  constexpr bool kRegHp = NCAP > 0 && NCAP != kDense;
+  std::conditional_t<kRegHp, NpcHpRegs<NCAP>, NpcMem> m;
+  if constexpr (kRegHp) m.load(st.npc_health, c.K, B, i);
+  else m = NpcMem{st.npc_pos, st.npc_health, B, i};
   Items<NCAP> items;
   load_rpg(st, c, B, i, p1, p2, npc, items);
   Deltas dl = {0, 0, 0, 0, 0, 0};
@@ -4909,7 +4961,8 @@ __global__ void __launch_bounds__(256) mov_rollout_kernel(orx_cfg_t hc, orx_stat
       ep += 1;
       if constexpr (!MT) src.ep = ep;
       setup_game<NCAP, GRID>(c, key, src, p1, p2, npc, tick, status);
-      if constexpr (NCAP > 0) store_new_npcs(st, c, B, i, npc);
+      if constexpr (kRegHp) m.fill(c.npc_hp);  // (the cells: store_npc_cells at the end)
+      else if constexpr (NCAP > 0) store_new_npcs(st, c, B, i, npc);
       stairs_dirty = true;
       npc_dirty = true;
       sep = -1;
@@ -4925,6 +4978,7 @@ __global__ void __launch_bounds__(256) mov_rollout_kernel(orx_cfg_t hc, orx_stat
   if (NCAP > 0 && npc_dirty) {
     npc.store_alive(st.npc_alive, B, i);
     store_npc_cells(st, c, B, i, npc);
+    if constexpr (kRegHp) m.store(st.npc_health, c.K, B, i);
   }
   flush_deltas(st, B, i, dl);
 }
@@ -5171,7 +5225,7 @@ __global__ void __launch_bounds__(256) stairs_kernel(orx_cfg_t hc, orx_state_t s
 #define ORX_I_MOV_ROLLOUT(N, G, M)                                                              \
   ORX_INST template __global__ void mov_rollout_kernel<N, G, M>(                                \
       orx_cfg_t, orx_state_t, int32_t, int32_t, int32_t, int32_t*, int8_t*, uint32_t, Key,      \
-      uint32_t, int32_t);
+      uint32_t, int32_t, uint32_t);
 #define ORX_I_STAIRS(G)                                                                         \
   ORX_INST template __global__ void stairs_kernel<G>(orx_cfg_t, orx_state_t, const uint32_t*,    \
                                                      const int32_t*, const int32_t*,            \
@@ -5462,6 +5516,16 @@ int lanes_override() {  // read per launch, so a sweep can change it in-process
   return (x >= 1 && x <= 64 && (x & (x - 1)) == 0) ? x : 0;
 }
 
+// Games per wave of mov_rollout_kernel (env ORX_MOV_LANES = 1..64, a power
+// of two, overrides, for measurements)
+uint32_t mov_lanes(uint32_t B) {
+  const char* e = getenv("ORX_MOV_LANES");
+  const int x = e ? atoi(e) : 0;
+  if (x >= 1 && x <= 64 && (x & (x - 1)) == 0) return (uint32_t)x;
+  (void)B;
+  return 64u;
+}
+
 // Threads per rollout workgroup: kRolloutBlock (env ORX_ROLLOUT_THREADS = 64
 // / 128 / 256 overrides, for measurements).
 uint32_t rollout_threads(uint32_t B, uint32_t lanes) {
@@ -5629,8 +5693,13 @@ int orx_rollout_shape(const orx_cfg_t* cfg, int32_t policy_p1, int32_t policy_p2
   const uint32_t B = (uint32_t)n_games;
   out->threads_per_block = kBlock;
   out->lds_bytes = 0;
-  if (cfg->rng == ORX_RNG_MT19937 || moving_npcs(cfg)) {  // mt_ / mov_rollout_kernel: one
-                                                          // game per lane, full waves
+  if (moving_npcs(cfg)) {  // mov_rollout_kernel: one game per lane, mov_lanes per wave
+    out->games_per_wave = (int32_t)mov_lanes(B);
+    out->lanes_per_game = 1;
+    out->nontemporal = 1;
+    return ORX_OK;
+  }
+  if (cfg->rng == ORX_RNG_MT19937) {  // mt_rollout_kernel: one game per lane, full waves
     out->games_per_wave = 64;
     out->lanes_per_game = 1;
     out->nontemporal = 1;
@@ -6030,10 +6099,13 @@ int orx_rollout_ex(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p
   const int nc = ncap_for(cfg->n_npcs);
   if (moving_npcs(cfg)) {  // the ordered tick with the enemy AI, one lane per game
     const bool mt = cfg->rng == ORX_RNG_MT19937;
+    const uint32_t lanes = mov_lanes(B);
+    const uint64_t threads = (((uint64_t)B + lanes - 1) / lanes) * 64u;
+    const dim3 g((unsigned)((threads + kBlock - 1) / kBlock));
 #define ORX_ROLLOUT(N, G, M)                                                                    \
     if (nc == N && grid == G && mt == M) {                                                      \
-      hipLaunchKernelGGL((mov_rollout_kernel<N, G, M>), grid_for(B), dim3(kBlock), 0, s, *cfg,  \
-                         *st, policy_p1, policy_p2, n_ticks, obs, act, B, k, off, obs_format);  \
+      hipLaunchKernelGGL((mov_rollout_kernel<N, G, M>), g, dim3(kBlock), 0, s, *cfg, *st,       \
+                         policy_p1, policy_p2, n_ticks, obs, act, B, k, off, obs_format, lanes); \
       return launch_status("orx_rollout");                                                     \
     }
     ORX_MOV_ROLLOUT_LIST(ORX_ROLLOUT)

@@ -707,6 +707,32 @@ class StreamShardedEngine:
                 g()
         return launch
 
+    def split_log(self, log: torch.Tensor) -> list:
+        """A move log int8 [T, n_games, 2] as per-shard contiguous logs (copies)."""
+        from .parallel import shard
+        out = []
+        for k, e in enumerate(self.parts):
+            off, cnt = shard(self.B, k, len(self.parts))
+            out.append(log[:, off:off + cnt].contiguous())
+        return out
+
+    def replay_launcher(self, logs, obs=None, obs_format: int = OBS_INT32):
+        """A zero-argument callable replaying every shard's move log (orx_step_n;
+        ``logs``: per-shard int8 [T, count, 2] as ``split_log`` makes them,
+        ``obs``: per-shard row buffers or None) on the shard's own stream;
+        ordered against the caller's stream by ``fork()`` / ``join()`` as
+        ``rollout_launcher``.  Results equal one engine's orx_step_n over the
+        whole log (tests/test_gpu_parity.py)."""
+        obs = obs or [None] * len(self.parts)
+        if len(logs) != len(self.parts) or len(obs) != len(self.parts):
+            raise ValueError(f"one log and one row buffer per shard ({len(self.parts)})")
+
+        def launch():
+            for e, s, l, o in zip(self.parts, self.streams, logs, obs):
+                with torch.cuda.stream(s):
+                    e.step_n(l, obs=o, obs_format=obs_format)
+        return launch
+
     def fork(self) -> None:
         """Every shard's stream waits for the caller's current stream's work so far."""
         cur = torch.cuda.current_stream(self.device)

@@ -432,6 +432,39 @@ def test_env_step_games_per_wave_invariance(cfgname, B, monkeypatch):
         assert np.array_equal(s64[k], s32[k]), (cfgname, k)
 
 
+@pytest.mark.parametrize("cfgname,B", [("random16", 1537), ("chase8", 999), ("dense", 333),
+                                       ("stock", 257)])
+def test_moving_rollout_games_per_wave_invariance(cfgname, B, monkeypatch):
+    """mov_rollout_kernel at 64, 16 and 1 games per wave (ORX_MOV_LANES)
+    writes identical rows and actions and leaves identical state, with
+    partial waves and workgroups, autoresets inside the launch, dense NPCs
+    and stock-seed mode."""
+    import torch
+    from optimax_rogue_amd import EnvConfig, OBS_FIELDS, Policy
+    from optimax_rogue_amd.engine import BatchedEngine
+    cfg = {"random16": EnvConfig(width=12, height=12, n_npcs=16, max_ticks=30, npc_policy=1),
+           "chase8": EnvConfig(width=10, height=9, n_npcs=8, max_ticks=25, npc_policy=2),
+           "dense": EnvConfig(width=12, height=12, n_npcs=20, max_ticks=30, npc_policy=1),
+           "stock": EnvConfig(width=10, height=10, n_npcs=5, max_ticks=30, npc_policy=1,
+                              rng=1)}[cfgname]
+    dev = torch.device("cuda", 0)
+    T = 70
+    res = []
+    for lanes in ("64", "16", "1"):
+        monkeypatch.setenv("ORX_MOV_LANES", lanes)
+        eng = BatchedEngine(cfg, B, seed=8, device=dev)
+        obs = torch.empty((T, len(OBS_FIELDS), B), dtype=torch.int32, device=dev)
+        act = torch.empty((T, B, 2), dtype=torch.int8, device=dev)
+        eng.rollout(T, Policy.Random, Policy.Random, obs=obs, act=act)
+        res.append((obs.cpu(), act.cpu(), eng.snapshot()))
+    base = res[0]
+    assert int(base[2]["episode"].sum()) > 0   # autoresets happened
+    for r in res[1:]:
+        assert torch.equal(r[0], base[0]) and torch.equal(r[1], base[1]), cfgname
+        for k in base[2]:
+            assert np.array_equal(r[2][k], base[2][k]), (cfgname, k)
+
+
 def test_vecenv_bad_actions_truncate_on_device():
     """Values outside the Move codes (0, -1, 6 without EXT_HEAL, 257 as
     int64 -- which an int8 cast would wrap to the legal 1 -- and 128..255 as

@@ -1221,7 +1221,7 @@ def test_replay_bench_shape_fast_equals_generic():
     assert s0["ep_count"].sum() > 0 and s0["counters"][0].sum() > 0
 
 
-@pytest.mark.parametrize("paired", ["plan", "1", "0"])
+@pytest.mark.parametrize("paired", ["plan", "1", "0", "shards"])
 def test_replay_bench_shape_vs_oracle(paired, oracle_lib, monkeypatch):
     """bench.py's replay_step_n extra as it is timed (C3, 65,536 games, seed
     3, 128-tick uniform move logs, int32 rows: the fast replay_kernel) against
@@ -1229,25 +1229,36 @@ def test_replay_bench_shape_vs_oracle(paired, oracle_lib, monkeypatch):
     every tick's 14-field row of all 65,536 games and the final state, over
     two consecutive logs (server/main.py:110-113 over updater.py:76-162);
     in the form the plan picks and with the paired LOG form forced on / off
-    (ORX_REPLAY_PAIRED)."""
+    (ORX_REPLAY_PAIRED); and as two stream shards
+    (StreamShardedEngine.replay_launcher, "shards")."""
     import torch
     from oracle_pool import OraclePool
-    if paired != "plan":
+    if paired not in ("plan", "shards"):
         monkeypatch.setenv("ORX_REPLAY_PAIRED", paired)
     from optimax_rogue_amd import EnvConfig
-    from optimax_rogue_amd.engine import BatchedEngine
+    from optimax_rogue_amd.engine import BatchedEngine, StreamShardedEngine
     from optimax_rogue_amd.enums import OBS_FIELDS
     dev = torch.device("cuda", 0)
     B, T, seed = 65536, 128, 3
     cfg = EnvConfig.c3()
-    eng = BatchedEngine(cfg, B, seed=seed, device=dev)
+    if paired == "shards":
+        eng = StreamShardedEngine(cfg, B, seed=seed, device=dev, n_streams=2)
+    else:
+        eng = BatchedEngine(cfg, B, seed=seed, device=dev)
     pool = OraclePool(oracle_lib, cfg.to_dict(), B, seed)
     g = torch.Generator(device="cpu").manual_seed(11)
     for k in range(2):
         log = torch.randint(1, 6, (T, B, 2), generator=g, dtype=torch.int8)
-        obs = torch.empty((T, len(OBS_FIELDS), B), dtype=torch.int32, device=dev)
-        eng.step_n(log.to(dev), obs=obs)
-        rows = obs.cpu().numpy()
+        if paired == "shards":
+            obs_l, _ = eng.trajectory_buffers(T)
+            eng.fork()
+            eng.replay_launcher(eng.split_log(log.to(dev)), obs_l)()
+            eng.join()
+            rows = torch.cat(obs_l, dim=2).cpu().numpy()
+        else:
+            obs = torch.empty((T, len(OBS_FIELDS), B), dtype=torch.int32, device=dev)
+            eng.step_n(log.to(dev), obs=obs)
+            rows = obs.cpu().numpy()
         ln = log.numpy()
         for t in range(T):
             pool.step(ln[t])
