@@ -357,15 +357,37 @@ def extras(torch, cfg, dev, B_cfg, K, large_rollout=False):
     # (1c) a replay: orx_step_n over a 128-tick move log (int8 [128, B, 2],
     # uniform 1..5) at the config batch, every tick's observation rows
     # written -- the paired LOG form (pair_rollout_kernel PM 6, two lanes per
-    # game, round 6; the one-lane replay_kernel timed beside it), one launch
-    # per 128 ticks
-    eng = BatchedEngine(cfg, B_cfg, seed=3, device=dev)
+    # game, round 6) as two stream shards, the headline's recipe
+    # (StreamShardedEngine.replay_launcher: each shard's log its own
+    # contiguous slice, 3 warmup + 20 timed launches per shard between one
+    # fork and one join); one launch over the whole log and the one-lane
+    # replay_kernel timed beside it
     T = 128
     log = torch.randint(1, 6, (T, B_cfg, 2), dtype=torch.int8, device=dev)
+    se = StreamShardedEngine(cfg, B_cfg, seed=3, device=dev, n_streams=2)
+    slogs = se.split_log(log)
+    sobs, _ = se.trajectory_buffers(T)
+    go = se.replay_launcher(slogs, sobs)
+    se.fork()
+    for _ in range(3):
+        go()
+    se.join()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    ev0.record()
+    se.fork()
+    for _ in range(20):
+        go()
+    se.join()
+    ev1.record()
+    torch.cuda.synchronize()
+    rmed = ev0.elapsed_time(ev1) * 1e-3 / 20
+    del se, slogs, sobs, go
+    eng = BatchedEngine(cfg, B_cfg, seed=3, device=dev)
     robs = torch.empty((T, len(OBS_FIELDS), B_cfg), dtype=torch.int32, device=dev)
     eng.step_n(log, obs=robs)
     rs = timed_launches(torch, lambda: eng.step_n(log, obs=robs), 10)
-    rmed = sorted(rs)[len(rs) // 2]
+    one_launch = sorted(rs)[len(rs) // 2]
     os.environ["ORX_REPLAY_PAIRED"] = "0"   # the one-lane replay_kernel, for the record
     try:
         r1 = timed_launches(torch, lambda: eng.step_n(log, obs=robs), 10)
@@ -375,17 +397,21 @@ def extras(torch, cfg, dev, B_cfg, K, large_rollout=False):
     # the rows (56 B a tick) and the log read (2 B a tick, in place of the
     # rollout's action rows: a replay writes none) + the state once
     rb = bytes_per_game("rollout", K, T) * B_cfg
-    out["replay_step_n"] = {"games": B_cfg, "ticks_per_launch": T, "us_per_launch": rmed * 1e6,
+    out["replay_step_n"] = {"games": B_cfg, "ticks_per_launch": T, "streams": 2,
+                            "us_per_launch": rmed * 1e6,
                             "env_steps_per_s": B_cfg * T / rmed,
                             "achieved_GBps": rb / rmed / 1e9,
                             "frac": rb / rmed / 1e9 / HBM_PEAK_GBS,
+                            "one_launch_us": one_launch * 1e6,
                             "one_lane_us_per_launch": one_lane * 1e6,
-                            "note": "orx_step_n: a 128-tick move log of both players replayed in "
-                                    "one launch with every tick's observation rows: the paired "
-                                    "LOG form (pair_rollout_kernel PM 6, 32 games per wave); "
-                                    "one_lane_us_per_launch = the one-lane replay_kernel "
-                                    "(ORX_REPLAY_PAIRED=0); medians of 10 launches; bytes: rows "
-                                    "56 + log 2 per env-step + the state once"}
+                            "note": "orx_step_n: a 128-tick move log of both players replayed "
+                                    "with every tick's observation rows, the paired LOG form "
+                                    "(pair_rollout_kernel PM 6, 32 games per wave) as two "
+                                    "32,768-game stream shards (us_per_launch: per step of both "
+                                    "shards, 20 timed); one_launch_us = orx_step_n over the "
+                                    "whole batch in one launch, one_lane_us_per_launch = the "
+                                    "one-lane replay_kernel (ORX_REPLAY_PAIRED=0), medians of "
+                                    "10; bytes: rows 56 + log 2 per env-step + the state once"}
     del eng, log, robs
     torch.cuda.empty_cache()
     # (2) large batch: the chip full (2^21 games)

@@ -467,6 +467,14 @@ int orx_step_n(const orx_cfg_t* cfg, const orx_state_t* st, const int8_t* action
                int32_t n_ticks, int32_t* obs, int32_t obs_format, int64_t n_games, uint64_t seed,
                int64_t game_offset, void* stream);
 
+/* orx_step_n with the number of launches sharing the device (ABI 7, as
+ * orx_rollout_ex's concurrency): a batch replayed as stream shards passes the
+ * shard count, so each launch's games per wave are planned for the device's
+ * total (orx_step_n = concurrency 1).  Results do not depend on it. */
+int orx_step_n_ex(const orx_cfg_t* cfg, const orx_state_t* st, const int8_t* actions,
+                  int32_t n_ticks, int32_t* obs, int32_t obs_format, int64_t n_games,
+                  uint64_t seed, int64_t game_offset, int32_t concurrency, void* stream);
+
 /* orx_step plus the update-event list of the tick: for game b,
  * events[(b * ORX_MAX_EVENTS + j) * 4 + 0..3], j < n_events[b], in the order
  * Updater.update appends them to its result list (updater.py:133-145).

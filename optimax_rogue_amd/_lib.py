@@ -43,7 +43,8 @@ EXPORTS = ("orx_abi_version", "orx_last_error", "orx_validate_cfg", "orx_reset",
            "orx_step_events", "orx_policy", "orx_rollout", "orx_dungeon_stairs",
            "orx_dungeon_spawn", "orx_seed_mt", "orx_build_id", "orx_rollout_lanes", "orx_dstore_depths",
            "orx_rollout_shape", "orx_rollout_concurrent", "orx_env_step",
-           "orx_rollout_ex", "orx_env_step_ex", "orx_step_n", "orx_max_events")
+           "orx_rollout_ex", "orx_env_step_ex", "orx_step_n", "orx_max_events",
+           "orx_step_n_ex")
 
 
 def load() -> ctypes.CDLL:
@@ -109,6 +110,10 @@ def load() -> ctypes.CDLL:
     if hasattr(L, "orx_step_n"):
         L.orx_step_n.restype = ctypes.c_int
         L.orx_step_n.argtypes = [P(OrxCfg), P(OrxState), vp, i32, vp, i32, i64, u64, i64, vp]
+    if hasattr(L, "orx_step_n_ex"):
+        L.orx_step_n_ex.restype = ctypes.c_int
+        L.orx_step_n_ex.argtypes = [P(OrxCfg), P(OrxState), vp, i32, vp, i32, i64, u64, i64, i32,
+                                    vp]
     if hasattr(L, "orx_max_events"):
         L.orx_max_events.restype = ctypes.c_int
         L.orx_max_events.argtypes = [P(OrxCfg)]

@@ -108,11 +108,22 @@ __device__ uint64_t g_stamps[65536 * 16];
 #define ORX_CYC_END(var, v)                                                            \
   var += (__lane_id() == (uint32_t)__builtin_ctzll(__builtin_amdgcn_read_exec()))     \
              ? (uint32_t)(__builtin_amdgcn_s_memtime() - (v)) : 0u
+// the moving-NPC rollout's sections: the first active lane of a wave adds
+// the section's shader-clock cycles to the wave's slot j (a vector atomic;
+// orx_diag_stamps_clear zeroes the slots first)
+#define ORX_MCYC_BEGIN(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#define ORX_MCYC_END(j, v)                                                                \
+  if (__lane_id() == (uint32_t)__builtin_ctzll(__builtin_amdgcn_read_exec()))             \
+  atomicAdd((unsigned long long*)&g_stamps[(size_t)((blockIdx.x * blockDim.x + threadIdx.x) >> 6) * \
+                                               16 + (j)],                                  \
+            (unsigned long long)(__builtin_amdgcn_s_memtime() - (v)))
 #else
 #define ORX_STAMP(j) ((void)0)
 #define ORX_COUNT(var) ((void)0)
 #define ORX_CYC_BEGIN(v) ((void)0)
 #define ORX_CYC_END(var, v) ((void)0)
+#define ORX_MCYC_BEGIN(v) ((void)0)
+#define ORX_MCYC_END(j, v) ((void)0)
 #endif
 #ifndef ORX_ROLLOUT_BLOCK
 #define ORX_ROLLOUT_BLOCK 256
@@ -1853,11 +1864,41 @@ __device__ __forceinline__ void end_tick(const Cfg& c, Key key, uint32_t game, u
 // skipped for good), then the top k bits of the next word of stream `s`;
 // with `refill` every word of `s` is a 30-bit segment of its own (the NPC
 // stream, purpose NPC, c2 = tick).  make_golden.TickBits / NpcBits.
+// The stream's first NB 4-word blocks are drawn up front, in the tick's
+// uniform control flow: its consumers run in per-lane loops (the AI's
+// rejection draws, the Fisher-Yates shuffle), where a Philox call inside the
+// loop body costs the whole wave whenever any one lane crosses a block
+// boundary.  Words past them come from the lazy Stream at block NB.
+template <int NB>
+struct AheadStream {
+  static_assert(NB == 1 || NB == 2, "one or two blocks ahead");
+  Stream s;
+  W4 w0, w1;
+  uint32_t i;
+  __device__ __forceinline__ void init(uint32_t game, uint32_t ep, uint32_t cc2, uint32_t t,
+                                       Key key) {
+    s.init(game, ep, cc2, t, 4u * NB);
+    w0 = philox(game, ep, cc2, t, key);
+    if constexpr (NB > 1) w1 = philox(game, ep, cc2, t | 1u, key);
+    i = 0;
+  }
+  __device__ __forceinline__ uint32_t next(Key key) {
+    if (i < 4u * NB) {
+      const uint32_t j = i & 3u;
+      const W4 v = (NB > 1 && i >= 4u) ? w1 : w0;
+      ++i;
+      return j == 0 ? v.a : j == 1 ? v.b : j == 2 ? v.c : v.d;
+    }
+    return s.next(key);
+  }
+};
+
+template <class S>
 struct PyBits {
   uint32_t res;
   int32_t nb;
   bool refill;
-  Stream s;
+  S s;
   __device__ __forceinline__ uint32_t bits(int k, Key key) {
     if (nb < k) {
       if (refill) {
@@ -2134,13 +2175,14 @@ __device__ __forceinline__ void npc_sweep(const Cfg& c, Npcs<NCAP>& npc, M& m, D
   }
 }
 
-template <int NCAP, bool EV, bool GRID, class Src, class M, class Bits>
+template <int NCAP, bool EV, bool GRID, class Src, class M, class BitsS, class BitsA>
 __device__ __forceinline__ void tick_moving_body(const Cfg& c, Key key, Src& src, uint32_t game,
                                                  uint32_t ep, Player& p1, Player& p2,
                                                  Npcs<NCAP>& npc, M& m, int32_t& tick,
                                                  int32_t& status, bool& err, Deltas& dl,
-                                                 Events<EV>& ev, int32_t& sep_start, Bits& sh,
-                                                 Bits& ai) {
+                                                 Events<EV>& ev, int32_t& sep_start, BitsS& sh,
+                                                 BitsA& ai) {
+  ORX_MCYC_BEGIN(cy0);
   p1.heal = p2.heal = 0;
   calc_pos(p1.x, p1.y, p1.move, p1.tx, p1.ty);          // updater.py:89-98
   if (blocked<GRID>(c, p1.lay, p1.tx, p1.ty)) p1.move = ORX_MOVE_STAY;
@@ -2155,6 +2197,8 @@ __device__ __forceinline__ void tick_moving_body(const Cfg& c, Key key, Src& src
     d = npc_depth<GRID>(c, key, src, game, ep, p1, p2, err);
     const bool freeze = d.present && ((p1.d == c.d1 && next_to_stairs<GRID>(c, d, p1)) ||
                                       (p2.d == c.d1 && next_to_stairs<GRID>(c, d, p2)));
+    ORX_MCYC_END(0, cy0);
+    ORX_MCYC_BEGIN(cy1);
     // decide_npc_move for every NPC in GameState.entities order (:116-126)
     if constexpr (NCAP == kDense) {
       for (int r = 0; r < (c.K + 31) >> 5; ++r) {
@@ -2175,6 +2219,8 @@ __device__ __forceinline__ void tick_moving_body(const Cfg& c, Key key, Src& src
         turns.set_slot(n++, k);
       }
     }
+    ORX_MCYC_END(1, cy1);
+    ORX_MCYC_BEGIN(cy2);
     // random.shuffle(npcs) (:127): Fisher-Yates over the list
 #pragma unroll 1
     for (int i = n - 1; i >= 1; --i) {
@@ -2183,7 +2229,9 @@ __device__ __forceinline__ void tick_moving_body(const Cfg& c, Key key, Src& src
       turns.set_slot(i, sj);
       turns.set_slot(j, si);
     }
+    ORX_MCYC_END(2, cy2);
   }
+  ORX_MCYC_BEGIN(cy3);
   // handle_move in initiative order (:133-134): the players, then the NPCs
   auto&& spawn = src.spawn(tick);
   Player A = pick(p1_first, p1, p2);
@@ -2195,6 +2243,8 @@ __device__ __forceinline__ void tick_moving_body(const Cfg& c, Key key, Src& src
                              turns, m, spawn, dl, err, ev);
   p1 = pick(p1_first, A, Bp);
   p2 = pick(p1_first, Bp, A);
+  ORX_MCYC_END(3, cy3);
+  ORX_MCYC_BEGIN(cy4);
   if constexpr (NCAP > 0) {
 #pragma unroll 1
     for (int j = 0; j < n; ++j) {
@@ -2203,9 +2253,12 @@ __device__ __forceinline__ void tick_moving_body(const Cfg& c, Key key, Src& src
       if (mv != ORX_MOVE_STAY) mov_npc<NCAP, EV, GRID>(c, k, mv, p1, p2, npc, turns, d, m, dl, ev);
       turns.mark(k);
     }
+    ORX_MCYC_END(4, cy4);
     npc_sweep(c, npc, m, dl, ev);                       // :136-145
   }
+  ORX_MCYC_BEGIN(cy5);
   end_tick<EV>(c, key, game, ep, p1, p2, tick, status, err, dl, ev, sep_start);
+  ORX_MCYC_END(5, cy5);
 }
 
 // One Updater.update with moving NPCs (p1.move / p2.move = the raw moves):
@@ -2218,21 +2271,25 @@ __device__ __forceinline__ void tick_moving(const Cfg& c, Key key, Src& src, uin
                                             uint32_t ep, Player& p1, Player& p2,
                                             Npcs<NCAP>& npc, M& m, int32_t& tick,
                                             int32_t& status, bool& err, Deltas& dl,
-                                            Events<EV>& ev, int32_t& sep_start) {
+                                            Events<EV>& ev, int32_t& sep_start,
+                                            const W4* tb = nullptr) {
   if constexpr (Src::kMt) {
     MtBits b{&src.py};
     tick_moving_body<NCAP, EV, GRID>(c, key, src, game, ep, p1, p2, npc, m, tick, status, err, dl,
                                      ev, sep_start, b, b);
   } else {
-    PyBits sh, ai;
-    sh.res = tick_block(key, game, ep, tick).a;
+    // (blocks ahead: the shuffle of 8 NPCs takes ~5 words past the tick
+    // block's word, the AI's choices of 8 ~2)
+    PyBits<AheadStream<2>> sh;
+    PyBits<AheadStream<1>> ai;
+    sh.res = tb ? tb->a : tick_block(key, game, ep, tick).a;  // (the caller's block if drawn)
     sh.nb = 32;
     sh.refill = false;
-    sh.s.init(game, ep, (uint32_t)tick, tag(PUR_SHUFFLE, 0));
+    sh.s.init(game, ep, (uint32_t)tick, tag(PUR_SHUFFLE, 0), key);
     ai.res = 0u;
     ai.nb = 0;
     ai.refill = true;
-    ai.s.init(game, ep, (uint32_t)tick, tag(PUR_NPC, 0));
+    ai.s.init(game, ep, (uint32_t)tick, tag(PUR_NPC, 0), key);
     tick_moving_body<NCAP, EV, GRID>(c, key, src, game, ep, p1, p2, npc, m, tick, status, err, dl,
                                      ev, sep_start, sh, ai);
   }
@@ -4938,26 +4995,33 @@ __global__ void __launch_bounds__(256) mov_rollout_kernel(orx_cfg_t hc, orx_stat
   if constexpr (MT) src.open(st, c, B, i);
   else src = PhiloxSrc{key, game, ep};
   TrajWriter<false> traj(obs, act, B, i, fmt);
-  const bool rng = pol1 == ORX_POLICY_RANDOM || pol2 == ORX_POLICY_RANDOM;
+  ORX_MCYC_BEGIN(cyl);
   for (int32_t t = 0; t < n_ticks; ++t) {
     int32_t a1 = ORX_MOVE_STAY, a2 = ORX_MOVE_STAY;
     bool err = false;
+    ORX_MCYC_BEGIN(cy6);
+    // the tick block serves the RandomBots and the moving tick's first draws
+    W4 tb{0u, 0u, 0u, 0u};
     if constexpr (MT) {
       mt_policy_pair(src.py, pol1, pol2, p1, p2, a1, a2, err);
     } else {
-      const W4 tb = rng ? tick_block(key, game, ep, tick) : W4{0u, 0u, 0u, 0u};
+      tb = tick_block(key, game, ep, tick);
       policy_pair(key, game, ep, tick, pol1, pol2, tb, p1, p2, a1, a2);
     }
+    ORX_MCYC_END(6, cy6);
     if (status == ORX_IN_PROGRESS) {
+      ORX_MCYC_BEGIN(cyt);
       p1.move = a1;
       p2.move = a2;
       const int32_t descents = dl.descend;
       Events<false> ev{nullptr, 0};
       tick_moving<NCAP, false, GRID>(c, key, src, game, ep, p1, p2, npc, m, tick, status, err, dl,
-                                     ev, sep);
+                                     ev, sep, MT ? nullptr : &tb);
       stairs_dirty |= dl.descend != descents;
       npc_dirty = true;
+      ORX_MCYC_END(10, cyt);
     } else if (c.autoreset) {
+      ORX_MCYC_BEGIN(cy7);
       ep += 1;
       if constexpr (!MT) src.ep = ep;
       setup_game<NCAP, GRID>(c, key, src, p1, p2, npc, tick, status);
@@ -4966,9 +5030,13 @@ __global__ void __launch_bounds__(256) mov_rollout_kernel(orx_cfg_t hc, orx_stat
       stairs_dirty = true;
       npc_dirty = true;
       sep = -1;
+      ORX_MCYC_END(7, cy7);
     }
+    ORX_MCYC_BEGIN(cy8);
     traj.write(t, p1, p2, tick, status, a1, a2);
+    ORX_MCYC_END(8, cy8);
   }
+  ORX_MCYC_END(9, cyl);
   if constexpr (MT) src.close();
   store_players<GRID>(st, B, i, p1, p2, stairs_dirty);
   st.tick[i] = tick;
@@ -5870,7 +5938,15 @@ int orx_step_events(const orx_cfg_t* cfg, const orx_state_t* st, const int8_t* a
 int orx_step_n(const orx_cfg_t* cfg, const orx_state_t* st, const int8_t* actions,
                int32_t n_ticks, int32_t* obs, int32_t obs_format, int64_t n_games, uint64_t seed,
                int64_t game_offset, void* stream) {
+  return orx_step_n_ex(cfg, st, actions, n_ticks, obs, obs_format, n_games, seed, game_offset, 1,
+                       stream);
+}
+
+int orx_step_n_ex(const orx_cfg_t* cfg, const orx_state_t* st, const int8_t* actions,
+                  int32_t n_ticks, int32_t* obs, int32_t obs_format, int64_t n_games,
+                  uint64_t seed, int64_t game_offset, int32_t concurrency, void* stream) {
   int r;
+  if (concurrency < 1) return fail(ORX_EINVAL, "concurrency must be >= 1");
   if ((r = check_cfg(cfg)) || (r = check_sizes(n_games, game_offset))) return r;
   if (n_ticks < 0) return fail(ORX_EINVAL, "n_ticks < 0");
   if (obs_format != ORX_OBS_INT32 && obs_format != ORX_OBS_COMPACT)
@@ -5906,11 +5982,13 @@ int orx_step_n(const orx_cfg_t* cfg, const orx_state_t* st, const int8_t* action
     const int rows = obs ? (obs_format == ORX_OBS_COMPACT ? 2 : 1) : 0;
     // the paired form (pair_rollout_kernel PM 6: two lanes per game, the
     // rollout's paired tick on the logged moves) for rows given under the
-    // reference's rules, at any batch: two waves per SIMD until the wave holds
-    // 32 games (C3, 65,536 games x 128 ticks, int32 rows: 103-104 us against
-    // 114-116 for the one-lane replay_kernel, profiles/r06_v3/
-    // ab_replay_paired.jsonl).  Env ORX_REPLAY_PAIRED=0 keeps the one-lane
-    // form, for measurements.
+    // reference's rules, at any batch: two waves per SIMD over the device's
+    // concurrent launches until the wave holds 32 games (C3, 65,536 games x
+    // 128 ticks, int32 rows: 103-104 us against 114-116 for the one-lane
+    // replay_kernel; as two 32,768-game stream shards at 32 games per wave
+    // 85-86 us, at 16 -- the plan without the concurrency -- 207,
+    // profiles/r06_v3 / r06_v4 ab_replay_paired.jsonl).  Env
+    // ORX_REPLAY_PAIRED=0 keeps the one-lane form, for measurements.
     const char* pe = getenv("ORX_REPLAY_PAIRED");
     RolloutPlan pl;
     bool paired = rows != 0 && cfg->flags == 0 && cfg->n_layouts == 0 && paired_enabled() &&
@@ -5918,7 +5996,7 @@ int orx_step_n(const orx_cfg_t* cfg, const orx_state_t* st, const int8_t* action
     if (paired) {
       const uint64_t simds = (uint64_t)device_simds();
       uint32_t L = 32;
-      while (L > 8 && (uint64_t)B < 2 * simds * L) L >>= 1;
+      while (L > 8 && (uint64_t)B * (uint32_t)concurrency < 2 * simds * L) L >>= 1;
       if (const int o = lanes_override()) L = o < 32 ? (uint32_t)o : 32u;
       pl.lanes = L;
       pl.nt = L * 4u >= 128u;
@@ -6213,6 +6291,11 @@ int orx_rollout_ex(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p
 }
 
 #ifdef ORX_STAMPS
+int orx_diag_stamps_clear(void) {
+  void* p = nullptr;
+  if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_stamps)) != hipSuccess) return -1;
+  return hipMemset(p, 0, sizeof(g_stamps)) == hipSuccess ? 0 : -1;
+}
 int orx_diag_stamps(uint64_t* host, int64_t n) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), (size_t)n * 8, 0, hipMemcpyDeviceToHost)
              == hipSuccess ? 0 : -1;

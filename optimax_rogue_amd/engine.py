@@ -310,8 +310,8 @@ class BatchedEngine:
                              f"{self.device}")
         T = int(actions.shape[0])
         self._check_traj(T, obs, None, obs_format)
-        self._call("orx_step_n", _ptr(actions), T, _ptr(obs), int(obs_format), self.B, self.seed,
-                   self.game_offset, self._stream())
+        self._call("orx_step_n_ex", _ptr(actions), T, _ptr(obs), int(obs_format), self.B,
+                   self.seed, self.game_offset, int(self.concurrency), self._stream())
         return self.status
 
     # learner action widths orx_env_step_ex reads (uint8 as int8: 1..6 read

@@ -43,6 +43,9 @@ int main(void) {
   if (orx_step_n(&c, NULL, NULL, -1, NULL, ORX_OBS_INT32, 16, 1, 0, NULL) != ORX_EINVAL) {
     printf("negative n_ticks accepted\n"); return 17;
   }
+  if (orx_step_n_ex(&c, NULL, NULL, 5, NULL, ORX_OBS_INT32, 16, 1, 0, 0, NULL) != ORX_EINVAL) {
+    printf("orx_step_n_ex accepted concurrency 0\n"); return 20;
+  }
   {
     orx_rollout_shape_t sh;
     if (orx_rollout_shape(&c, ORX_POLICY_RANDOM, ORX_POLICY_RANDOM, 65536, 1, 1, &sh) != ORX_OK ||

@@ -38,7 +38,8 @@ def test_library_exports_every_declared_symbol(lib):
                            "orx_dungeon_stairs", "orx_dungeon_spawn", "orx_seed_mt",
                            "orx_build_id", "orx_rollout_lanes", "orx_dstore_depths",
                            "orx_rollout_shape", "orx_rollout_concurrent", "orx_env_step",
-                           "orx_rollout_ex", "orx_env_step_ex", "orx_step_n", "orx_max_events"])
+                           "orx_rollout_ex", "orx_env_step_ex", "orx_step_n", "orx_max_events",
+                           "orx_step_n_ex"])
     from optimax_rogue_amd import _lib
     assert sorted(_lib.EXPORTS) == decl
     for name in decl:
