@@ -2025,6 +2025,15 @@ __device__ __forceinline__ bool next_to_stairs(const Cfg& c, const NpcDepth& d, 
   }
 }
 
+// The AI's move m for the NPC on cell key `nk`, or Stay where it is blocked
+template <bool GRID>
+__device__ __forceinline__ int32_t npc_step_or_stay(const Cfg& c, const NpcDepth& d, uint32_t nk,
+                                                    int32_t m) {
+  int32_t tx, ty;
+  calc_pos((int32_t)(nk & 0xFFu), (int32_t)(nk >> 8), m, tx, ty);
+  return blocked<GRID>(c, d.lay, tx, ty) ? ORX_MOVE_STAY : m;
+}
+
 // decide_npc_move (updater.py:165-178) for the NPC on cell key `nk`
 template <bool GRID, class Bits>
 __device__ __forceinline__ int32_t decide_npc_move(const Cfg& c, Key key, const NpcDepth& d,
@@ -2045,9 +2054,7 @@ __device__ __forceinline__ int32_t decide_npc_move(const Cfg& c, Key key, const 
     m = abs(dx) > abs(dy) ? (dx > 0 ? ORX_MOVE_RIGHT : ORX_MOVE_LEFT)
                           : (dy > 0 ? ORX_MOVE_DOWN : ORX_MOVE_UP);
   }
-  int32_t tx, ty;
-  calc_pos(x, y, m, tx, ty);
-  return blocked<GRID>(c, d.lay, tx, ty) ? ORX_MOVE_STAY : m;
+  return npc_step_or_stay<GRID>(c, d, nk, m);
 }
 
 // The flag of a move into an occupied cell (updater.py:222-243): the
@@ -2211,23 +2218,101 @@ __device__ __forceinline__ void tick_moving_body(const Cfg& c, Key key, Src& src
         }
       }
     } else {
+#pragma unroll
+      for (int k = 0; k < NCAP; ++k)
+        if (k < c.K && npc.is_alive(k)) turns.set_slot(n++, k);
+      if (c.npc_pol == ORX_NPC_RANDOM && d.present && !freeze) {
+        // random.choice(list(Move)) per NPC as ONE per-lane loop over all the
+        // NPCs' rejection draws (randbelow_bits unrolled by hand: same draws,
+        // same give-up rule), so a wave iterates the max over its lanes of
+        // the draws' sum -- a loop per NPC would cost the sum over NPCs of
+        // the max, ~2x the draws at 64 lanes
+        // The loop only collects the accepted draws (3 bits each, in alive
+        // order); the moves follow in an unrolled pass over the slots, where
+        // slot k's draw is the one at its rank among the alive slots.
+        int j = 0;
+        uint32_t tries = 0;
+        uint64_t draws = 0;
 #pragma unroll 1
-      for (int k = 0; k < c.K; ++k) {
-        if (!npc.is_alive(k)) continue;
-        turns.set_move(k, decide_npc_move<GRID>(c, key, d, freeze, p1, p2, npc.get_rt(k), ai,
-                                                err));
-        turns.set_slot(n++, k);
+        while (j < n) {
+          const uint32_t r = ai.bits(3, key);
+          const bool acc = r < 5u;
+          const bool give_up = !acc && ++tries >= kWordCap;
+          if (acc || give_up) {
+            err |= give_up;
+            draws |= (uint64_t)(acc ? r : 0u) << (3 * j);
+            ++j;
+            tries = 0;
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < NCAP; ++k) {
+          if (k < c.K && npc.is_alive(k)) {
+            const int rank = __popc(npc.alive & ((1u << k) - 1u));
+            const int32_t mv = 1 + (int32_t)((draws >> (3 * rank)) & 7ull);
+            turns.set_move(k, npc_step_or_stay<GRID>(c, d, npc.get(k), mv));
+          }
+        }
+      } else {
+#pragma unroll 1
+        for (int j = 0; j < n; ++j) {
+          const int k = turns.slot(j);
+          turns.set_move(k, decide_npc_move<GRID>(c, key, d, freeze, p1, p2, npc.get_rt(k), ai,
+                                                  err));
+        }
       }
     }
     ORX_MCYC_END(1, cy1);
     ORX_MCYC_BEGIN(cy2);
-    // random.shuffle(npcs) (:127): Fisher-Yates over the list
+    // random.shuffle(npcs) (:127): Fisher-Yates over the list, its rejection
+    // draws as one per-lane loop (as the AI's above)
+    if constexpr (NCAP == kDense) {
+      int i = n - 1;
+      uint32_t tries = 0;
 #pragma unroll 1
-    for (int i = n - 1; i >= 1; --i) {
-      const int j = (int)randbelow_bits(sh, key, (uint32_t)i + 1u, err);
-      const int si = turns.slot(i), sj = turns.slot(j);
-      turns.set_slot(i, sj);
-      turns.set_slot(j, si);
+      while (i >= 1) {
+        const uint32_t bound = (uint32_t)i + 1u;
+        const uint32_t r = sh.bits(32 - __clz(bound), key);
+        const bool acc = r < bound;
+        const bool give_up = !acc && ++tries >= kWordCap;
+        if (acc || give_up) {
+          err |= give_up;
+          const int jj = acc ? (int)r : 0;
+          const int si = turns.slot(i), sj = turns.slot(jj);
+          turns.set_slot(i, sj);
+          turns.set_slot(jj, si);
+          --i;
+          tries = 0;
+        }
+      }
+    } else if constexpr (NCAP > 0) {
+      // register NPCs: the loop collects each position's accepted draw (4
+      // bits at 4 i), the swaps follow unrolled, in the shuffle's order
+      int i = n - 1;
+      uint32_t tries = 0;
+      uint64_t js = 0;
+#pragma unroll 1
+      while (i >= 1) {
+        const uint32_t bound = (uint32_t)i + 1u;
+        const uint32_t r = sh.bits(32 - __clz(bound), key);
+        const bool acc = r < bound;
+        const bool give_up = !acc && ++tries >= kWordCap;
+        if (acc || give_up) {
+          err |= give_up;
+          js |= (uint64_t)(acc ? r : 0u) << (4 * i);
+          --i;
+          tries = 0;
+        }
+      }
+#pragma unroll
+      for (int ii = NCAP - 1; ii >= 1; --ii) {
+        if (ii < n) {
+          const int jj = (int)((js >> (4 * ii)) & 15ull);
+          const int si = turns.slot(ii), sj = turns.slot(jj);
+          turns.set_slot(ii, sj);
+          turns.set_slot(jj, si);
+        }
+      }
     }
     ORX_MCYC_END(2, cy2);
   }
