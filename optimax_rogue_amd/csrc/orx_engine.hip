@@ -1934,6 +1934,73 @@ __device__ __forceinline__ uint32_t randbelow_bits(Bits& b, Key key, uint32_t n,
   return 0;
 }
 
+// Keyed mode's AI draws of a tick, branch-free: random.choice(list(Move))
+// for n NPCs is randbelow(5) n times over the NPC stream's 30-bit segments,
+// i.e. NPC j's value is the j-th accepted 3-bit field (value < 5) of the
+// field sequence (10 per word, LSB first; kWordCap rejections in a row give
+// up with 0 and err, as randbelow_bits).  A word's ten fields are scanned
+// unrolled, and the lanes loop over words, not over draws.  Returns the
+// values packed 3 bits apiece.
+template <class D>
+__device__ __forceinline__ D ai_choices(PyBits<AheadStream<1>>& ai, Key key, int n, bool& err) {
+  D draws = 0;
+  int cnt = 0;
+  uint32_t rej = 0;
+#pragma unroll 1
+  while (cnt < n) {
+    const uint32_t seg = ai.s.next(key) & 0x3FFFFFFFu;
+#pragma unroll
+    for (int f = 0; f < 10; ++f) {
+      const uint32_t v = (seg >> (3 * f)) & 7u;
+      const bool active = cnt < n, acc = v < 5u;
+      const uint32_t rj = acc ? 0u : rej + 1u;
+      const bool give = !acc && rj >= kWordCap;
+      const bool take = active && (acc || give);
+      draws |= take ? (D)(acc ? v : 0u) << (3 * cnt) : (D)0;
+      err |= active && give;
+      rej = take ? 0u : (active ? rj : rej);
+      cnt += take ? 1 : 0;
+    }
+  }
+  return draws;
+}
+
+// Keyed mode's Fisher-Yates draws of random.shuffle over n entries:
+// randbelow(i + 1) for i = n-1 .. 1 from the shuffle source (the tick
+// block's reservoir, then one word per draw), one draw per trip of a single
+// per-lane loop, branch-free but for the rare word past the two blocks drawn
+// ahead.  Returns draw j of position i at bits 4 i.
+__device__ __forceinline__ uint64_t shuffle_draws(PyBits<AheadStream<2>>& sh, Key key, int n,
+                                                  bool& err) {
+  uint64_t js = 0;
+  int i = n - 1;
+  uint32_t rej = 0, res = sh.res, wi = sh.s.i;
+  int32_t nb = sh.nb;
+  const W4 w0 = sh.s.w0, w1 = sh.s.w1;
+#pragma unroll 1
+  while (i >= 1) {
+    const uint32_t bound = (uint32_t)i + 1u;
+    const int kb = 32 - __clz(bound);
+    const bool take_res = nb >= kb;
+    const W4 h = (wi & 4u) ? w1 : w0;
+    const uint32_t j3 = wi & 3u;
+    uint32_t w = j3 == 0 ? h.a : j3 == 1 ? h.b : j3 == 2 ? h.c : h.d;
+    if (!take_res && wi >= 8u) w = sh.s.s.next(key);  // past the blocks drawn ahead (rare)
+    const uint32_t r = take_res ? (res & ((1u << kb) - 1u)) : (w >> (32 - kb));
+    res = take_res ? (res >> kb) : res;
+    nb = take_res ? nb - kb : 0;
+    wi += take_res ? 0u : 1u;
+    const bool acc = r < bound;
+    const uint32_t rj = acc ? 0u : rej + 1u;
+    const bool give = !acc && rj >= kWordCap;
+    err |= give;
+    js |= (acc || give) ? (uint64_t)(acc ? r : 0u) << (4 * i) : 0ull;
+    rej = (acc || give) ? 0u : rj;
+    i -= (acc || give) ? 1 : 0;
+  }
+  return js;
+}
+
 // The tick's NPC updents (updater.py:116-128): each NPC's decided move (by
 // slot), the shuffled order (position j -> slot) and which have acted.
 // Register NPCs: packed in 64-bit registers (4-bit slots, 3-bit moves, runtime
@@ -2230,19 +2297,23 @@ __device__ __forceinline__ void tick_moving_body(const Cfg& c, Key key, Src& src
         // The loop only collects the accepted draws (3 bits each, in alive
         // order); the moves follow in an unrolled pass over the slots, where
         // slot k's draw is the one at its rank among the alive slots.
-        int j = 0;
-        uint32_t tries = 0;
         uint64_t draws = 0;
+        if constexpr (std::is_same_v<BitsA, PyBits<AheadStream<1>>>) {
+          draws = ai_choices<std::conditional_t<(NCAP <= 10), uint32_t, uint64_t>>(ai, key, n, err);
+        } else {  // stock-seed mode: a word of the game's CPython random per draw
+          int j = 0;
+          uint32_t tries = 0;
 #pragma unroll 1
-        while (j < n) {
-          const uint32_t r = ai.bits(3, key);
-          const bool acc = r < 5u;
-          const bool give_up = !acc && ++tries >= kWordCap;
-          if (acc || give_up) {
-            err |= give_up;
-            draws |= (uint64_t)(acc ? r : 0u) << (3 * j);
-            ++j;
-            tries = 0;
+          while (j < n) {
+            const uint32_t r = ai.bits(3, key);
+            const bool acc = r < 5u;
+            const bool give_up = !acc && ++tries >= kWordCap;
+            if (acc || give_up) {
+              err |= give_up;
+              draws |= (uint64_t)(acc ? r : 0u) << (3 * j);
+              ++j;
+              tries = 0;
+            }
           }
         }
 #pragma unroll
@@ -2288,20 +2359,24 @@ __device__ __forceinline__ void tick_moving_body(const Cfg& c, Key key, Src& src
     } else if constexpr (NCAP > 0) {
       // register NPCs: the loop collects each position's accepted draw (4
       // bits at 4 i), the swaps follow unrolled, in the shuffle's order
-      int i = n - 1;
-      uint32_t tries = 0;
       uint64_t js = 0;
+      if constexpr (std::is_same_v<BitsS, PyBits<AheadStream<2>>>) {
+        js = shuffle_draws(sh, key, n, err);
+      } else {  // stock-seed mode
+        int i = n - 1;
+        uint32_t tries = 0;
 #pragma unroll 1
-      while (i >= 1) {
-        const uint32_t bound = (uint32_t)i + 1u;
-        const uint32_t r = sh.bits(32 - __clz(bound), key);
-        const bool acc = r < bound;
-        const bool give_up = !acc && ++tries >= kWordCap;
-        if (acc || give_up) {
-          err |= give_up;
-          js |= (uint64_t)(acc ? r : 0u) << (4 * i);
-          --i;
-          tries = 0;
+        while (i >= 1) {
+          const uint32_t bound = (uint32_t)i + 1u;
+          const uint32_t r = sh.bits(32 - __clz(bound), key);
+          const bool acc = r < bound;
+          const bool give_up = !acc && ++tries >= kWordCap;
+          if (acc || give_up) {
+            err |= give_up;
+            js |= (uint64_t)(acc ? r : 0u) << (4 * i);
+            --i;
+            tries = 0;
+          }
         }
       }
 #pragma unroll
