@@ -1970,33 +1970,41 @@ __device__ __forceinline__ D ai_choices(PyBits<AheadStream<1>>& ai, Key key, int
 // block's reservoir, then one word per draw), one draw per trip of a single
 // per-lane loop, branch-free but for the rare word past the two blocks drawn
 // ahead.  Returns draw j of position i at bits 4 i.
-__device__ __forceinline__ uint64_t shuffle_draws(PyBits<AheadStream<2>>& sh, Key key, int n,
-                                                  bool& err) {
-  uint64_t js = 0;
+template <class J>
+__device__ __forceinline__ J shuffle_draws(PyBits<AheadStream<2>>& sh, Key key, int n, bool& err) {
+  J js = 0;
   int i = n - 1;
   uint32_t rej = 0, res = sh.res, wi = sh.s.i;
   int32_t nb = sh.nb;
-  const W4 w0 = sh.s.w0, w1 = sh.s.w1;
+  // the words drawn ahead as a queue: q0 is word wi; a trip that takes a
+  // word shifts it (eight selects, no branch)
+  uint32_t q0 = sh.s.w0.a, q1 = sh.s.w0.b, q2 = sh.s.w0.c, q3 = sh.s.w0.d;
+  uint32_t q4 = sh.s.w1.a, q5 = sh.s.w1.b, q6 = sh.s.w1.c, q7 = sh.s.w1.d;
+  for (uint32_t k = 0; k < wi; ++k) {  // (words the initiative draw took: none in practice)
+    q0 = q1; q1 = q2; q2 = q3; q3 = q4; q4 = q5; q5 = q6; q6 = q7;
+  }
 #pragma unroll 1
   while (i >= 1) {
     const uint32_t bound = (uint32_t)i + 1u;
     const int kb = 32 - __clz(bound);
     const bool take_res = nb >= kb;
-    const W4 h = (wi & 4u) ? w1 : w0;
-    const uint32_t j3 = wi & 3u;
-    uint32_t w = j3 == 0 ? h.a : j3 == 1 ? h.b : j3 == 2 ? h.c : h.d;
+    uint32_t w = q0;
     if (!take_res && wi >= 8u) w = sh.s.s.next(key);  // past the blocks drawn ahead (rare)
     const uint32_t r = take_res ? (res & ((1u << kb) - 1u)) : (w >> (32 - kb));
     res = take_res ? (res >> kb) : res;
     nb = take_res ? nb - kb : 0;
     wi += take_res ? 0u : 1u;
+    q0 = take_res ? q0 : q1; q1 = take_res ? q1 : q2; q2 = take_res ? q2 : q3;
+    q3 = take_res ? q3 : q4; q4 = take_res ? q4 : q5; q5 = take_res ? q5 : q6;
+    q6 = take_res ? q6 : q7;
     const bool acc = r < bound;
     const uint32_t rj = acc ? 0u : rej + 1u;
     const bool give = !acc && rj >= kWordCap;
+    const bool step = acc || give;
     err |= give;
-    js |= (acc || give) ? (uint64_t)(acc ? r : 0u) << (4 * i) : 0ull;
-    rej = (acc || give) ? 0u : rj;
-    i -= (acc || give) ? 1 : 0;
+    js |= step ? (J)(acc ? r : 0u) << (4 * i) : (J)0;
+    rej = step ? 0u : rj;
+    i -= step ? 1 : 0;
   }
   return js;
 }
@@ -2361,7 +2369,7 @@ __device__ __forceinline__ void tick_moving_body(const Cfg& c, Key key, Src& src
       // bits at 4 i), the swaps follow unrolled, in the shuffle's order
       uint64_t js = 0;
       if constexpr (std::is_same_v<BitsS, PyBits<AheadStream<2>>>) {
-        js = shuffle_draws(sh, key, n, err);
+        js = shuffle_draws<std::conditional_t<(NCAP <= 8), uint32_t, uint64_t>>(sh, key, n, err);
       } else {  // stock-seed mode
         int i = n - 1;
         uint32_t tries = 0;
