@@ -126,6 +126,25 @@ def physical_cores() -> int:
     return os.cpu_count() or 1
 
 
+def cpu_quota():
+    """CPUs this job's cgroup may use at once (cgroup v2 cpu.max, v1
+    cfs_quota_us / cfs_period_us), or None when it sets no limit."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        return None if q == "max" else int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = int(f.read())
+        return None if q <= 0 else q / per
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(cfg_dict: dict, seconds: float) -> dict:
     """The C oracle (scalar port of the reference updater) on the host cores
     (the reference's own Python updater, timed in the build container, rides
@@ -232,8 +251,9 @@ def cpu_baseline(cfg_dict: dict, seconds: float) -> dict:
         pyr_all.pop("lscpu", None)
     except (subprocess.SubprocessError, ValueError, IndexError) as e:
         pyr_all = {"error": repr(e)}
+    quota = cpu_quota()
     whole = {"physical_cores": phys, "cpus_visible": os.cpu_count(), "cpus_in_affinity": avail,
-             "cores_used": n_all, "host": _cpu_model(),
+             "cgroup_cpu_quota": quota, "cores_used": n_all, "host": _cpu_model(),
              "port": {"value": tot_all / el_all, "unit": "env-steps/s", "cores": n_all,
                       "per_core": tot_all / el_all / n_all,
                       "sample": f"{n_all} threads x 256 games for {el_all:.1f} s "
@@ -241,7 +261,11 @@ def cpu_baseline(cfg_dict: dict, seconds: float) -> dict:
              "python_restatement": pyr_all,
              "note": "every physical core of the host this job may run on (lscpu: unique "
                      "(core, socket) pairs, capped by the process's CPU affinity); the "
-                     "top-level value is the per-GPU share of 16 threads"}
+                     "top-level value is the per-GPU share of 16 threads"
+                     + ("" if quota is None else
+                        f"; this job's cgroup allows {quota:g} CPUs at once, so these threads "
+                        "time-share them and the whole-host figure is bounded by the quota, "
+                        "not by the cores")}
     return {"value": total / el, "unit": "env-steps/s", "cores": cores, "kind": "port",
             "whole_host": whole,
             "python_restatement": pyr,
