@@ -2,7 +2,8 @@
 oracle on configurations drawn from the whole orx_cfg_t space at once
 (grid shape, despawn rule, start mode and depths, max_ticks, NPC count in the
 register and dense forms, combat attributes, dungeon bank, stock seeding,
-every build-extension flag, games per rollout wave), so feature combinations
+every build-extension flag, moving NPCs, games per rollout wave), so feature
+combinations
 no hand-written case names are exercised too.
 
 Each configuration runs twice against the oracle from the same reset:
@@ -99,6 +100,12 @@ def _draw(case: int, base: int = None):
                item_slots=int(rs.randint(0, 4)), combat_cooldown=int(rs.randint(0, 4)))
     if W <= 256 and H <= 256 and rs.rand() < 0.2:
         cfg["rng"] = 1
+    # moving NPCs (round 6): the enemy AI on about a third of the configurations
+    # it supports (NPCs, flags within separation damage and double death),
+    # drawn from a stream of its own so the other draws stay as they were
+    mv = np.random.RandomState(((BASE if base is None else base) + case) ^ 0x5EED)
+    if K > 0 and not (flags & ~3) and mv.rand() < 0.35:
+        cfg["npc_policy"] = int(mv.choice([1, 2]))
     B = int(rs.choice([1, 63, 257, 1000, 1531]))
     T = int(rs.randint(40, 161))
     pol = (int(rs.choice([1, 1, 2, 2, 3])), int(rs.choice([1, 1, 2, 2, 3])))
@@ -130,8 +137,9 @@ def test_draws_are_valid_and_varied(oracle_lib):
         seen |= {"stock"} if cfg.get("rng") else set()
         seen |= {f"flag{f}" for f in (1, 2, MANA, HEAL, LEVEL, ITEMS, README) if cfg["flags"] & f}
         seen |= {"plain"} if not cfg["flags"] else set()
+        seen |= {f"moving{cfg['npc_policy']}"} if cfg.get("npc_policy") else set()
     want = {"bank", "dense", "npcs", "separated", "stock", "plain", "flag1", "flag2",
-            "flag4", "flag16", "flag32", "flag64"}
+            "flag4", "flag16", "flag32", "flag64", "moving1", "moving2"}
     assert want <= seen, want - seen
 
 
