@@ -31,6 +31,7 @@ def main():
     # dungeon bank; c3_rpg: C3 with the character mechanics
     cname = os.environ.get("STAMPS_CFG", "c3")
     pol = 2 if cname.startswith("c5") else 1
+    pol2 = 2 if cname == "c3_mixed" else pol   # c3_mixed: RandomBot vs StaircaseBot on C3
     if cname == "bank":
         from optimax_rogue_amd import DungeonBank
         cfg = EnvConfig(width=64, height=64, n_npcs=8,
@@ -39,22 +40,26 @@ def main():
         from optimax_rogue_amd.enums import EXT_RPG
         cfg = EnvConfig(width=64, height=64, n_npcs=8, flags=EXT_RPG)
     else:
-        cfg = EnvConfig.c5() if cname == "c5sep" else getattr(EnvConfig, cname)()
+        cfg = EnvConfig.c5() if cname == "c5sep" else \
+            EnvConfig.c3() if cname == "c3_mixed" else getattr(EnvConfig, cname)()
     if cname == "c5sep":
         from optimax_rogue_amd.enums import EXT_SEPARATION_DAMAGE
         cfg.flags, cfg.sep_period = EXT_SEPARATION_DAMAGE, 8
     e = BatchedEngine(cfg, B, seed=1, device=dev)
+    # STAMPS_CONC: plan the launch as one of that many sharing the device (a
+    # stream shard's shape, e.g. C5 131,072 as two 65,536-game shards)
+    e.concurrency = int(os.environ.get("STAMPS_CONC", "1"))
     obs = torch.empty((T, 14, B), dtype=torch.int32, device=dev)
     act = torch.empty((T, B, 2), dtype=torch.int8, device=dev)
     for _ in range(4):
-        e.rollout(T, pol, pol, obs=obs, act=act)
+        e.rollout(T, pol, pol2, obs=obs, act=act)
     torch.cuda.synchronize()
     s, f = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
-    e.rollout(T, pol, pol, obs=obs, act=act)
+    e.rollout(T, pol, pol2, obs=obs, act=act)
     f.record()
     torch.cuda.synchronize()
-    shape = e.rollout_shape(pol, pol)
+    shape = e.rollout_shape(pol, pol2)
     W = -(-B // shape["games_per_wave"])   # the launch's waves (paired: two lanes per game)
     buf = np.zeros(W * 16, dtype=np.uint64)
     dl = ctypes.CDLL(lib)
