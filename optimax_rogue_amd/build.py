@@ -46,6 +46,7 @@ VARIANTS = {
     "envw6": ("ORX_ENV_WAVES=6",),    # ... to 6
     "envd1": ("ORX_ENV_DIAG=1",),     # orx_env_step without its tick (outputs of the loaded state)
     "envd2": ("ORX_ENV_DIAG=2",),     # orx_env_step without its observation rows
+    "routl": ("ORX_RARE_OUTLINE=1",),  # the paired fallback rare tick out of line (rejected)
 }
 
 

@@ -3979,6 +3979,29 @@ struct PairWriter {
 // grid's edge blocks, ANY staircase tile makes the tick rare; descends and
 // resets take rare_tick's bank forms (the closed-form fast paths are for
 // empty dungeons).
+// The paired rollout's fallback rare tick, out of line (-DORX_RARE_OUTLINE=1,
+// build variant `routl`; measured and rejected): its state goes through a
+// stack frame on the (rare) call, so the common tick and the lean rare
+// branches would not carry the merges of an inlined rare_tick's values.  The
+// call makes the kernel take the callee's registers (196-248 VGPRs, two
+// waves per SIMD) and 464-788 B of scratch per lane, and every paired form
+// slows by a third or more (C3 85 -> 110 us, c3_mixed 155 -> 243, C5's share
+// 64 -> 102; profiles/r06_v7/ab_rare_outline_rejected.jsonl).
+#ifndef ORX_RARE_OUTLINE
+#define ORX_RARE_OUTLINE 0
+#endif
+template <int NCAP, bool GRID, class M>
+__device__ __noinline__ bool rare_tick_ool(const Cfg c, const orx_state_t st, uint32_t B,
+                                           uint32_t i, Key key, uint32_t game, uint32_t& ep,
+                                           Player& p1, Player& p2, Npcs<NCAP>& npc,
+                                           Items<NCAP>& items, M& hp, int32_t& tick,
+                                           int32_t& status, Deltas& dl, int32_t& sep,
+                                           bool& restarted, const W4 tb, int need, int32_t t1x,
+                                           int32_t t1y, int32_t t2x, int32_t t2y) {
+  return rare_tick<NCAP, GRID>(c, st, B, i, key, game, ep, p1, p2, npc, items, hp, tick, status,
+                               dl, sep, restarted, tb, need, t1x, t1y, t2x, t2y, false);
+}
+
 template <int NCAP, int PM, int AUX, bool SEP, bool CF = false, bool GRID = false>
 __global__ void __launch_bounds__(GRID ? 512 : kRolloutBlock) ORX_PAIR_ATTR
     __attribute__((amdgpu_waves_per_eu(ORX_SEP_WAVES && PM == 2 && SEP ? 4 : 1)))
@@ -4597,10 +4620,35 @@ __global__ void __launch_bounds__(GRID ? 512 : kRolloutBlock) ORX_PAIR_ATTR
           o.nitems = pair_swap(me.nitems);
         }
         Player p1 = pick(isB, o, me), p2 = pick(isB, me, o);
-        took_ordered = rare_tick<NCAP, GRID>(c, st, B, i, key, game, ep, p1, p2, npc, items, hp,
-                                          tick, status, dl, sep, restarted, tb, need,
-                                          isB ? otx : tx, isB ? oty : ty, isB ? tx : otx,
-                                          isB ? ty : oty, false);
+        if constexpr (ORX_RARE_OUTLINE != 0) {
+          // the call's copies: only they live in the frame
+          uint32_t q_ep = ep;
+          Npcs<NCAP> q_npc = npc;
+          Items<NCAP> q_items = items;
+          auto q_hp = hp;
+          int32_t q_tick = tick, q_status = status, q_sep = sep;
+          Deltas q_dl = dl;
+          bool q_restarted = restarted;
+          took_ordered = rare_tick_ool<NCAP, GRID>(c, st, B, i, key, game, q_ep, p1, p2, q_npc,
+                                                   q_items, q_hp, q_tick, q_status, q_dl, q_sep,
+                                                   q_restarted, tb, need, isB ? otx : tx,
+                                                   isB ? oty : ty, isB ? tx : otx,
+                                                   isB ? ty : oty);
+          ep = q_ep;
+          npc = q_npc;
+          items = q_items;
+          hp = q_hp;
+          tick = q_tick;
+          status = q_status;
+          sep = q_sep;
+          dl = q_dl;
+          restarted = q_restarted;
+        } else {
+          took_ordered = rare_tick<NCAP, GRID>(c, st, B, i, key, game, ep, p1, p2, npc, items, hp,
+                                            tick, status, dl, sep, restarted, tb, need,
+                                            isB ? otx : tx, isB ? oty : ty, isB ? tx : otx,
+                                            isB ? ty : oty, false);
+        }
         me = pick(isB, p2, p1);
         me.move = move;
       }
