@@ -2044,6 +2044,34 @@ struct NpcTurns<kDense> {
   __device__ __forceinline__ void mark(int k) { acted_[k >> 5] |= 1u << (k & 31); }
 };
 
+// Register NPCs (moves decided): true iff no mover's target is a live NPC's
+// cell or another mover's target -- then the NPCs' handle_move calls commute
+// (updater.py:133-134: a move to a free cell, a hit on a player, or a
+// staircase death), whatever order the shuffle gives.  Dead slots hold
+// 0xFFFF, which no interior target equals.
+template <int NCAP>
+__device__ __forceinline__ bool npc_moves_commute(const Cfg& c, const Npcs<NCAP>& npc,
+                                                  const NpcTurns<NCAP>& turns) {
+  uint32_t t[NCAP > 0 ? NCAP : 1];
+  bool clash = false;
+#pragma unroll
+  for (int k = 0; k < NCAP; ++k) {
+    const int32_t mv = turns.move(k);
+    const bool mover = k < c.K && npc.is_alive(k) && mv != ORX_MOVE_STAY;
+    const uint32_t cell = npc.get(k);
+    int32_t tx, ty;
+    calc_pos((int32_t)(cell & 0xFFu), (int32_t)(cell >> 8), mv, tx, ty);
+    const uint32_t tk = pack_xy(tx, ty);
+    t[k] = mover ? tk : 0x10000u + (uint32_t)k;  // (distinct non-cells for the others)
+    clash = clash || (mover && npc.any(tk));
+  }
+#pragma unroll
+  for (int k = 1; k < NCAP; ++k)
+#pragma unroll
+    for (int j = 0; j < k; ++j) clash = clash || t[j] == t[k];
+  return !clash;
+}
+
 // The dungeon of the NPCs' depth nd (player 1's start depth) at the start of
 // the tick: a player's, when one stands on nd; else, under Unreachable with
 // player 2 still above nd (player 1 started on nd and has left it), its
@@ -2368,8 +2396,19 @@ __device__ __forceinline__ void tick_moving_body(const Cfg& c, Key key, Src& src
       // register NPCs: the loop collects each position's accepted draw (4
       // bits at 4 i), the swaps follow unrolled, in the shuffle's order
       uint64_t js = 0;
+      bool shuffled = true;
       if constexpr (std::is_same_v<BitsS, PyBits<AheadStream<2>>>) {
-        js = shuffle_draws<std::conditional_t<(NCAP <= 8), uint32_t, uint64_t>>(sh, key, n, err);
+        // keyed mode without an event list: where no mover's target is an
+        // NPC's cell or another mover's target, the NPCs' handle_move calls
+        // commute (each is a move to a free cell, a hit on a player -- the
+        // players moved first -- or a staircase death), so their order is
+        // unobservable and its draws are skipped (the SHUFFLE stream is the
+        // tick's own: nothing later reads it).  Only games whose NPCs
+        // interact run the Fisher-Yates draws.
+        shuffled = EV || !npc_moves_commute<NCAP>(c, npc, turns);
+        if (shuffled)
+          js = shuffle_draws<std::conditional_t<(NCAP <= 8), uint32_t, uint64_t>>(sh, key, n,
+                                                                                 err);
       } else {  // stock-seed mode
         int i = n - 1;
         uint32_t tries = 0;
@@ -2389,7 +2428,7 @@ __device__ __forceinline__ void tick_moving_body(const Cfg& c, Key key, Src& src
       }
 #pragma unroll
       for (int ii = NCAP - 1; ii >= 1; --ii) {
-        if (ii < n) {
+        if (shuffled && ii < n) {
           const int jj = (int)((js >> (4 * ii)) & 15ull);
           const int si = turns.slot(ii), sj = turns.slot(jj);
           turns.set_slot(ii, sj);
