@@ -622,7 +622,8 @@ def test_bench_c5_share_stream_shards_vs_oracle(sep, oracle_lib):
     -- pair_rollout_kernel<0, 2, 0, SEP> at 8 games per wave -- for 9
     back-to-back 128-tick launches (fork, launches, join), separation damage
     off (reference semantics) and on; sampled games replayed on the oracle
-    tick by tick (staircasebot.py:9-21, updater.py:76-162)."""
+    tick by tick, and every game's state after every launch against a
+    threaded oracle over the batch (staircasebot.py:9-21, updater.py:76-162)."""
     import torch
     from optimax_rogue_amd import EnvConfig
     from optimax_rogue_amd.engine import StreamShardedEngine
@@ -640,7 +641,7 @@ def test_bench_c5_share_stream_shards_vs_oracle(sep, oracle_lib):
     launch = eng.rollout_launcher(T, 2, 2, obs=obs, act=act)
     starts = _window_starts(B, 8192, 6, 17)
     snap, gids = _timed_form_vs_oracle(oracle_lib, eng, eng.parts, obs, act, launch, cfg,
-                                       (2, 2), seed, T, L, starts)
+                                       (2, 2), seed, T, L, starts, whole=True)
     assert (snap["ep_count"][gids] >= 1).all()
     assert snap["counters"][1][gids].sum() > 100   # the StaircaseBots went deep
 
@@ -688,7 +689,9 @@ def test_bench_sharded_extras_vs_oracle(name, oracle_lib):
     256-thread workgroups, the bank's 65,536 B LDS stage -- the staging loop's
     boundary), then 9 launches of 128 ticks with >= 64 sampled games (8-game
     windows incl. both ends of each shard) replayed on the oracle: every
-    tick's observation row, both actions and the state after each launch
+    tick's observation row, both actions and the state after each launch --
+    and every game's state after each launch against a threaded oracle over
+    the whole batch
     (worldgen.py:9-26, world.py:41-66 for the bank; readme.md:44-48,69-74 for
     the character mechanics, parity unpinned; staircasebot.py:9-21)."""
     import torch
@@ -705,13 +708,39 @@ def test_bench_sharded_extras_vs_oracle(name, oracle_lib):
     launch = eng.rollout_launcher(T, *pol, obs=obs, act=act)
     starts = _window_starts(B, B // streams, 6, 13)
     snap, gids = _timed_form_vs_oracle(oracle_lib, eng, eng.parts, obs, act, launch, cfg, pol,
-                                       seed, T, L, starts)
+                                       seed, T, L, starts, whole=True)
     assert len(gids) >= 64
     assert (snap["ep_count"][gids] >= 1).all()
     if which.startswith("c5"):
         assert snap["counters"][1][gids].sum() > 100   # the StaircaseBots went deep
     else:
         assert snap["counters"][0][gids].sum() > 0     # combats happened
+
+
+@pytest.mark.parametrize("npc_policy", [1, 2])
+def test_bench_moving_extras_vs_oracle(npc_policy, oracle_lib):
+    """bench.py's c3_moving_npcs / c3_chasing_npcs extras as they are timed
+    (rollout_rate: C3 with npc_policy RANDOM / CHASE, 65,536 games, seed 5,
+    2x RandomBot, one stream, int32 rows + actions; mov_rollout_kernel), for
+    3 back-to-back 128-tick launches: every game's state after each launch
+    against a threaded oracle over the batch, and 8-game windows replayed
+    tick by tick (every observation row and action pair) -- the reference's
+    decide_npc_move override and the NPC resolution it drives
+    (updater.py:116-145, 165-178)."""
+    import torch
+    from optimax_rogue_amd import EnvConfig
+    from optimax_rogue_amd.engine import BatchedEngine
+    from optimax_rogue_amd.enums import OBS_FIELDS
+    cfg = EnvConfig(width=64, height=64, n_npcs=8, npc_policy=npc_policy)
+    B, T, L, seed = 65536, 128, 3, 5
+    eng = BatchedEngine(cfg, B, seed=seed, device=torch.device("cuda", 0))
+    obs = torch.empty((T, len(OBS_FIELDS), B), dtype=torch.int32, device=eng.device)
+    act = torch.empty((T, B, 2), dtype=torch.int8, device=eng.device)
+    launch = eng.rollout_launcher(T, 1, 1, obs=obs, act=act)
+    starts = _window_starts(B, B, 6, 29)
+    snap, gids = _timed_form_vs_oracle(oracle_lib, eng, [eng], [obs], [act], launch, cfg, (1, 1),
+                                       seed, T, L, starts, whole=True)
+    assert snap["counters"][0].sum() > 0 and snap["counters"][3].sum() > 0  # combats, NPC deaths
 
 
 # round 5: banks above the default 64 KiB of LDS stay paired with the tiles
