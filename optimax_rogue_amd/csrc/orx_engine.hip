@@ -2988,7 +2988,7 @@ env_step_kernel(
     int32_t pol2, int8_t* __restrict__ act, int32_t* __restrict__ obs, float* __restrict__ reward,
     uint8_t* __restrict__ done, int32_t* __restrict__ status_out, uint32_t* __restrict__ bad_count,
     uint32_t B, Key key, uint32_t off, int32_t lds_rows, uint32_t lanes) {
-  __shared__ int32_t rows_lds[256 * ORX_OBS_FIELDS];
+  __shared__ __attribute__((aligned(16))) int32_t rows_lds[256 * ORX_OBS_FIELDS];
   // `lanes` games per wave (64, or 32: two half-full waves per SIMD at the
   // config batch, whose state loads then overlap the other wave's tick); a
   // workgroup's games are contiguous, its row in LDS is the game's index in it
@@ -3029,10 +3029,10 @@ env_step_kernel(
                                            tick, after, p1.sx, p1.sy, p2.sx, p2.sy};
       if constexpr ((ORX_ENV_DIAG & 2) != 0) {  // diagnostic: no observation rows
         if (row[0] == -12345) obs[i] = row[1];   // (keeps the row's values live)
-      } else if (lds_rows) {  // (uniform)
+      } else if (lds_rows) {  // (uniform) seven 8-byte LDS writes (a row is 56 B)
+        int2* r2 = reinterpret_cast<int2*>(rows_lds + gi * ORX_OBS_FIELDS);
 #pragma unroll
-        for (int f = 0; f < ORX_OBS_FIELDS; ++f)
-          rows_lds[gi * ORX_OBS_FIELDS + f] = row[f];
+        for (int f = 0; f < ORX_OBS_FIELDS / 2; ++f) r2[f] = make_int2(row[2 * f], row[2 * f + 1]);
       } else {
 #pragma unroll
         for (int f = 0; f < ORX_OBS_FIELDS; ++f) obs[(size_t)i * ORX_OBS_FIELDS + f] = row[f];
@@ -3062,11 +3062,18 @@ env_step_kernel(
     const uint32_t g0 = blockIdx.x * per_block;
     const uint32_t n = (g0 < B ? min(B - g0, per_block) : 0u) * ORX_OBS_FIELDS;
     int32_t* base = obs + (size_t)g0 * ORX_OBS_FIELDS;
+    // 16-byte stores (a full block's run is 896 of them; its base is
+    // 14,336 B-aligned), the run's last n % 4 words one by one
+    const uint32_t n4 = n >> 2;
+    const int4* src4 = reinterpret_cast<const int4*>(rows_lds);
+    int4* dst4 = reinterpret_cast<int4*>(base);
 #pragma unroll
-    for (int k = 0; k < ORX_OBS_FIELDS; ++k) {
+    for (int k = 0; k < (256 * ORX_OBS_FIELDS / 4 + 255) / 256; ++k) {
       const uint32_t j = (uint32_t)k * blockDim.x + threadIdx.x;
-      if (j < n) base[j] = rows_lds[j];
+      if (j < n4) dst4[j] = src4[j];
     }
+    const uint32_t jt = (n4 << 2) + threadIdx.x;
+    if (jt < n) base[jt] = rows_lds[jt];
   }
   if (bad_count) {  // uniform (idle lanes: bad false)
     const uint64_t m = __builtin_amdgcn_ballot_w64(bad);
@@ -6357,9 +6364,11 @@ int orx_env_step_ex(const orx_cfg_t* cfg, const orx_state_t* st, const void* act
   const Key k = make_key(seed);
   const int nc = ncap_for(cfg->n_npcs);
   const bool grid = cfg->n_layouts > 0;
-  // the rows through LDS (env ORX_ENV_DIRECT_ROWS=1: direct stores, for measurements)
+  // the rows through LDS and 16-byte stores when obs is 16-byte aligned (a
+  // torch allocation is; a view may not be: then direct stores), env
+  // ORX_ENV_DIRECT_ROWS=1: direct stores, for measurements
   const char* dr = getenv("ORX_ENV_DIRECT_ROWS");
-  const int32_t lds_rows = (dr && dr[0] == '1') ? 0 : 1;
+  const int32_t lds_rows = ((dr && dr[0] == '1') || ((uintptr_t)obs & 15u) != 0) ? 0 : 1;
   // games per wave: 64, or 32 where that still leaves at most two waves per
   // SIMD (env ORX_ENV_LANES = 64 / 32 overrides, for measurements)
   const char* le = getenv("ORX_ENV_LANES");
