@@ -1965,6 +1965,40 @@ __device__ __forceinline__ D ai_choices(PyBits<AheadStream<1>>& ai, Key key, int
   return draws;
 }
 
+// ai_choices for at most 8 NPCs from the first three words alone, without a
+// loop: each segment's ten acceptance bits by bit slicing (a field v = b2 b1
+// b0 is rejected iff b2 & (b1 | b0)), then NPC j's value is the field at the
+// lowest acceptance bit left.  Returns false (nothing consumed: ai_choices
+// then runs from word 0) when the 30 fields hold fewer than n accepted ones
+// (p ~ 1e-5 per game-tick at n = 8).
+__device__ __forceinline__ bool ai_choices8(const PyBits<AheadStream<1>>& ai, int n,
+                                            uint32_t& draws) {
+  constexpr uint32_t M = 0x09249249u;  // bit 3f of each of the ten fields
+  const uint32_t s0 = ai.s.w0.a & 0x3FFFFFFFu, s1 = ai.s.w0.b & 0x3FFFFFFFu,
+                 s2 = ai.s.w0.c & 0x3FFFFFFFu;
+  auto acc = [](uint32_t sg) {
+    const uint32_t b0 = sg & M, b1 = (sg >> 1) & M, b2 = (sg >> 2) & M;
+    return ~(b2 & (b1 | b0)) & M;
+  };
+  uint32_t m0 = acc(s0), m1 = acc(s1), m2 = acc(s2);
+  if (__popc(m0) + __popc(m1) + __popc(m2) < n) return false;
+  uint32_t d = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const bool h0 = m0 != 0u, h1 = m1 != 0u;
+    const uint32_t mm = h0 ? m0 : h1 ? m1 : m2;
+    const uint32_t ss = h0 ? s0 : h1 ? s1 : s2;
+    const uint32_t v = (ss >> __builtin_ctz(mm | 0x80000000u)) & 7u;
+    const bool take = j < n;
+    d |= take ? v << (3 * j) : 0u;
+    m0 = (take && h0) ? (m0 & (m0 - 1u)) : m0;
+    m1 = (take && !h0 && h1) ? (m1 & (m1 - 1u)) : m1;
+    m2 = (take && !h0 && !h1) ? (m2 & (m2 - 1u)) : m2;
+  }
+  draws = d;
+  return true;
+}
+
 // Keyed mode's Fisher-Yates draws of random.shuffle over n entries:
 // randbelow(i + 1) for i = n-1 .. 1 from the shuffle source (the tick
 // block's reservoir, then one word per draw), one draw per trip of a single
@@ -2334,7 +2368,11 @@ __device__ __forceinline__ void tick_moving_body(const Cfg& c, Key key, Src& src
         // order); the moves follow in an unrolled pass over the slots, where
         // slot k's draw is the one at its rank among the alive slots.
         uint64_t draws = 0;
-        if constexpr (std::is_same_v<BitsA, PyBits<AheadStream<1>>>) {
+        if constexpr (std::is_same_v<BitsA, PyBits<AheadStream<1>>> && NCAP <= 8) {
+          uint32_t d8 = 0;
+          if (ai_choices8(ai, n, d8)) draws = d8;
+          else draws = ai_choices<uint32_t>(ai, key, n, err);
+        } else if constexpr (std::is_same_v<BitsA, PyBits<AheadStream<1>>>) {
           draws = ai_choices<std::conditional_t<(NCAP <= 10), uint32_t, uint64_t>>(ai, key, n, err);
         } else {  // stock-seed mode: a word of the game's CPython random per draw
           int j = 0;
