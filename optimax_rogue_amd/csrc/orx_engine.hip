@@ -2286,6 +2286,34 @@ __device__ __forceinline__ void mov_npc(const Cfg& c, int k, int32_t mv, Player&
   ev.emit(ORX_EV_POSITION, 3 + k, nd, (tx & 0xFFFF) | (ty << 16));
 }
 
+// mov_npc where the tick's NPC moves commute (npc_moves_commute): the
+// target holds no NPC, so the move is a hit on a player (Block or Ambush:
+// the players acted first), a staircase death or a free step; no event list
+template <int NCAP, bool GRID>
+__device__ __forceinline__ void mov_npc_free(const Cfg& c, int k, int32_t mv, Player& p1,
+                                             Player& p2, Npcs<NCAP>& npc, const NpcDepth& d,
+                                             Deltas& dl) {
+  const uint32_t k0 = npc.get(k);
+  int32_t tx, ty;
+  calc_pos((int32_t)(k0 & 0xFFu), (int32_t)(k0 >> 8), mv, tx, ty);
+  const int32_t nd = c.d1, dmg = c.npc_dmg_net;
+  const bool on1 = p1.d == nd && p1.x == tx && p1.y == ty;
+  const bool on2 = p2.d == nd && p2.x == tx && p2.y == ty;
+  if (on1 || on2) {
+    if (dmg > 0) {
+      if (on1) p1.hp -= dmg;
+      else p2.hp -= dmg;
+    }
+    dl.combat += 1;
+  } else if (npc_stair<GRID>(c, d, tx, ty)) {  // handle_descend: the NPC dies
+    npc.mark_dead(k);
+    npc.kill(k);
+    dl.npc_death += 1;
+  } else {
+    npc.set(k, pack_xy(tx, ty));
+  }
+}
+
 // The death sweep over every NPC (updater.py:136-145: GameState.entities
 // backwards, i.e. descending slots), any of which may have been hit
 template <int NCAP, bool EV, class M>
@@ -2336,6 +2364,7 @@ __device__ __forceinline__ void tick_moving_body(const Cfg& c, Key key, Src& src
   NpcTurns<NCAP> turns;
   turns.clear();
   int n = 0;
+  bool order_free = false;  // this game's NPC moves commute (keyed mode, no event list)
   NpcDepth d{false, -1, -1, -1};
   if constexpr (NCAP > 0) {
     d = npc_depth<GRID>(c, key, src, game, ep, p1, p2, err);
@@ -2444,6 +2473,7 @@ __device__ __forceinline__ void tick_moving_body(const Cfg& c, Key key, Src& src
         // tick's own: nothing later reads it).  Only games whose NPCs
         // interact run the Fisher-Yates draws.
         shuffled = EV || !npc_moves_commute<NCAP>(c, npc, turns);
+        order_free = !shuffled;
         if (shuffled)
           js = shuffle_draws<std::conditional_t<(NCAP <= 8), uint32_t, uint64_t>>(sh, key, n,
                                                                                  err);
@@ -2491,12 +2521,29 @@ __device__ __forceinline__ void tick_moving_body(const Cfg& c, Key key, Src& src
   ORX_MCYC_END(3, cy3);
   ORX_MCYC_BEGIN(cy4);
   if constexpr (NCAP > 0) {
+    // a wave whose every game's NPC moves commute takes them per slot,
+    // unrolled (constant slot indices, no occupant scan); otherwise the
+    // shuffled order, as the reference
+    bool done = false;
+    if constexpr (NCAP != kDense && !EV) {
+      if (__builtin_amdgcn_ballot_w64(!order_free) == 0ull) {
+#pragma unroll
+        for (int k = 0; k < NCAP; ++k) {
+          const int32_t mv = turns.move(k);
+          if (k < c.K && npc.is_alive(k) && mv != ORX_MOVE_STAY)
+            mov_npc_free<NCAP, GRID>(c, k, mv, p1, p2, npc, d, dl);
+        }
+        done = true;
+      }
+    }
+    if (!done) {
 #pragma unroll 1
-    for (int j = 0; j < n; ++j) {
-      const int k = turns.slot(j);
-      const int32_t mv = turns.move(k);
-      if (mv != ORX_MOVE_STAY) mov_npc<NCAP, EV, GRID>(c, k, mv, p1, p2, npc, turns, d, m, dl, ev);
-      turns.mark(k);
+      for (int j = 0; j < n; ++j) {
+        const int k = turns.slot(j);
+        const int32_t mv = turns.move(k);
+        if (mv != ORX_MOVE_STAY) mov_npc<NCAP, EV, GRID>(c, k, mv, p1, p2, npc, turns, d, m, dl, ev);
+        turns.mark(k);
+      }
     }
     ORX_MCYC_END(4, cy4);
     npc_sweep(c, npc, m, dl, ev);                       // :136-145
