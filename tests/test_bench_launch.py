@@ -93,3 +93,16 @@ def test_more_gpus_than_visible_refused():
         pytest.skip("enough GPUs visible")
     r = _run(["--gpus", "2", "--launch-check"])
     assert r.returncode != 0 and "GPU(s) visible" in r.stderr
+
+
+def test_cpu_quota_and_physical_cores():
+    """The whole-host CPU baseline's host facts: the physical core count (lscpu
+    (core, socket) pairs) is positive and at most the visible CPUs, and the
+    cgroup CPU quota is either absent (None) or a positive CPU count."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    phys = bench.physical_cores()
+    assert 1 <= phys <= (os.cpu_count() or phys)
+    q = bench.cpu_quota()
+    assert q is None or q > 0
