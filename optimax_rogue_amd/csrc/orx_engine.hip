@@ -5931,14 +5931,14 @@ int lanes_override() {  // read per launch, so a sweep can change it in-process
   return (x >= 1 && x <= 64 && (x & (x - 1)) == 0) ? x : 0;
 }
 
-// Games per wave of mov_rollout_kernel (env ORX_MOV_LANES = 1..64, a power
-// of two, overrides, for measurements)
-uint32_t mov_lanes(uint32_t B) {
+// Games per wave of mov_rollout_kernel: 64 (its tick is issue-bound, so
+// fewer games per wave only add waves: 32 / 16 / 8 measured equal or slower,
+// profiles/r06_v4/ab_mov_lanes_regs.jsonl); env ORX_MOV_LANES = 1..64, a
+// power of two, overrides, for measurements and tests
+uint32_t mov_lanes() {
   const char* e = getenv("ORX_MOV_LANES");
   const int x = e ? atoi(e) : 0;
-  if (x >= 1 && x <= 64 && (x & (x - 1)) == 0) return (uint32_t)x;
-  (void)B;
-  return 64u;
+  return (x >= 1 && x <= 64 && (x & (x - 1)) == 0) ? (uint32_t)x : 64u;
 }
 
 // Threads per rollout workgroup: kRolloutBlock (env ORX_ROLLOUT_THREADS = 64
@@ -6109,7 +6109,7 @@ int orx_rollout_shape(const orx_cfg_t* cfg, int32_t policy_p1, int32_t policy_p2
   out->threads_per_block = kBlock;
   out->lds_bytes = 0;
   if (moving_npcs(cfg)) {  // mov_rollout_kernel: one game per lane, mov_lanes per wave
-    out->games_per_wave = (int32_t)mov_lanes(B);
+    out->games_per_wave = (int32_t)mov_lanes();
     out->lanes_per_game = 1;
     out->nontemporal = 1;
     return ORX_OK;
@@ -6526,7 +6526,7 @@ int orx_rollout_ex(const orx_cfg_t* cfg, const orx_state_t* st, int32_t policy_p
   const int nc = ncap_for(cfg->n_npcs);
   if (moving_npcs(cfg)) {  // the ordered tick with the enemy AI, one lane per game
     const bool mt = cfg->rng == ORX_RNG_MT19937;
-    const uint32_t lanes = mov_lanes(B);
+    const uint32_t lanes = mov_lanes();
     const uint64_t threads = (((uint64_t)B + lanes - 1) / lanes) * 64u;
     const dim3 g((unsigned)((threads + kBlock - 1) / kBlock));
 #define ORX_ROLLOUT(N, G, M)                                                                    \
