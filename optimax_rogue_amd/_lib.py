@@ -31,6 +31,19 @@ class OrxRolloutShape(ctypes.Structure):
                                                 "threads_per_block", "lds_bytes")]
 
 
+class OrxEnvStepArgs(ctypes.Structure):
+    """ctypes mirror of orx_env_step_args_t (orx_env_step_ex's arguments in
+    one block: VecEnv.step updates a prebuilt block and passes one pointer)."""
+    _fields_ = [("cfg", ctypes.POINTER(OrxCfg)), ("st", ctypes.POINTER(OrxState)),
+                ("actions", ctypes.c_void_p), ("action_bytes", ctypes.c_int32),
+                ("action_cols", ctypes.c_int32), ("policy_p2", ctypes.c_int32),
+                ("pad0", ctypes.c_int32), ("act", ctypes.c_void_p), ("obs", ctypes.c_void_p),
+                ("reward", ctypes.c_void_p), ("done", ctypes.c_void_p),
+                ("status", ctypes.c_void_p), ("bad_actions", ctypes.c_void_p),
+                ("n_games", ctypes.c_int64), ("seed", ctypes.c_uint64),
+                ("game_offset", ctypes.c_int64), ("stream", ctypes.c_void_p)]
+
+
 class OrxError(RuntimeError):
     def __init__(self, fn: str, code: int, msg: str):
         super().__init__(f"{fn} returned {code}: {msg}")
@@ -44,7 +57,7 @@ EXPORTS = ("orx_abi_version", "orx_last_error", "orx_validate_cfg", "orx_reset",
            "orx_dungeon_spawn", "orx_seed_mt", "orx_build_id", "orx_rollout_lanes", "orx_dstore_depths",
            "orx_rollout_shape", "orx_rollout_concurrent", "orx_env_step",
            "orx_rollout_ex", "orx_env_step_ex", "orx_step_n", "orx_max_events",
-           "orx_step_n_ex")
+           "orx_step_n_ex", "orx_env_step_args")
 
 
 def load() -> ctypes.CDLL:
@@ -107,6 +120,9 @@ def load() -> ctypes.CDLL:
         L.orx_env_step_ex.restype = ctypes.c_int
         L.orx_env_step_ex.argtypes = [P(OrxCfg), P(OrxState), vp, i32, i32, i32, vp, vp, vp, vp,
                                       vp, vp, i64, u64, i64, vp]
+    if hasattr(L, "orx_env_step_args"):
+        L.orx_env_step_args.restype = ctypes.c_int
+        L.orx_env_step_args.argtypes = [P(OrxEnvStepArgs)]
     if hasattr(L, "orx_step_n"):
         L.orx_step_n.restype = ctypes.c_int
         L.orx_step_n.argtypes = [P(OrxCfg), P(OrxState), vp, i32, vp, i32, i64, u64, i64, vp]

@@ -6422,6 +6422,13 @@ int orx_env_step(const orx_cfg_t* cfg, const orx_state_t* st, const void* action
                          done, status, nullptr, n_games, seed, game_offset, stream);
 }
 
+int orx_env_step_args(const orx_env_step_args_t* a) {
+  if (!a) return fail(ORX_EINVAL, "args is NULL");
+  return orx_env_step_ex(a->cfg, a->st, a->actions, a->action_bytes, a->action_cols,
+                         a->policy_p2, a->act, a->obs, a->reward, a->done, a->status,
+                         a->bad_actions, a->n_games, a->seed, a->game_offset, a->stream);
+}
+
 int orx_env_step_ex(const orx_cfg_t* cfg, const orx_state_t* st, const void* actions,
                     int32_t action_bytes, int32_t action_cols, int32_t policy_p2, int8_t* act,
                     int32_t* obs, float* reward, uint8_t* done, int32_t* status,

@@ -379,6 +379,44 @@ class BatchedEngine:
                 check("orx_env_step_ex", code)
         return launch
 
+    def env_step_slot(self, p2: int, obs: torch.Tensor, reward: torch.Tensor,
+                      done: torch.Tensor, status: torch.Tensor,
+                      bad_actions: Optional[torch.Tensor] = None):
+        """A callable ``launch(actions_ptr, nb, cols)`` -- orx_env_step_args over
+        one prebuilt argument block for this output set (VecEnv.step's ring of
+        preallocated outputs: per call the actions pointer, the current stream
+        and whatever changed since the last call are written into the block,
+        and ctypes passes one pointer).  The caller has checked the tensors."""
+        a = _lib.OrxEnvStepArgs()
+        a.cfg = ctypes.pointer(self._ccfg)
+        a.st = ctypes.pointer(self._st)
+        a.policy_p2 = int(p2)
+        a.act = self.actions.data_ptr()
+        a.obs, a.reward, a.done, a.status = (obs.data_ptr(), reward.data_ptr(), done.data_ptr(),
+                                             status.data_ptr())
+        a.bad_actions = None if bad_actions is None else bad_actions.data_ptr()
+        a.n_games = self.B
+        fn, check, ref = self.lib.orx_env_step_args, _lib.check, ctypes.byref(a)
+        stream = _raw_stream_getter(self.device)
+        eng = self
+        last = [None, None, None, None]   # nb, cols, seed, game_offset in the block
+
+        def launch(a_ptr, nb, cols):
+            a.actions = a_ptr
+            if nb != last[0] or cols != last[1]:
+                a.action_bytes, a.action_cols = nb, cols
+                last[0], last[1] = nb, cols
+            # seed and game_offset read per call, as step / rollout read them
+            if eng.seed != last[2] or eng.game_offset != last[3]:
+                a.seed, a.game_offset = eng.seed, eng.game_offset
+                last[2], last[3] = eng.seed, eng.game_offset
+            a.stream = stream()
+            code = fn(ref)
+            if code:
+                check("orx_env_step_args", code)
+        launch.args = a   # (keeps the block alive with the callable)
+        return launch
+
     def policy(self, p1: int = Policy.Random, p2: int = Policy.Random,
                out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """RandomBot / StaircaseBot moves for both players into ``out``."""

@@ -102,7 +102,7 @@ class VecEnv:
         self.warnings_seen = 0
         self._steps = 0
         self._ring = [self._alloc_out() for _ in range(self.out_buffers)]
-        self._ring_ptrs = [tuple(t.data_ptr() for t in out) for out in self._ring]
+        self._ring_launch = [None] * len(self._ring)   # their prebuilt launches (first use)
         self._slot = 0
         self._launch = None   # the pre-bound orx_env_step_ex, made at the first step
 
@@ -230,7 +230,11 @@ class VecEnv:
             k = self._slot
             out = self._ring[k]
             self._slot = (k + 1) % len(self._ring)
-            self._launch(a.data_ptr(), nb, len(shape), *self._ring_ptrs[k], bad)
+            go = self._ring_launch[k]
+            if go is None:   # one prebuilt argument block per output set
+                go = self._ring_launch[k] = self.engine.env_step_slot(
+                    self._p2, *out, self._bad_dev if deferred else None)
+            go(a.data_ptr(), nb, len(shape))
         else:
             out = self._alloc_out()
             obs, reward, done, status = out

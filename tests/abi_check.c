@@ -63,9 +63,26 @@ int main(void) {
   }
   c.npc_policy = ORX_NPC_STAY;
   if (orx_max_events(&c) != ORX_MAX_EVENTS) { printf("event bound wrong\n"); return 19; }
+  /* ABI 7: orx_env_step_ex's arguments as one block */
+  {
+    orx_env_step_args_t ea;
+    memset(&ea, 0, sizeof ea);
+    ea.cfg = &c;
+    ea.action_bytes = 8;
+    ea.action_cols = 1;
+    ea.policy_p2 = ORX_POLICY_RANDOM;
+    ea.seed = 1;
+    if (orx_env_step_args(&ea) != ORX_OK) { printf("empty env step args failed\n"); return 21; }
+    ea.policy_p2 = ORX_POLICY_NONE;
+    ea.n_games = 16;
+    if (orx_env_step_args(&ea) != ORX_EINVAL) { printf("env step args unchecked\n"); return 22; }
+    if (orx_env_step_args(NULL) != ORX_EINVAL) { printf("NULL env step args accepted\n"); return 23; }
+  }
   c.n_npcs = 8;
-  printf("sizeof(orx_cfg_t)=%zu sizeof(orx_state_t)=%zu off_flags=%zu off_npc_alive=%zu\n",
+  printf("sizeof(orx_cfg_t)=%zu sizeof(orx_state_t)=%zu off_flags=%zu off_npc_alive=%zu "
+         "sizeof(orx_env_step_args_t)=%zu off_stream=%zu\n",
          sizeof(orx_cfg_t), sizeof(orx_state_t), offsetof(orx_cfg_t, flags),
-         offsetof(orx_state_t, npc_alive));
+         offsetof(orx_state_t, npc_alive), sizeof(orx_env_step_args_t),
+         offsetof(orx_env_step_args_t, stream));
   return 0;
 }

@@ -39,7 +39,7 @@ def test_library_exports_every_declared_symbol(lib):
                            "orx_build_id", "orx_rollout_lanes", "orx_dstore_depths",
                            "orx_rollout_shape", "orx_rollout_concurrent", "orx_env_step",
                            "orx_rollout_ex", "orx_env_step_ex", "orx_step_n", "orx_max_events",
-                           "orx_step_n_ex"])
+                           "orx_step_n_ex", "orx_env_step_args"])
     from optimax_rogue_amd import _lib
     assert sorted(_lib.EXPORTS) == decl
     for name in decl:
@@ -192,6 +192,10 @@ def test_plain_c_consumer(lib, tmp_path):
     r = subprocess.run([str(exe)], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "sizeof(orx_cfg_t)=116" in r.stdout
+    # the ctypes mirror of orx_env_step_args_t matches the C layout
+    from optimax_rogue_amd._lib import OrxEnvStepArgs
+    assert f"sizeof(orx_env_step_args_t)={ctypes.sizeof(OrxEnvStepArgs)}" in r.stdout
+    assert f"off_stream={OrxEnvStepArgs.stream.offset}" in r.stdout
 
 
 def test_engine_refuses_cpu():
