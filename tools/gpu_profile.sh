@@ -24,9 +24,15 @@ python3 $R/tools/ktrace_summary.py $f > $O/kernel_trace_summary.txt
 KNAME=$(python3 -c "import json,sys; print(json.load(open(sys.argv[1]))['roofline']['kernel'])" $O/bench.json)
 python3 $R/tools/ktrace_summary.py --span $f "$KNAME" 65536 2 >> $O/kernel_trace_summary.txt
 cp $(find $O/trace -name "run_kernel_stats.csv" | head -1) $O/kernel_stats.csv
+# the PMC passes need only the headline's dispatches (make_traffic.py reads
+# those): without the extras and the CPU baseline, so a pass stays short
+# (the extras' thousands of small dispatches under counter collection can
+# run minutes without output)
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $O/fetch -o pmc --output-format csv \
-  -- python3 $R/bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_under_fetch.json 2> $O/fetch.err
+  -- python3 $R/bench.py --gpus 1 --steps 20 --warmup 5 --no-extras --no-cpu-baseline \
+  > $O/bench_under_fetch.json 2> $O/fetch.err
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d $O/write -o pmc --output-format csv \
-  -- python3 $R/bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_under_write.json 2> $O/write.err
+  -- python3 $R/bench.py --gpus 1 --steps 20 --warmup 5 --no-extras --no-cpu-baseline \
+  > $O/bench_under_write.json 2> $O/write.err
 python3 $R/tools/make_traffic.py $O/fetch $O/write $O/traffic.json > /dev/null
 cat $O/traffic.json | tail -16
