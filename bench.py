@@ -372,10 +372,11 @@ def extras(torch, cfg, dev, B_cfg, K, large_rollout=False):
                           "graph_us_per_tick": gel * 1e6,
                           "note": "VecEnv.step called eagerly from Python (int64 learner actions "
                                   "+ RandomBot opponent -> obs, reward, done, status): one "
-                                  "orx_env_step_ex launch per tick, no host sync; us_per_tick "
-                                  "with fresh output tensors, ring_us_per_tick with "
-                                  "out_buffers=2; graph_us_per_tick: 50 calls captured in one "
-                                  "HIP graph"}
+                                  "learner-tick launch per tick (env_step_kernel), no host "
+                                  "sync; us_per_tick with fresh output tensors "
+                                  "(orx_env_step_ex), ring_us_per_tick with out_buffers=2 (one "
+                                  "prebuilt orx_env_step_args block per output set); "
+                                  "graph_us_per_tick: 50 calls captured in one HIP graph"}
     del env, pool, gv
     torch.cuda.empty_cache()
     # (1c) a replay: orx_step_n over a 128-tick move log (int8 [128, B, 2],
