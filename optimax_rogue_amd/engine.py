@@ -382,11 +382,13 @@ class BatchedEngine:
     def env_step_slot(self, p2: int, obs: torch.Tensor, reward: torch.Tensor,
                       done: torch.Tensor, status: torch.Tensor,
                       bad_actions: Optional[torch.Tensor] = None):
-        """A callable ``launch(actions_ptr, nb, cols)`` -- orx_env_step_args over
-        one prebuilt argument block for this output set (VecEnv.step's ring of
-        preallocated outputs: per call the actions pointer, the current stream
-        and whatever changed since the last call are written into the block,
-        and ctypes passes one pointer).  The caller has checked the tensors."""
+        """A callable ``launch(actions_ptr, nb, cols, outs=None)`` --
+        orx_env_step_args over one prebuilt argument block for this output set
+        (VecEnv.step's ring of preallocated outputs: per call the actions
+        pointer, the current stream and whatever changed since the last call
+        are written into the block, and ctypes passes one pointer; ``outs``,
+        four data pointers, redirects the block to fresh outputs).  The caller
+        has checked the tensors."""
         a = _lib.OrxEnvStepArgs()
         a.cfg = ctypes.pointer(self._ccfg)
         a.st = ctypes.pointer(self._st)
@@ -401,7 +403,9 @@ class BatchedEngine:
         eng = self
         last = [None, None, None, None]   # nb, cols, seed, game_offset in the block
 
-        def launch(a_ptr, nb, cols):
+        def launch(a_ptr, nb, cols, outs=None):
+            if outs is not None:   # (fresh outputs: their four pointers this call)
+                a.obs, a.reward, a.done, a.status = outs
             a.actions = a_ptr
             if nb != last[0] or cols != last[1]:
                 a.action_bytes, a.action_cols = nb, cols

@@ -104,7 +104,8 @@ class VecEnv:
         self._ring = [self._alloc_out() for _ in range(self.out_buffers)]
         self._ring_launch = [None] * len(self._ring)   # their prebuilt launches (first use)
         self._slot = 0
-        self._launch = None   # the pre-bound orx_env_step_ex, made at the first step
+        self._stock = None   # stock-seed mode (orx_policy + orx_step per tick)
+        self._fresh_launch = None   # the argument-block launch for fresh outputs
 
     def _alloc_out(self):
         d = self.device
@@ -216,10 +217,10 @@ class VecEnv:
             if bool(((a < 1) | (a > hi)).any()):
                 raise ValueError(f"actions must be Move values 1..{hi} (an argmax over logits is "
                                  "0-based: add 1)")
-        if self._launch is None:
-            if getattr(self.engine, "mt_py", None) is not None:   # stock-seed mode
-                return self._step_stock(a)
-            self._launch = self.engine.env_step_launcher(self._p2)
+        if self._stock is None:   # (decided at the first step)
+            self._stock = getattr(self.engine, "mt_py", None) is not None
+        if self._stock:   # stock-seed mode
+            return self._step_stock(a)
         deferred = self._bad_host is not None
         bad = self._bad_ptr if deferred else None
         if deferred:   # (before the launch: a call that raises plays no tick)
@@ -238,8 +239,12 @@ class VecEnv:
         else:
             out = self._alloc_out()
             obs, reward, done, status = out
-            self._launch(a.data_ptr(), nb, len(shape), obs.data_ptr(), reward.data_ptr(),
-                         done.data_ptr(), status.data_ptr(), bad)
+            if self._fresh_launch is None:   # one argument block, its outputs set per call
+                self._fresh_launch = self.engine.env_step_slot(
+                    self._p2, *out, self._bad_dev if deferred else None)
+            self._fresh_launch(a.data_ptr(), nb, len(shape),
+                               (obs.data_ptr(), reward.data_ptr(), done.data_ptr(),
+                                status.data_ptr()))
         return out
 
     def _step_stock(self, a: torch.Tensor):

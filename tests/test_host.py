@@ -117,7 +117,8 @@ def test_engine_refuses_snapshots_off_the_grid():
 @pytest.mark.parametrize("ring", [0, 2])
 def test_vecenv_step_passes_bad_actions_to_the_engine(bad, ring):
     """check_actions=False: no host check and no sync -- the learner's tensor
-    goes to orx_env_step_ex as it is (its own pointer at full width: 257 is
+    goes to the learner-tick launch (orx_env_step_args) as it is (its own
+    pointer at full width: 257 is
     not cast to int8, where it would wrap to a legal 1); the engine stops
     those games with STATUS_BAD_ACTION and step() reports them done (GPU
     tests: test_vecenv_bad_actions_truncate_on_device).  Status is its own
@@ -131,9 +132,13 @@ def test_vecenv_step_passes_bad_actions_to_the_engine(bad, ring):
     class Eng:
         cfg, mt_py = EnvConfig(), None
 
-        def env_step_launcher(self, p2):
-            def launch(a_ptr, nb, cols, obs, rew, done, status, bad_ptr):
-                calls.append((a_ptr, nb, cols, p2, obs, rew, done, status, bad_ptr))
+        def env_step_slot(self, p2, obs, rew, done, status, bad=None):
+            # (BatchedEngine.env_step_slot: a launch over one argument block)
+            ptrs = (obs.data_ptr(), rew.data_ptr(), done.data_ptr(), status.data_ptr())
+
+            def launch(a_ptr, nb, cols, outs=None):
+                o = ptrs if outs is None else outs
+                calls.append((a_ptr, nb, cols, p2, *o, None if bad is None else bad.data_ptr()))
             return launch
 
     env = VecEnv.__new__(VecEnv)
